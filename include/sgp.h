@@ -1,0 +1,137 @@
+/*
+ * sgp.h -- C ABI of the MI355X-native sparse-GP objective+gradient path.
+ *
+ * Drop-in boundary for luisdamiano/sparseRGPs' native layer and hot path.
+ * Plain C: pointers, sizes and enums only; no torch/HIP types in signatures
+ * (streams are passed as `void*` = hipStream_t).  Matrices use R's layout:
+ * column-major fp64 with an explicit leading dimension.
+ *
+ * Layer 1 (elementwise fillers, host buffers) replaces the Rcpp .Call routines
+ * registered in src/RcppExports.cpp:284-311:
+ *   sgp_make_cov      <- make_cov_matC     src/covariance_functionsC.cpp:72-169
+ *                        make_cov_mat_ardC src/covariance_functionsC.cpp:191-252
+ *   sgp_dsig_dtheta   <- dsig_dthetaC      src/covariance_function_derivativesC.cpp:307-552
+ *                        dsig_dtheta_ardC  src/covariance_function_derivativesC.cpp:555-722
+ *   sgp_kernel_pair / sgp_dkernel_pair <- the per-pair exports cov_fun_*C, dsqexp_*C
+ *                        (covariance_functionsC.cpp:5-52, covariance_function_derivativesC.cpp:35-171)
+ *
+ * Layer 2 (fused evaluation over a device-resident context) replaces the R-level
+ * hot path that calls those routines once per optimizer iteration:
+ *   sgp_eval_vi     <- elbo_fun (R/vi_functions.R:64-121) + delbo_dcov_par (126-602),
+ *                      with K12/K22/Z built as in norm_grad_ascent_vi (vi_functions.R:1089-1128)
+ *   sgp_eval_fitc   <- obj_fun_norm (R/laplace_approx_obj_funs.R:6-52) + dlogp_dcov_par
+ *                      (R/laplace_approx_gradient.R:720-1135), Z as in norm_grad_ascent
+ *                      (R/laplace_gradient_ascent.R:1568-1593)
+ *   sgp_vi_phase1/2, sgp_vi_finish: the same VI evaluation split at its two
+ *                      row-sum reductions so a caller can all-reduce across GPUs.
+ *
+ * Hyperparameters are passed as `theta` laid out [sigma, l_1..l_L, tau] with
+ * L = 1 (sqexp, exp) or L = d (ard).  Gradients are d/d log(theta) in that order
+ * (the reference's trans_par scale, R/laplace_approx_gradient.R:850-853).
+ *
+ * Errors: every entry point returns an sgp_status; sgp_last_error() gives a
+ * thread-local message.  A failed Cholesky returns SGP_ENOTPD (R's chol() error,
+ * caught by try() in R/knot_proposal_functions.R:641-642).
+ */
+#ifndef SGP_H
+#define SGP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SGP_ABI_VERSION 1
+
+typedef enum {
+  SGP_OK = 0,
+  SGP_EINVAL = 1,  /* bad argument: unknown kernel/parameter, size, NULL        */
+  SGP_ENOTPD = 2,  /* Cholesky pivot <= 0 or non-finite; see sgp_last_error()    */
+  SGP_EHIP = 3,    /* HIP runtime failure                                        */
+  SGP_ENOMEM = 4   /* device allocation failed                                   */
+} sgp_status;
+
+typedef enum {
+  SGP_KERNEL_SQEXP = 0, /* "sqexp": sigma^2 exp(-|x-u|^2/(2 l^2))                */
+  SGP_KERNEL_ARD = 1,   /* "ard":   sigma^2 exp(-sum_c ((x_c-u_c)/l_c)^2 / 2)      */
+  SGP_KERNEL_EXP = 2    /* "exp":   sigma^2 exp(-sum_c |x_c-u_c| / l)  (L1)        */
+} sgp_kernel;
+
+/* flags for the fused evaluations */
+#define SGP_FLAG_R_DET 1u /* reproduce R's det() overflow in log(det(K22)) */
+
+const char* sgp_last_error(void);
+int sgp_abi_version(void);
+int sgp_device_count(int* count);
+
+/* number of hyperparameters for a kernel and input dimension d: 3 or d + 2 */
+int sgp_num_params(int kernel, int d);
+
+/* ---------------- Layer 1: elementwise fillers (host in/out) ---------------- */
+
+/* K(x_i, x'_j) for all pairs.  x: n x d (ldx >= n), xp: np x d (ldxp >= np) or NULL for the
+ * symmetric mode (R's x_pred = matrix()), which adds tau^2 + delta on the diagonal.
+ * out: n x np column-major (ldo >= n).  Runs on `device` (HIP). */
+int sgp_make_cov(int device, int kernel, const double* x, int64_t n, int64_t ldx,
+                 const double* xp, int64_t np, int64_t ldxp, int d,
+                 const double* theta, double delta, double* out, int64_t ldo);
+
+/* d K / d log(theta_p) for all pairs; param indexes theta's layout.  Reproduces the
+ * reference's quirks: tau -> 2 tau^2 iff all coordinates equal; "exp" derivatives use the
+ * L2 distance; "exp" cross-mode tau returns zeros. */
+int sgp_dsig_dtheta(int device, int kernel, const double* x, int64_t n, int64_t ldx,
+                    const double* xp, int64_t np, int64_t ldxp, int d,
+                    const double* theta, int param, double* out, int64_t ldo);
+
+/* per-pair scalar forms (host-only, for the R shim's cov_fun_*C / dsqexp_*C exports) */
+double sgp_kernel_pair(int kernel, const double* x1, const double* x2, int d, const double* theta);
+double sgp_dkernel_pair(int kernel, const double* x1, const double* x2, int d,
+                        const double* theta, int param);
+
+/* ---------------- Layer 2: device-resident context + fused evaluation ---------------- */
+
+typedef struct sgp_ctx sgp_ctx;
+
+/* Copy X (n x d, column-major, ldx >= n), y and mu (n) to HBM on `device`; reserve work
+ * space for up to m_max inducing points.  The context owns all device memory; nothing is
+ * allocated per evaluation.  A context is externally synchronized (one host thread). */
+int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_t ldx, int d,
+                   const double* y, const double* mu, int64_t m_max);
+int sgp_ctx_destroy(sgp_ctx* ctx);
+/* launch on this hipStream_t (NULL = the context's own stream) */
+int sgp_ctx_set_stream(sgp_ctx* ctx, void* hip_stream);
+/* replace y / mu (e.g. Laplace pseudo-data); host buffers of length n */
+int sgp_ctx_set_data(sgp_ctx* ctx, const double* y, const double* mu);
+int64_t sgp_ctx_rows(const sgp_ctx* ctx);
+
+/* Titsias ELBO and d ELBO / d log theta at knots U (m x d column-major, ldu >= m).
+ * K22 = Kuu + delta I, Z = tau^2 + delta (vi_functions.R:733-753).  grad: num_params. */
+int sgp_eval_vi(sgp_ctx* ctx, int kernel, const double* theta, const double* U, int64_t m,
+                int64_t ldu, double delta, unsigned flags, double* obj, double* grad);
+
+/* FITC log marginal likelihood and gradient (obj_fun_norm + dlogp_dcov_par). */
+int sgp_eval_fitc(sgp_ctx* ctx, int kernel, const double* theta, const double* U, int64_t m,
+                  int64_t ldu, double delta, unsigned flags, double* obj, double* grad);
+
+/* Multi-GPU VI: each rank owns a row block of X.  phase1 writes its partial first
+ * reduction (sgp_vi_red1_count doubles) to the DEVICE buffer red1; the caller sums red1
+ * over ranks in place (e.g. RCCL all-reduce); phase2 consumes the reduced red1 and writes
+ * its partial second reduction (sgp_vi_red2_count doubles) to red2; after summing red2 over
+ * ranks, sgp_vi_finish returns the objective and gradient.  n_global = total rows. */
+int64_t sgp_vi_red1_count(int64_t m);
+int64_t sgp_vi_red2_count(int kernel, int d);
+int sgp_vi_phase1(sgp_ctx* ctx, int kernel, const double* theta, const double* U, int64_t m,
+                  int64_t ldu, double delta, double* red1);
+int sgp_vi_phase2(sgp_ctx* ctx, const double* red1, int64_t n_global, unsigned flags, double* red2);
+int sgp_vi_finish(sgp_ctx* ctx, const double* red2, double* obj, double* grad);
+
+/* Per-kernel timing of the last evaluation (HIP events on the launch stream).
+ * names: '\n'-separated kernel-phase names; ms: their durations (max n entries). */
+int sgp_ctx_enable_timing(sgp_ctx* ctx, int enable);
+int sgp_ctx_timings(sgp_ctx* ctx, char* names, int64_t names_len, double* ms, int max_n, int* count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SGP_H */

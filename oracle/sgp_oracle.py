@@ -1,0 +1,669 @@
+"""CPU oracle for the sparseRGPs hot path -- TEST INFRASTRUCTURE ONLY.
+
+A literal numpy restatement of the reference R/Rcpp algorithm
+(luisdamiano/sparseRGPs, mounted read-only at /root/reference).  It is the
+*checker* for the MI355X product path in ``sparsergps_amd``: only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+it.  Nothing in the product path calls into this file.
+
+Parity status: the reference ships no tests, no golden vectors and cannot be
+built or run here (R and Rcpp are absent).  This restatement is
+therefore pinned *independently* (tests/test_oracle.py):
+  * central finite differences of its own objectives in log(theta);
+  * a dense n x n formulation (slogdet / direct inverse of Sigma_y);
+  * hand-checked closed forms of the per-pair kernels.
+Relative to the reference itself parity is "unpinned" (no reference outputs exist).
+
+Every function mirrors one reference function, cited file:line.  R semantics
+are reproduced literally where they matter:
+  * ``solve(a, b)``  -> LAPACK gesv (np.linalg.solve), ``solve(a)`` -> inverse;
+  * ``chol(x)``      -> UPPER factor R with t(R) %*% R = x;
+  * ``det(x)``       -> LU determinant (overflows to +/-Inf like R);
+  * ``(1/Z) * M``    -> R recycling of an n-vector down the columns = row scaling;
+  * ``apply(M, 1, sum)`` -> row sums.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import numpy as np
+
+# --------------------------------------------------------------------------------------
+# helpers reproducing base-R linear algebra semantics
+# --------------------------------------------------------------------------------------
+
+
+def r_chol(x):
+    """R ``chol(x)``: upper-triangular R with t(R) %*% R = x (LAPACK dpotrf)."""
+    return np.linalg.cholesky(x).T
+
+
+def r_solve(a, b=None):
+    """R ``solve(a, b)`` (dgesv); ``solve(a)`` is the inverse."""
+    if b is None:
+        return np.linalg.inv(a)
+    return np.linalg.solve(a, b)
+
+
+def r_det(a):
+    """R ``det(a)`` = exp(modulus) * sign from an LU factorisation; overflows like R."""
+    with np.errstate(over="ignore", under="ignore"):
+        return float(np.linalg.det(a))
+
+
+def _as_matrix(x):
+    x = np.asarray(x, dtype=np.float64)
+    if x.ndim == 1:
+        x = x.reshape(-1, 1)
+    return x
+
+
+def _is_sym(x_pred):
+    """Symmetric-mode sentinel: R passes ``matrix()`` (a 1x1 NA); we accept None/NaN."""
+    if x_pred is None:
+        return True
+    xp = np.asarray(x_pred, dtype=np.float64)
+    return xp.size >= 1 and np.isnan(xp.reshape(-1)[0])
+
+
+def _diff(x, xp):
+    """Pairwise coordinate differences x_i - x'_j, shape (n, n', d)."""
+    return x[:, None, :] - xp[None, :, :]
+
+
+# --------------------------------------------------------------------------------------
+# L0: per-pair kernels and matrix fillers (src/covariance_functionsC.cpp)
+# --------------------------------------------------------------------------------------
+
+
+def make_cov_matC(x, x_pred, cov_par, cov_fun, delta):
+    """covariance_functionsC.cpp:72-169.
+
+    sqexp: sigma^2 exp(-1/(2 l^2) sum (x-u)^2)  (l.10)
+    exp:   sigma^2 exp(-1/l sum |x-u|)          (l.50, L1 distance -- quirk Q12)
+    Symmetric mode (x_pred NA, l.81) adds tau^2 + delta on the diagonal (l.91, 133);
+    cross mode adds nothing, even for coincident points (l.111).
+    Invalid cov_fun -> 0x0 matrix (l.161-168).
+    """
+    x = _as_matrix(x)
+    sym = _is_sym(x_pred)
+    xp = x if sym else _as_matrix(x_pred)
+    sigma = float(cov_par["sigma"])
+    if cov_fun == "sqexp":
+        l = float(cov_par["l"])
+        diff = _diff(x, xp)
+        mat = sigma ** 2 * np.exp(-1.0 / (2.0 * l ** 2) * np.sum(diff ** 2, axis=2))
+    elif cov_fun == "exp":
+        l = float(cov_par["l"])
+        diff = _diff(x, xp)
+        mat = sigma ** 2 * np.exp(-1.0 / l * np.sum(np.abs(diff), axis=2))
+    else:
+        return np.zeros((0, 0))
+    if sym:
+        tau = float(cov_par["tau"])
+        mat[np.diag_indices_from(mat)] += tau ** 2 + delta
+    return mat
+
+
+def make_cov_mat_ardC(x, x_pred, cov_par, cov_fun, delta, lnames):
+    """covariance_functionsC.cpp:191-252 with cov_fun_sqrd_exp_ardC 16-42.
+
+    ARD: sigma^2 exp(-sum(((x-u)/l)^2)/2) with l_c = cov_par[lnames[c]] (l.24-28, 40).
+    """
+    if cov_fun != "ard":
+        return np.zeros((0, 0))
+    x = _as_matrix(x)
+    sym = _is_sym(x_pred)
+    xp = x if sym else _as_matrix(x_pred)
+    sigma = float(cov_par["sigma"])
+    l = np.array([float(cov_par[nm]) for nm in lnames])
+    diff = _diff(x, xp)
+    mat = sigma ** 2 * np.exp(-np.sum((diff / l) ** 2, axis=2) / 2.0)
+    if sym:
+        tau = float(cov_par["tau"])
+        mat[np.diag_indices_from(mat)] += tau ** 2 + delta
+    return mat
+
+
+# --------------------------------------------------------------------------------------
+# L0: derivative matrix fillers (src/covariance_function_derivativesC.cpp)
+# --------------------------------------------------------------------------------------
+
+
+def _coincident(x, xp):
+    """``all(x1 == x2)`` per pair (dsqexp_dtauC l.157)."""
+    return np.all(x[:, None, :] == xp[None, :, :], axis=2)
+
+
+def dsig_dthetaC(x, x_pred, cov_par, cov_fun, par_name):
+    """covariance_function_derivativesC.cpp:307-552 (per-pair fns 35-52, 86-104, 142-171, 232-301).
+
+    d K / d log(theta):
+      sigma -> 2 sigma exp(...) sigma                      (l.47)
+      l     -> sigma^2 exp(...) * (1/l^3) sum(d^2) * l      (l.98-99)
+      tau   -> 2 tau^2 iff all(x1 == x2) else 0             (l.157-163)
+    No nugget in symmetric mode except through the tau rule.
+    'exp' derivatives use the L2 distance (quirk Q12, l.244/264) and the cross-mode
+    tau case returns a zero matrix (quirk Q13, l.520).  Unknown names -> 0x0 or zeros
+    exactly as the C++ control flow does.
+    """
+    x = _as_matrix(x)
+    sym = _is_sym(x_pred)
+    xp = x if sym else _as_matrix(x_pred)
+    nrow, ncol = x.shape[0], xp.shape[0]
+    if cov_fun == "sqexp":
+        sigma = float(cov_par["sigma"])
+        if par_name == "sigma":
+            l = float(cov_par["l"])
+            s2 = np.sum(_diff(x, xp) ** 2, axis=2)
+            return 2 * sigma * np.exp(-(1 / (2 * l ** 2)) * s2) * sigma
+        if par_name == "l":
+            l = float(cov_par["l"])
+            s2 = np.sum(_diff(x, xp) ** 2, axis=2)
+            return (sigma ** 2 * np.exp((-1 / (2 * l ** 2)) * s2)) * ((1 / (l ** 3)) * s2) * l
+        if par_name == "tau":
+            tau = float(cov_par["tau"])
+            return np.where(_coincident(x, xp), 2 * tau * tau, 0.0)
+        return np.zeros((0, 0))
+    if cov_fun == "exp":
+        sigma = float(cov_par["sigma"])
+        if par_name == "sigma":
+            l = float(cov_par["l"])
+            dist = np.sqrt(np.sum(_diff(x, xp) ** 2, axis=2))
+            return 2 * sigma * np.exp(-(1 / l) * dist) * sigma
+        if par_name == "l":
+            l = float(cov_par["l"])
+            dist = np.sqrt(np.sum(_diff(x, xp) ** 2, axis=2))
+            return (sigma ** 2 * np.exp((-1 / l) * dist)) * ((1 / (l ** 2)) * dist) * l
+        if sym:
+            if par_name == "tau":
+                tau = float(cov_par["tau"])
+                return np.where(_coincident(x, xp), 2 * tau * tau, 0.0)
+            return np.zeros((0, 0))
+        # cross mode: `return mat;` precedes the tau branch (l.520) -> zeros
+        return np.zeros((nrow, ncol))
+    return np.zeros((0, 0))
+
+
+def dsig_dtheta_ardC(x, x_pred, cov_par, cov_fun, par_name, lnames):
+    """covariance_function_derivativesC.cpp:555-722 (dsqexp_dsigma_ardC 55-83, dsqexp_dl_ardC 107-139).
+
+      sigma -> 2 sigma exp(-sum((d/l)^2)/2) sigma                 (l.78)
+      l_c   -> sigma^2 exp(-sum((d/l)^2)/2) (1/l_c^3) d_c^2 l_c   (l.133-134)
+      tau   -> coincidence rule                                   (l.634)
+    """
+    if cov_fun != "ard":
+        return np.zeros((0, 0))
+    x = _as_matrix(x)
+    sym = _is_sym(x_pred)
+    xp = x if sym else _as_matrix(x_pred)
+    sigma = float(cov_par["sigma"])
+    l = np.array([float(cov_par[nm]) for nm in lnames])
+    if par_name == "sigma":
+        diff = _diff(x, xp)
+        return 2 * sigma * np.exp(-(np.sum((diff / l) ** 2, axis=2) / 2)) * sigma
+    if par_name in list(lnames):
+        c = list(lnames).index(par_name)
+        diff = _diff(x, xp)
+        return (sigma ** 2 * np.exp(-(np.sum((diff / l) ** 2, axis=2) / 2))) * \
+            ((1 / (l[c] ** 3)) * (diff[:, :, c] ** 2)) * l[c]
+    if par_name == "tau":
+        tau = float(cov_par["tau"])
+        return np.where(_coincident(x, xp), 2 * tau * tau, 0.0)
+    return np.zeros((0, 0))
+
+
+# --------------------------------------------------------------------------------------
+# R closures used for the diagonal derivative A1 and the parameter transforms
+# (R/covariance_function_derivatives.R:7-154)
+# --------------------------------------------------------------------------------------
+
+
+def a1_diag(cov_fun, par_name, cov_par, lnames):
+    """Value of dcov_fun_dtheta$<par>(x1 = xy[i,], x2 = xy[i,], transform=TRUE)$derivative.
+
+    dsqexp_dsigma / _ard -> 2 sigma^2 (covariance_function_derivatives.R:24, 63)
+    dsqexp_dl            -> 0           (l.140)
+    dsqexp_dtau          -> 2 tau^2     (l.101)
+    ARD length scales are skipped by the callers (vi_functions.R:326, laplace_approx_gradient.R:908).
+    Returns None when the caller skips the loop (A1 stays numeric(n) zeros).
+    """
+    if cov_fun == "ard" and par_name in lnames:
+        return None
+    if par_name == "sigma":
+        return 2.0 * float(cov_par["sigma"]) ** 2
+    if par_name == "l":
+        return 0.0
+    if par_name == "tau":
+        return 2.0 * float(cov_par["tau"]) ** 2
+    raise KeyError(par_name)
+
+
+def _cov_mats(cov_par, cov_fun, xu, xy, delta, lnames):
+    if cov_fun == "ard":
+        s12 = make_cov_mat_ardC(xy, xu, cov_par, cov_fun, delta, lnames)
+        s22 = make_cov_mat_ardC(xu, None, cov_par, cov_fun, delta, lnames)
+    else:
+        s12 = make_cov_matC(xy, xu, cov_par, cov_fun, delta)
+        s22 = make_cov_matC(xu, None, cov_par, cov_fun, delta)
+    return s12, s22
+
+
+def _dmats(cov_par, cov_fun, xu, xy, par_name, lnames):
+    if cov_fun == "ard":
+        d12 = dsig_dtheta_ardC(xy, xu, cov_par, cov_fun, par_name, lnames)
+        d22 = dsig_dtheta_ardC(xu, None, cov_par, cov_fun, par_name, lnames)
+    else:
+        d12 = dsig_dthetaC(xy, xu, cov_par, cov_fun, par_name)
+        d22 = dsig_dthetaC(xu, None, cov_par, cov_fun, par_name)
+    return d12, d22
+
+
+def lnames_for(cov_fun, d):
+    return [f"l{c + 1}" for c in range(d)] if cov_fun == "ard" else []
+
+
+# --------------------------------------------------------------------------------------
+# L2: Titsias VI objective and gradient (R/vi_functions.R)
+# --------------------------------------------------------------------------------------
+
+
+def trace_term_fun(cov_par, Sigma12, Sigma22, delta):
+    """vi_functions.R:14-27.  Lambda = sigma^2 + delta - rowsum(K12 * t(K22^-1 K21)); / (2 tau^2)."""
+    tau = float(cov_par["tau"])
+    sigma = float(cov_par["sigma"])
+    Z2 = r_solve(Sigma22, Sigma12.T)
+    Z3 = Sigma12 * Z2.T
+    Z4 = Z3.sum(axis=1)
+    Lam = sigma ** 2 + delta - Z4
+    return -(1 / (2 * tau ** 2)) * np.sum(Lam)
+
+
+def elbo_fun(mu, Z, Sigma12, Sigma22, y, cov_par, delta):
+    """vi_functions.R:64-121 (Titsias bound; det() quirk F8 kept)."""
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    mu = np.asarray(mu, dtype=np.float64).reshape(-1)
+    r = y - mu
+    ZSig12 = (1 / Z)[:, None] * Sigma12
+    R = r_chol(Sigma22 + Sigma12.T @ ZSig12)
+    logdetR = 2 * np.sum(np.log(np.diag(R)))
+    v = ZSig12.T @ r
+    quad = -0.5 * (r @ ((1 / Z) * r)) + 0.5 * (v @ r_solve(R, r_solve(R.T, v)))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        det_part = -0.5 * (np.sum(np.log(Z)) - np.log(r_det(Sigma22)) + logdetR)   # l.106 (det() quirk F8)
+    tt = trace_term_fun(cov_par, Sigma12, Sigma22, delta)
+    return float(quad + det_part - (len(y) / 2) * math.log(2 * math.pi) + tt)
+
+
+def vi_mats(cov_par, cov_fun, xu, xy, delta):
+    """Driver construction (vi_functions.R:733-753): K12, K22 = Kuu + delta I, Z = tau^2 + delta."""
+    lnames = lnames_for(cov_fun, np.asarray(xy).shape[1])
+    s12, s22 = _cov_mats(cov_par, cov_fun, xu, xy, delta, lnames)
+    s22 = s22 - float(cov_par["tau"]) ** 2 * np.eye(s22.shape[0])
+    Z = np.full(s12.shape[0], float(cov_par["tau"]) ** 2 + delta)
+    return s12, s22, Z
+
+
+def elbo_eval(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6):
+    """One ELBO evaluation exactly as norm_grad_ascent_vi performs it (vi_functions.R:733-771)."""
+    s12, s22, Z = vi_mats(cov_par, cov_fun, xu, xy, delta)
+    return elbo_fun(mu, Z, s12, s22, y, cov_par, delta)
+
+
+def _gaussian_comps(A, B, C, FF, Sigma12, Sigma22, dS12, dS22, comp2_1):
+    """comp1 (5 pieces) and comp2 shared by delbo_dcov_par / dlogp_dcov_par / dlogq_dcov_par.
+
+    vi_functions.R:377-400; laplace_approx_gradient.R:936-959, 282-300.
+    """
+    BS12 = B[:, None] * Sigma12
+    comp1_1 = np.sum(A * B) - np.trace(C @ Sigma12.T @ ((B * A * B)[:, None] * Sigma12))
+    comp1_2_1 = 2 * np.trace(r_solve(Sigma22, Sigma12.T @ (B[:, None] * dS12)))
+    comp1_2_2 = np.trace(FF @ r_solve(Sigma22, BS12.T).T @ dS22)
+    comp1_2_3 = 2 * np.trace((FF @ BS12) @ (C @ Sigma12.T @ (B[:, None] * dS12)))
+    comp1_2_4 = np.trace((FF @ BS12) @ ((C @ Sigma12.T) @ BS12) @ r_solve(Sigma22, dS22))
+    comp1 = comp1_1 + comp1_2_1 - comp1_2_2 - comp1_2_3 + comp1_2_4
+    s = r_solve(Sigma22, Sigma12.T @ comp2_1)
+    comp2_2 = A * comp2_1 + 2 * dS12 @ s - FF.T @ dS22 @ s
+    comp2 = comp2_1 @ comp2_2
+    return comp1, comp2
+
+
+def delbo_dcov_par(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6):
+    """vi_functions.R:126-602 with dcov_fun_dknot = NA (xu_opt = "fixed").
+
+    Returns {"gradient": OrderedDict(name -> d ELBO / d log theta), "trans_par": OrderedDict}.
+    Order follows names(cov_par) (quirk Q15).
+    """
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    mu = np.asarray(mu, dtype=np.float64).reshape(-1)
+    xy = _as_matrix(xy)
+    xu = _as_matrix(xu)
+    lnames = lnames_for(cov_fun, xy.shape[1])
+    tau = float(cov_par["tau"])
+    Sigma12, Sigma22 = _cov_mats(cov_par, cov_fun, xu, xy, delta, lnames)
+    Sigma22 = Sigma22 - tau ** 2 * np.eye(xu.shape[0])                    # l.199-204
+    FF = r_solve(Sigma22, Sigma12.T)                                       # l.227
+    Z = np.full(Sigma12.shape[0], tau ** 2 + delta)                        # l.229
+    B = 1 / Z
+    R = r_chol(Sigma22 + Sigma12.T @ ((1 / Z)[:, None] * Sigma12))        # l.231
+    C = r_solve(Sigma22 + Sigma12.T @ (B[:, None] * Sigma12))             # l.239
+    ZS = (1 / Z)[:, None] * Sigma12
+    comp2_1 = (1 / Z) * (y - mu) - r_solve(R, r_solve(R.T, ZS.T)).T @ (ZS.T @ (y - mu))  # l.245
+    current_trace_term = trace_term_fun(cov_par, Sigma12, Sigma22, delta)  # l.250
+    grad = OrderedDict()
+    trans_par = OrderedDict()
+    n = xy.shape[0]
+    for par_name in cov_par.keys():
+        trans_par[par_name] = math.log(float(cov_par[par_name]))
+        dS12, dS22 = _dmats(cov_par, cov_fun, xu, xy, par_name, lnames)
+        if par_name == "tau":                                              # l.313-316
+            dS22 = np.zeros((xu.shape[0], xu.shape[0]))
+        if par_name != "tau":                                              # l.322-353
+            a1 = a1_diag(cov_fun, par_name, cov_par, lnames)
+            A1_trace = np.zeros(n) if a1 is None else np.full(n, a1)
+            temp1 = 2 * dS12 - FF.T @ dS22
+            A2_trace = np.sum(temp1 * FF.T, axis=1)
+            A_trace = A1_trace - A2_trace
+        A1 = np.zeros(n)                                                   # l.358-371
+        if par_name == "tau":
+            A1[:] = a1_diag(cov_fun, par_name, cov_par, lnames)
+        A = A1
+        comp1, comp2 = _gaussian_comps(A, B, C, FF, Sigma12, Sigma22, dS12, dS22, comp2_1)
+        if par_name == "tau":
+            dtrace = -2 * current_trace_term                               # l.38-44
+        else:
+            dtrace = -(1 / (2 * tau ** 2)) * np.sum(A_trace)               # l.54-60
+        grad[par_name] = float(0.5 * comp2 - 0.5 * comp1 + dtrace)         # l.416-417
+    return {"gradient": grad, "trans_par": trans_par}
+
+
+def vi_posterior_u(cov_par, cov_fun, xu, xy, y, mu, muu, delta=1e-6):
+    """Posterior of u at the end of norm_grad_ascent_vi (vi_functions.R:1161-1180)."""
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    mu = np.asarray(mu, dtype=np.float64).reshape(-1)
+    Sigma12, Sigma22, Z = vi_mats(cov_par, cov_fun, xu, xy, delta)
+    ZSig12 = (1 / Z)[:, None] * Sigma12
+    R1 = r_chol(Sigma22 + Sigma12.T @ ZSig12)
+    v = ZSig12.T @ (y - mu)
+    u_mean = muu + v - Sigma12.T @ (ZSig12 @ r_solve(R1, r_solve(R1.T, v)))
+    Y = r_solve(R1.T, Sigma12.T)
+    u_var = Sigma22 - Sigma12.T @ ZSig12 + (ZSig12.T @ Y.T @ Y @ ZSig12)
+    return u_mean, u_var
+
+
+# --------------------------------------------------------------------------------------
+# L2: FITC Gaussian objective and gradient
+# --------------------------------------------------------------------------------------
+
+
+def obj_fun_norm(mu, Z, Sigma12, Sigma22, y):
+    """laplace_approx_obj_funs.R:6-52 (FITC log marginal likelihood via Woodbury)."""
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    r = y - np.asarray(mu, dtype=np.float64).reshape(-1)
+    ZSig12 = (1 / Z)[:, None] * Sigma12
+    R = r_chol(Sigma22 + Sigma12.T @ ZSig12)
+    logdetR = 2 * np.sum(np.log(np.diag(R)))
+    v = ZSig12.T @ r
+    quad = -0.5 * (r @ ((1 / Z) * r)) + 0.5 * (v @ r_solve(R, r_solve(R.T, v)))
+    with np.errstate(divide="ignore"):
+        det_part = -0.5 * (np.sum(np.log(Z)) - np.log(r_det(Sigma22)) + logdetR)
+    return float(quad + det_part - (len(y) / 2) * math.log(2 * math.pi))
+
+
+def fitc_mats(cov_par, cov_fun, xu, xy, delta):
+    """norm_grad_ascent driver (laplace_gradient_ascent.R:1238-1263): K22 = Kuu + delta I,
+    Z = sigma^2 + tau^2 + delta - rowsum(K12 * t(K22^-1 K21))."""
+    lnames = lnames_for(cov_fun, np.asarray(xy).shape[1])
+    s12, s22 = _cov_mats(cov_par, cov_fun, xu, xy, delta, lnames)
+    s22 = s22 - float(cov_par["tau"]) ** 2 * np.eye(s22.shape[0])
+    Z2 = r_solve(s22, s12.T)
+    Z4 = np.sum(s12 * Z2.T, axis=1)
+    Z = float(cov_par["sigma"]) ** 2 + float(cov_par["tau"]) ** 2 + delta - Z4
+    return s12, s22, Z
+
+
+def fitc_obj_eval(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6):
+    s12, s22, Z = fitc_mats(cov_par, cov_fun, xu, xy, delta)
+    return obj_fun_norm(mu, Z, s12, s22, y)
+
+
+def dlogp_dcov_par(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6):
+    """laplace_approx_gradient.R:720-971 (FITC gradient, knots fixed)."""
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    mu = np.asarray(mu, dtype=np.float64).reshape(-1)
+    xy = _as_matrix(xy)
+    xu = _as_matrix(xu)
+    lnames = lnames_for(cov_fun, xy.shape[1])
+    tau = float(cov_par["tau"])
+    sigma = float(cov_par["sigma"])
+    Sigma12, Sigma22 = _cov_mats(cov_par, cov_fun, xu, xy, delta, lnames)
+    Sigma22 = Sigma22 - tau ** 2 * np.eye(xu.shape[0])                    # l.792-813
+    FF = r_solve(Sigma22, Sigma12.T)                                       # l.819
+    Z = sigma ** 2 + tau ** 2 + delta - np.sum(Sigma12 * FF.T, axis=1)    # l.820-822
+    B = 1 / Z
+    R = r_chol(Sigma22 + Sigma12.T @ ((1 / Z)[:, None] * Sigma12))
+    C = r_solve(Sigma22 + Sigma12.T @ (B[:, None] * Sigma12))
+    ZS = (1 / Z)[:, None] * Sigma12
+    comp2_1 = (1 / Z) * (y - mu) - r_solve(R, r_solve(R.T, ZS.T)).T @ (ZS.T @ (y - mu))
+    grad = OrderedDict()
+    trans_par = OrderedDict()
+    n = xy.shape[0]
+    for par_name in cov_par.keys():
+        trans_par[par_name] = math.log(float(cov_par[par_name]))
+        dS12, dS22 = _dmats(cov_par, cov_fun, xu, xy, par_name, lnames)
+        if par_name == "tau":                                              # l.899-902
+            dS22 = np.zeros((xu.shape[0], xu.shape[0]))
+        a1 = a1_diag(cov_fun, par_name, cov_par, lnames)                   # l.906-920
+        A1 = np.zeros(n) if a1 is None else np.full(n, a1)
+        temp1 = 2 * dS12 - FF.T @ dS22                                     # l.924-930
+        A2 = np.sum(temp1 * FF.T, axis=1)
+        A = A1 - A2
+        comp1, comp2 = _gaussian_comps(A, B, C, FF, Sigma12, Sigma22, dS12, dS22, comp2_1)
+        grad[par_name] = float(0.5 * comp2 - 0.5 * comp1)                  # l.964-965
+    return {"gradient": grad, "trans_par": trans_par}
+
+
+# --------------------------------------------------------------------------------------
+# L2: Poisson Laplace (sparse FIC) -- newtrap_sparseGP, obj_fun_pois, dlogq_dcov_par
+# --------------------------------------------------------------------------------------
+
+
+def d2log_py_dff_pois(ff, m):
+    """derivative_functions_of_data_likelihoods.R:7-12."""
+    return -m * np.exp(ff)
+
+
+d3log_py_dff_pois = d2log_py_dff_pois  # l.16-21
+
+
+def dlog_py_dff_pois(ff, y, m):
+    """derivative_functions_of_data_likelihoods.R:25-30."""
+    return -m * np.exp(ff) + y
+
+
+def lfactorial(y):
+    from scipy.special import gammaln
+    return gammaln(np.asarray(y, dtype=np.float64) + 1.0)
+
+
+def grad_loglik_fn_pois(ff, y, mu, Sigma12, Sigma22, Z, m):
+    """derivative_functions_of_data_likelihoods.R:34-61."""
+    d1 = -m * np.exp(ff) + y
+    R = r_chol(Sigma22 + Sigma12.T @ ((1 / Z)[:, None] * Sigma12))
+    d2 = -1 / Z * (ff - mu) + ((1 / Z)[:, None] * Sigma12) @ r_solve(R, r_solve(R.T, Sigma12.T @ (1 / Z * (ff - mu))))
+    return d1 + d2
+
+
+def obj_fun_pois(ff, mu, Z, Sigma12, Sigma22, y, m):
+    """laplace_approx_obj_funs.R:108-174 (log q(y | theta, xu, f_hat))."""
+    ff = np.asarray(ff, dtype=np.float64)
+    W = -m * np.exp(ff)
+    Z2 = 1 + np.sqrt(-W) * Z * np.sqrt(-W)
+    log_py = np.sum(y * np.log(m) - lfactorial(y) - m * np.exp(ff) + y * ff)
+    ZSig12 = (1 / Z)[:, None] * Sigma12
+    R = r_chol(Sigma22 + Sigma12.T @ ZSig12)
+    sw = np.sqrt(-W)[:, None] * Sigma12
+    R2 = r_chol(Sigma22 + sw.T @ ((1 / Z2)[:, None] * sw))
+    logdetR2 = 2 * np.sum(np.log(np.diag(R2)))
+    R_Sigma22 = r_chol(Sigma22)
+    v = r_solve(R.T, ZSig12.T @ (ff - mu))
+    quad = -0.5 * ((ff - mu) @ ((1 / Z) * (ff - mu))) + 0.5 * (v @ v)
+    det_part_1 = -0.5 * (-2 * np.sum(np.log(np.diag(R_Sigma22))) + logdetR2)
+    det_part_2 = -0.5 * np.sum(np.log(Z2))
+    return float(quad + log_py + det_part_1 + det_part_2)
+
+
+def newtrap_sparseGP_update(ff, W, Z, Sigma12, Sigma22, grad_psi, y, mu, m):
+    """newtrap_sparseGP.R:234-325."""
+    ZSig12 = (1 / Z)[:, None] * Sigma12
+    R = r_chol(Sigma22 + Sigma12.T @ ZSig12)
+    R3 = r_chol(Sigma22 + Sigma12.T @ (((Z - 1 / W) ** (-1))[:, None] * Sigma12))
+    omzw = 1 - Z * W
+    A11 = (Z / omzw) * dlog_py_dff_pois(ff, y, m)
+    A12 = omzw ** (-1) * (ff - mu)
+    A13 = r_solve(R.T, ((1 / omzw)[:, None] * Sigma12).T).T @ r_solve(R.T, ZSig12.T @ (ff - mu))
+    A2 = r_solve(R3.T, ((omzw ** (-1))[:, None] * Sigma12).T).T @ \
+        r_solve(R3.T, Sigma12.T @ ((1 / omzw) * grad_psi))
+    return ff + (A11 - A12 + A13 + A2)
+
+
+def laplace_mats(cov_par, cov_fun, xu, xy, delta):
+    """newtrap_sparseGP.R:43-66: K22 = Kuu + (tau^2 + delta) I (quirk Q1), Z via LU."""
+    lnames = lnames_for(cov_fun, np.asarray(xy).shape[1])
+    s12, s22 = _cov_mats(cov_par, cov_fun, xu, xy, delta, lnames)
+    Z2 = r_solve(s22, s12.T)
+    Z4 = np.sum(s12 * Z2.T, axis=1)
+    Z = float(cov_par["sigma"]) ** 2 + float(cov_par["tau"]) ** 2 + delta - Z4
+    return s12, s22, Z
+
+
+def newtrap_sparseGP(start_vals, cov_par, cov_fun, xy, xu, y, mu, m, delta=1e-6,
+                     maxit=1000, tol=1e-6):
+    """newtrap_sparseGP.R:6-186 for the Poisson likelihood.
+
+    Returns dict(gp, objective_function_values, gradient, u_posterior_mean/variance needs muu -> omitted).
+    """
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    mu = np.asarray(mu, dtype=np.float64).reshape(-1)
+    Sigma12, Sigma22, Z = laplace_mats(cov_par, cov_fun, xu, xy, delta)
+    ff = np.asarray(start_vals, dtype=np.float64).copy()
+    obj = [obj_fun_pois(ff, mu, Z, Sigma12, Sigma22, y, m)]
+    it = 1
+    it += 1
+    W = d2log_py_dff_pois(ff, m)
+    grad_psi = grad_loglik_fn_pois(ff, y, mu, Sigma12, Sigma22, Z, m)
+    ff = newtrap_sparseGP_update(ff, W, Z, Sigma12, Sigma22, grad_psi, y, mu, m)
+    obj.append(obj_fun_pois(ff, mu, Z, Sigma12, Sigma22, y, m))
+    while it < maxit and (abs(obj[it - 1] - obj[it - 2]) > tol or np.any(np.abs(grad_psi) > tol)):
+        it += 1
+        W = d2log_py_dff_pois(ff, m)
+        grad_psi = grad_loglik_fn_pois(ff, y, mu, Sigma12, Sigma22, Z, m)
+        ff = newtrap_sparseGP_update(ff, W, Z, Sigma12, Sigma22, grad_psi, y, mu, m)
+        obj.append(obj_fun_pois(ff, mu, Z, Sigma12, Sigma22, y, m))
+    return {"gp": ff, "objective_function_values": np.array(obj), "gradient": grad_psi}
+
+
+def dlogq_dcov_par(cov_par, cov_fun, xu, xy, y, ff, mu, m, delta=1e-6):
+    """laplace_approx_gradient.R:25-553 (Poisson sparse Laplace gradient, knots fixed)."""
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    mu = np.asarray(mu, dtype=np.float64).reshape(-1)
+    ff = np.asarray(ff, dtype=np.float64).reshape(-1)
+    xy = _as_matrix(xy)
+    xu = _as_matrix(xu)
+    lnames = lnames_for(cov_fun, xy.shape[1])
+    Sigma12, Sigma22 = _cov_mats(cov_par, cov_fun, xu, xy, delta, lnames)  # l.92-120 (tau^2 kept)
+    FF = r_solve(Sigma22, Sigma12.T)
+    Z = float(cov_par["sigma"]) ** 2 + float(cov_par["tau"]) ** 2 + delta - np.sum(Sigma12 * FF.T, axis=1)
+    W = d2log_py_dff_pois(ff, m)
+    B = 1 / (Z - (1 / W))                                                 # l.133
+    R = r_chol(Sigma22 + Sigma12.T @ ((1 / Z)[:, None] * Sigma12))
+    W3 = d3log_py_dff_pois(ff, m)
+    C = r_solve(Sigma22 + Sigma12.T @ (B[:, None] * Sigma12))
+    ZS = (1 / Z)[:, None] * Sigma12
+    comp2_1 = (1 / Z) * (ff - mu) - r_solve(R, r_solve(R.T, ZS.T)).T @ (ZS.T @ (ff - mu))
+    grad_log_py_ff = dlog_py_dff_pois(ff, y, m)
+    GG = r_solve(Sigma22, Sigma12.T @ grad_log_py_ff)                      # l.155
+    D = W - 1 / Z                                                          # l.161
+    E2 = np.eye(Sigma22.shape[0]) + r_solve(R.T, ZS.T) @ \
+        r_solve(R.T, (((1 / D) * (1 / Z))[:, None] * Sigma12).T).T       # l.164
+    RE2 = r_chol(E2)
+    RE = RE2 @ R
+    REinv = r_solve(RE)
+    coef = (1 / Z) * (1 / D)
+    tm = REinv.T @ (coef[None, :] * Sigma12.T)                            # column i = temp_mat_i (l.171-177)
+    comp4_1 = np.sum(tm * tm, axis=0)
+    comp4 = -(1 / D) + comp4_1
+    grad = OrderedDict()
+    trans_par = OrderedDict()
+    n = xy.shape[0]
+    for par_name in cov_par.keys():
+        trans_par[par_name] = math.log(float(cov_par[par_name]))
+        dS12, dS22 = _dmats(cov_par, cov_fun, xu, xy, par_name, lnames)
+        a1 = a1_diag(cov_fun, par_name, cov_par, lnames)
+        A1 = np.zeros(n) if a1 is None else np.full(n, a1)
+        temp1 = 2 * dS12 - FF.T @ dS22
+        A2 = np.sum(temp1 * FF.T, axis=1)
+        A = A1 - A2
+        comp1, comp2 = _gaussian_comps(A, B, C, FF, Sigma12, Sigma22, dS12, dS22, comp2_1)
+        comp3_1 = A * grad_log_py_ff + 2 * dS12 @ GG - FF.T @ dS22 @ GG       # l.308-310
+        BS12 = B[:, None] * Sigma12
+        comp3 = -(1 / W) * (B * comp3_1) + (1 / W) * (BS12 @ (C @ (Sigma12.T @ (B * comp3_1))))  # l.313-314
+        grad[par_name] = float(0.5 * comp2 - 0.5 * comp1 - 0.5 * ((comp4 * (-W3)) @ comp3))  # l.334-336
+    return {"gradient": grad, "trans_par": trans_par}
+
+
+# --------------------------------------------------------------------------------------
+# Synthetic workloads; numpy PCG64 streams
+# --------------------------------------------------------------------------------------
+
+
+def _rng(seed):
+    return np.random.Generator(np.random.PCG64(seed))
+
+
+def make_gaussian_problem(config, n=None, m=None):
+    """C2 / C3 (and C4 = C3 row-sharded) synthetic Gaussian regression inputs.
+
+    C2: d=3, sqexp, theta=(sigma=1, l=1, tau=0.5); seeds X=2, U=3, y=4.
+    C3: d=8, ARD,   theta=(sigma=1, l1..l8=3, tau=0.5); seeds X=5, U=6, y=7.
+    y = sum_c sin(x_c) [/sqrt(d) for C3] + N(0, 0.5^2); mu = mean(y) (quirk Q14).
+    """
+    if config == "C2":
+        n = n or 100_000
+        m = m or 256
+        d, sx, su, sy = 3, 2, 3, 4
+        X = _rng(sx).uniform(0.0, 10.0, size=(n, d))
+        U = _rng(su).uniform(0.0, 10.0, size=(m, d))
+        y = np.sin(X).sum(axis=1) + _rng(sy).normal(0.0, 0.5, size=n)
+        cov_par = OrderedDict([("sigma", 1.0), ("l", 1.0), ("tau", 0.5)])
+        cov_fun = "sqexp"
+    elif config in ("C3", "C4"):
+        n = n or 1_000_000
+        m = m or 1024
+        d, sx, su, sy = 8, 5, 6, 7
+        X = _rng(sx).uniform(0.0, 10.0, size=(n, d))
+        U = _rng(su).uniform(0.0, 10.0, size=(m, d))
+        y = np.sin(X).sum(axis=1) / math.sqrt(d) + _rng(sy).normal(0.0, 0.5, size=n)
+        cov_par = OrderedDict([("sigma", 1.0)] + [(f"l{c + 1}", 3.0) for c in range(d)] + [("tau", 0.5)])
+        cov_fun = "ard"
+    else:
+        raise ValueError(config)
+    mu = np.full(n, y.mean())
+    return dict(X=X, U=U, y=y, mu=mu, cov_par=cov_par, cov_fun=cov_fun, delta=1e-6)
+
+
+def make_poisson_problem(n=None, m=None):
+    """C5: Poisson Laplace, n=5e5, m=512, d=5, sqexp, theta=(1, 2, 0.1); seeds X=8, U=9, y=10."""
+    n = n or 500_000
+    m = m or 512
+    d = 5
+    X = _rng(8).uniform(0.0, 10.0, size=(n, d))
+    U = _rng(9).uniform(0.0, 10.0, size=(m, d))
+    f = 0.5 * np.sin(X).sum(axis=1) / math.sqrt(d) + math.log(2.0)
+    a = 1.0
+    y = _rng(10).poisson(a * np.exp(f)).astype(np.float64)
+    mu = np.full(n, math.log(y.mean()))
+    f0 = np.full(n, math.log(y.mean()) - math.log(a))
+    cov_par = OrderedDict([("sigma", 1.0), ("l", 2.0), ("tau", 0.1)])
+    return dict(X=X, U=U, y=y, mu=mu, f0=f0, a=a, cov_par=cov_par, cov_fun="sqexp", delta=1e-6)

@@ -1,0 +1,107 @@
+"""ctypes binding of libsgp.so (include/sgp.h).
+
+There is no CPU fallback: if the HIP library is missing or cannot be loaded, every entry
+point raises.  Compute entry points additionally require a visible GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+from ._build import LIB, build
+
+_lock = threading.Lock()
+_lib = None
+
+c_double_p = C.POINTER(C.c_double)
+c_int_p = C.POINTER(C.c_int)
+
+SGP_OK, SGP_EINVAL, SGP_ENOTPD, SGP_EHIP, SGP_ENOMEM = 0, 1, 2, 3, 4
+KERNELS = {"sqexp": 0, "ard": 1, "exp": 2}
+SGP_FLAG_R_DET = 1
+
+# name -> (restype, argtypes); exactly the functions declared in include/sgp.h
+PROTOTYPES = {
+    "sgp_last_error": (C.c_char_p, []),
+    "sgp_abi_version": (C.c_int, []),
+    "sgp_device_count": (C.c_int, [c_int_p]),
+    "sgp_num_params": (C.c_int, [C.c_int, C.c_int]),
+    "sgp_make_cov": (C.c_int, [C.c_int, C.c_int, c_double_p, C.c_int64, C.c_int64, c_double_p,
+                               C.c_int64, C.c_int64, C.c_int, c_double_p, C.c_double, c_double_p,
+                               C.c_int64]),
+    "sgp_dsig_dtheta": (C.c_int, [C.c_int, C.c_int, c_double_p, C.c_int64, C.c_int64, c_double_p,
+                                  C.c_int64, C.c_int64, C.c_int, c_double_p, C.c_int, c_double_p,
+                                  C.c_int64]),
+    "sgp_kernel_pair": (C.c_double, [C.c_int, c_double_p, c_double_p, C.c_int, c_double_p]),
+    "sgp_dkernel_pair": (C.c_double, [C.c_int, c_double_p, c_double_p, C.c_int, c_double_p,
+                                      C.c_int]),
+    "sgp_ctx_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, c_double_p, C.c_int64, C.c_int64,
+                                 C.c_int, c_double_p, c_double_p, C.c_int64]),
+    "sgp_ctx_destroy": (C.c_int, [C.c_void_p]),
+    "sgp_ctx_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "sgp_ctx_set_data": (C.c_int, [C.c_void_p, c_double_p, c_double_p]),
+    "sgp_ctx_rows": (C.c_int64, [C.c_void_p]),
+    "sgp_eval_vi": (C.c_int, [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_int64, C.c_int64,
+                              C.c_double, C.c_uint, c_double_p, c_double_p]),
+    "sgp_eval_fitc": (C.c_int, [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_int64, C.c_int64,
+                                C.c_double, C.c_uint, c_double_p, c_double_p]),
+    "sgp_vi_red1_count": (C.c_int64, [C.c_int64]),
+    "sgp_vi_red2_count": (C.c_int64, [C.c_int, C.c_int]),
+    "sgp_vi_phase1": (C.c_int, [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_int64, C.c_int64,
+                                C.c_double, C.c_void_p]),
+    "sgp_vi_phase2": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_uint, C.c_void_p]),
+    "sgp_vi_finish": (C.c_int, [C.c_void_p, C.c_void_p, c_double_p, c_double_p]),
+    "sgp_ctx_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
+    "sgp_ctx_timings": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64, c_double_p, C.c_int, c_int_p]),
+}
+
+
+class SGPError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"sgp status {status}: {msg}")
+        self.status = status
+
+
+class NotPositiveDefinite(SGPError):
+    """R's chol() failure (caught by try() in the reference's knot proposals)."""
+
+
+def lib(auto_build: bool = True):
+    """Load (building if needed) libsgp.so.  Raises if it cannot be loaded."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if auto_build and not os.path.exists(LIB):
+            build()
+        if not os.path.exists(LIB):
+            raise RuntimeError(f"libsgp.so not found at {LIB}; run sparsergps_amd._build.build()")
+        h = C.CDLL(LIB, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in PROTOTYPES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+        return h
+
+
+def check(status: int):
+    if status == SGP_OK:
+        return
+    msg = lib().sgp_last_error().decode(errors="replace")
+    if status == SGP_ENOTPD:
+        raise NotPositiveDefinite(status, msg)
+    raise SGPError(status, msg)
+
+
+def dptr(a):
+    return a.ctypes.data_as(c_double_p)
+
+
+def require_gpu():
+    n = C.c_int(0)
+    st = lib().sgp_device_count(C.byref(n))
+    if st != SGP_OK or n.value < 1:
+        raise RuntimeError("sparsergps_amd: no HIP device visible (the MI355X path has no CPU fallback)")
+    return n.value

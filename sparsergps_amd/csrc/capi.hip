@@ -1,0 +1,667 @@
+// C ABI of libsgp.so (include/sgp.h): context management and the fused VI evaluation.
+//
+// One evaluation of sgp_eval_vi == one optimizer-iteration body of the reference's
+// norm_grad_ascent_vi (R/vi_functions.R:1089-1128): build K12/K22 at (theta, U), the ELBO
+// (elbo_fun, vi_functions.R:64-121) and its gradient w.r.t. log(theta)
+// (delbo_dcov_par, vi_functions.R:126-602).  The reference evaluates the gradient as
+// P separate n x m^2 pipelines; this implementation uses the adjoint form
+//     S = K^T K, t = K^T r (one SYRK)              -> every m x m quantity
+//     G = alpha u^T + K P (one GEMM) contracted with dK/dtheta in the epilogue
+// which is algebraically identical and needs ~3 n m^2 flops in total.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/sgp.h"
+#include "sgp_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+#define HIPCHK(expr)                                                                       \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess) {                                                                \
+      set_err("HIP error '%s' at %s:%d", hipGetErrorString(e_), __FILE__, __LINE__);      \
+      return SGP_EHIP;                                                                     \
+    }                                                                                      \
+  } while (0)
+
+inline int64_t round_up(int64_t v, int64_t q) { return (v + q - 1) / q * q; }
+
+int num_ls(int kernel, int d) { return kernel == SGP_KERNEL_ARD ? d : 1; }
+
+int make_params(int kernel, int d, const double* theta, double delta, KernParams* kp) {
+  if (kernel < 0 || kernel > 2) {
+    set_err("invalid covariance function (kernel=%d)", kernel);
+    return SGP_EINVAL;
+  }
+  if (d < 1 || d > SGP_MAXD) {
+    set_err("input dimension d=%d outside [1, %d]", d, SGP_MAXD);
+    return SGP_EINVAL;
+  }
+  if (!theta) {
+    set_err("theta is NULL");
+    return SGP_EINVAL;
+  }
+  memset(kp, 0, sizeof(*kp));
+  kp->kernel = kernel;
+  kp->d = d;
+  kp->L = num_ls(kernel, d);
+  kp->P = kp->L + 2;
+  kp->sigma = theta[0];
+  kp->sig2 = theta[0] * theta[0];
+  kp->tau = theta[kp->L + 1];
+  kp->tau2 = kp->tau * kp->tau;
+  kp->delta = delta;
+  for (int c = 0; c < kp->L; ++c) {
+    const double l = theta[1 + c];
+    if (!(l > 0.0)) {
+      set_err("length scale %d is not positive (%g)", c + 1, l);
+      return SGP_EINVAL;
+    }
+    kp->l[c] = l;
+    kp->rl[c] = 1.0 / l;
+    kp->rl2[c] = 1.0 / (l * l);
+  }
+  if (kernel == SGP_KERNEL_SQEXP) kp->coef = -1.0 / (2.0 * (theta[1] * theta[1]));
+  else if (kernel == SGP_KERNEL_ARD) kp->coef = -0.5;
+  else kp->coef = -1.0 / theta[1];
+  if (kernel != SGP_KERNEL_ARD)
+    for (int c = 1; c < d; ++c) { kp->l[c] = kp->l[0]; kp->rl[c] = kp->rl[0]; kp->rl2[c] = kp->rl2[0]; }
+  return SGP_OK;
+}
+
+struct Timer {
+  std::string name;
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct sgp_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  int64_t n = 0, n_pad = 0, m_max = 0, mp_max = 0;
+  int d = 0;
+  // per-row data (HBM-resident for the context's lifetime)
+  double* X = nullptr;      // n_pad x d, column-major, ld = n_pad
+  double* r = nullptr;      // y - mu, n_pad
+  double* K = nullptr;      // n_pad x mp (row-major, ld = mp)
+  double* alpha = nullptr;  // n_pad
+  double* zinv = nullptr;   // n_pad (FITC weights)
+  // knots and m x m work
+  double* U = nullptr;      // mp_max x d, column-major, ld = mp_max
+  double *K22 = nullptr, *K22inv = nullptr, *Bm = nullptr, *Binv = nullptr, *Pm = nullptr;
+  double *Xt = nullptr, *T1 = nullptr, *M3 = nullptr;
+  double *dinv = nullptr, *logd22 = nullptr, *logdB = nullptr;
+  double *uvec = nullptr, *cdiag = nullptr;
+  int* status = nullptr;
+  double *red1 = nullptr, *red2 = nullptr;
+  double *slab_syrk = nullptr, *slab_con = nullptr, *slab_small = nullptr, *sc = nullptr;
+  int64_t slab_syrk_cap = 0, slab_con_cap = 0;
+  // state carried between phases
+  KernParams kp;
+  int64_t m = 0, mp = 0, n_global = 0;
+  double delta = 0.0;
+  unsigned flags = 0;
+  int phase = 0;
+  // timing
+  bool timing = false;
+  std::vector<Timer> timers;
+  std::vector<hipEvent_t> pool;
+  size_t pool_used = 0;
+};
+
+namespace {
+
+constexpr int SC_LD22 = 0, SC_LDB = 1, SC_TU = 2, SC_TRKS = 3, SC_TRBS = 4, SC_RR = 5,
+              SC_G22 = 8;  // SC_G22 .. SC_G22 + P - 2
+constexpr int SC_N = 64;
+constexpr int SLAB_SMALL = 4096;
+
+hipEvent_t pool_event(sgp_ctx* c) {
+  if (c->pool_used < c->pool.size()) return c->pool[c->pool_used++];
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  c->pool.push_back(e);
+  c->pool_used++;
+  return e;
+}
+
+struct Scope {
+  sgp_ctx* c;
+  size_t idx;
+  Scope(sgp_ctx* ctx, const char* name) : c(ctx), idx((size_t)-1) {
+    if (!c->timing) return;
+    Timer t;
+    t.name = name;
+    t.a = pool_event(c);
+    t.b = pool_event(c);
+    if (!t.a || !t.b) return;
+    hipEventRecord(t.a, c->stream);
+    c->timers.push_back(t);
+    idx = c->timers.size() - 1;
+  }
+  ~Scope() {
+    if (idx != (size_t)-1) hipEventRecord(c->timers[idx].b, c->stream);
+  }
+};
+
+void timers_reset(sgp_ctx* c) {
+  c->timers.clear();
+  c->pool_used = 0;
+}
+
+template <typename T>
+int dalloc(T** p, int64_t count) {
+  *p = nullptr;
+  if (count <= 0) count = 1;
+  hipError_t e = hipMalloc((void**)p, sizeof(T) * (size_t)count);
+  if (e != hipSuccess) {
+    set_err("hipMalloc of %lld bytes failed: %s", (long long)(sizeof(T) * count),
+            hipGetErrorString(e));
+    return SGP_ENOMEM;
+  }
+  return SGP_OK;
+}
+
+void ctx_free(sgp_ctx* c) {
+  void* ptrs[] = {c->X,      c->r,     c->K,      c->alpha,   c->zinv,  c->U,    c->K22,
+                  c->K22inv, c->Bm,    c->Binv,   c->Pm,      c->Xt,    c->T1,   c->M3,
+                  c->dinv,   c->logd22, c->logdB, c->uvec,    c->cdiag, c->status, c->red1,
+                  c->red2,   c->slab_syrk, c->slab_con, c->slab_small, c->sc};
+  for (void* p : ptrs)
+    if (p) hipFree(p);
+  for (hipEvent_t e : c->pool) hipEventDestroy(e);
+  if (c->own) hipStreamDestroy(c->own);
+}
+
+int upload_knots(sgp_ctx* c, const double* U, int64_t m, int64_t ldu) {
+  std::vector<double> h((size_t)(c->mp * c->d), 0.0);
+  for (int q = 0; q < c->d; ++q)
+    for (int64_t j = 0; j < m; ++j) h[(size_t)(q * c->mp + j)] = U[j + q * ldu];
+  HIPCHK(hipMemcpyAsync(c->U, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice,
+                        c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));  // h goes out of scope
+  return SGP_OK;
+}
+
+int check_eval_args(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
+                    int64_t ldu, double delta, KernParams* kp) {
+  if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
+  if (kernel == SGP_KERNEL_EXP) {
+    set_err("fused evaluation supports 'sqexp' and 'ard' (optimize_gp.R:263 rejects others)");
+    return SGP_EINVAL;
+  }
+  int st = make_params(kernel, c->d, theta, delta, kp);
+  if (st) return st;
+  if (!U || m < 1 || m > c->m_max || ldu < m) {
+    set_err("invalid knots: m=%lld (m_max=%lld), ldu=%lld", (long long)m, (long long)c->m_max,
+            (long long)ldu);
+    return SGP_EINVAL;
+  }
+  if (!(kp->tau > 0.0) || !(kp->sigma > 0.0)) {
+    set_err("sigma and tau must be positive");
+    return SGP_EINVAL;
+  }
+  return SGP_OK;
+}
+
+}  // namespace
+
+// =========================================================================== public API
+extern "C" {
+
+const char* sgp_last_error(void) { return g_err.c_str(); }
+int sgp_abi_version(void) { return SGP_ABI_VERSION; }
+
+int sgp_device_count(int* count) {
+  if (!count) return SGP_EINVAL;
+  HIPCHK(hipGetDeviceCount(count));
+  return SGP_OK;
+}
+
+int sgp_num_params(int kernel, int d) {
+  if (kernel < 0 || kernel > 2 || d < 1) return -1;
+  return num_ls(kernel, d) + 2;
+}
+
+double sgp_kernel_pair(int kernel, const double* x1, const double* x2, int d,
+                       const double* theta) {
+  KernParams kp;
+  if (make_params(kernel, d, theta, 0.0, &kp)) return NAN;
+  double s = 0.0;
+  if (kernel == SGP_KERNEL_SQEXP) {
+    for (int c = 0; c < d; ++c) { double t = x1[c] - x2[c]; s = fma(t, t, s); }
+    return kp.sig2 * exp(kp.coef * s);
+  } else if (kernel == SGP_KERNEL_ARD) {
+    for (int c = 0; c < d; ++c) { double t = (x1[c] - x2[c]) * kp.rl[c]; s = fma(t, t, s); }
+    return kp.sig2 * exp(-s / 2.0);
+  }
+  for (int c = 0; c < d; ++c) s += fabs(x1[c] - x2[c]);
+  return kp.sig2 * exp(kp.coef * s);
+}
+
+double sgp_dkernel_pair(int kernel, const double* x1, const double* x2, int d,
+                        const double* theta, int param) {
+  KernParams kp;
+  if (make_params(kernel, d, theta, 0.0, &kp)) return NAN;
+  if (param < 0 || param >= kp.P) { set_err("invalid parameter index %d", param); return NAN; }
+  if (param == kp.P - 1) {
+    bool eq = true;
+    for (int c = 0; c < d; ++c) eq = eq && (x1[c] == x2[c]);
+    return eq ? 2.0 * kp.tau * kp.tau : 0.0;
+  }
+  double s = 0.0;
+  if (kernel == SGP_KERNEL_SQEXP) {
+    for (int c = 0; c < d; ++c) { double t = x1[c] - x2[c]; s = fma(t, t, s); }
+    const double e = exp(kp.coef * s);
+    if (param == 0) return 2.0 * kp.sigma * e * kp.sigma;
+    return (kp.sig2 * e) * ((1.0 / (kp.l[0] * kp.l[0] * kp.l[0])) * s) * kp.l[0];
+  } else if (kernel == SGP_KERNEL_ARD) {
+    for (int c = 0; c < d; ++c) { double t = (x1[c] - x2[c]) * kp.rl[c]; s = fma(t, t, s); }
+    const double e = exp(-(s / 2.0));
+    if (param == 0) return 2.0 * kp.sigma * e * kp.sigma;
+    const int c = param - 1;
+    const double dc = x1[c] - x2[c], lc = kp.l[c];
+    return (kp.sig2 * e) * ((1.0 / (lc * lc * lc)) * (dc * dc)) * lc;
+  }
+  for (int c = 0; c < d; ++c) { double t = x1[c] - x2[c]; s = fma(t, t, s); }
+  const double dist = sqrt(s);
+  const double e = exp(-(1.0 / kp.l[0]) * dist);
+  if (param == 0) return 2.0 * kp.sigma * e * kp.sigma;
+  return (kp.sig2 * e) * ((1.0 / (kp.l[0] * kp.l[0])) * dist) * kp.l[0];
+}
+
+static int fill_common(int device, int kernel, const double* x, int64_t n, int64_t ldx,
+                       const double* xp, int64_t np, int64_t ldxp, int d, const double* theta,
+                       double delta, int param, bool deriv, double* out, int64_t ldo) {
+  KernParams kp;
+  int st = make_params(kernel, d, theta, delta, &kp);
+  if (st) return st;
+  const bool sym = (xp == nullptr);
+  if (sym) { xp = x; np = n; ldxp = ldx; }
+  if (!x || !out || n < 0 || np < 0 || ldx < n || ldxp < np || ldo < n) {
+    set_err("invalid matrix arguments");
+    return SGP_EINVAL;
+  }
+  if (deriv && (param < 0 || param >= kp.P)) {
+    set_err("invalid parameter name for chosen covariance function (index %d)", param);
+    return SGP_EINVAL;
+  }
+  if (n == 0 || np == 0) return SGP_OK;
+  HIPCHK(hipSetDevice(device));
+  double *dx = nullptr, *dxp = nullptr, *dout = nullptr;
+  st = dalloc(&dx, n * d);
+  if (!st) st = dalloc(&dxp, np * d);
+  if (!st) st = dalloc(&dout, n * np);
+  if (st) { hipFree(dx); hipFree(dxp); hipFree(dout); return st; }
+  std::vector<double> hx((size_t)(n * d)), hxp((size_t)(np * d));
+  for (int c = 0; c < d; ++c) {
+    for (int64_t i = 0; i < n; ++i) hx[(size_t)(i + c * n)] = x[i + c * ldx];
+    for (int64_t j = 0; j < np; ++j) hxp[(size_t)(j + c * np)] = xp[j + c * ldxp];
+  }
+  hipError_t e = hipMemcpy(dx, hx.data(), sizeof(double) * n * d, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dxp, hxp.data(), sizeof(double) * np * d, hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = deriv ? launch_fill_dcov(kp, dx, n, n, dxp, np, np, sym, param, dout, n, 0)
+              : launch_fill_cov(kp, dx, n, n, dxp, np, np, sym, dout, n, 0);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  std::vector<double> ho;
+  if (e == hipSuccess) {
+    ho.resize((size_t)(n * np));
+    e = hipMemcpy(ho.data(), dout, sizeof(double) * n * np, hipMemcpyDeviceToHost);
+  }
+  hipFree(dx);
+  hipFree(dxp);
+  hipFree(dout);
+  if (e != hipSuccess) {
+    set_err("HIP error '%s' in covariance fill", hipGetErrorString(e));
+    return SGP_EHIP;
+  }
+  for (int64_t j = 0; j < np; ++j)
+    memcpy(out + j * ldo, ho.data() + j * n, sizeof(double) * (size_t)n);
+  return SGP_OK;
+}
+
+int sgp_make_cov(int device, int kernel, const double* x, int64_t n, int64_t ldx,
+                 const double* xp, int64_t np, int64_t ldxp, int d, const double* theta,
+                 double delta, double* out, int64_t ldo) {
+  return fill_common(device, kernel, x, n, ldx, xp, np, ldxp, d, theta, delta, 0, false, out,
+                     ldo);
+}
+
+int sgp_dsig_dtheta(int device, int kernel, const double* x, int64_t n, int64_t ldx,
+                    const double* xp, int64_t np, int64_t ldxp, int d, const double* theta,
+                    int param, double* out, int64_t ldo) {
+  return fill_common(device, kernel, x, n, ldx, xp, np, ldxp, d, theta, 0.0, param, true, out,
+                     ldo);
+}
+
+// ------------------------------------------------------------------------- context
+int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_t ldx, int d,
+                   const double* y, const double* mu, int64_t m_max) {
+  if (!out || !X || !y || !mu || n < 1 || ldx < n || d < 1 || d > SGP_MAXD || m_max < 1) {
+    set_err("invalid sgp_ctx_create arguments (n=%lld, d=%d, m_max=%lld)", (long long)n, d,
+            (long long)m_max);
+    return SGP_EINVAL;
+  }
+  *out = nullptr;
+  HIPCHK(hipSetDevice(device));
+  sgp_ctx* c = new sgp_ctx();
+  c->device = device;
+  c->n = n;
+  c->d = d;
+  c->n_pad = round_up(n, SGP_TILE);
+  c->m_max = m_max;
+  c->mp_max = round_up(m_max, SGP_TILE);
+  const int64_t np_ = c->n_pad, mp = c->mp_max, mm = mp * mp;
+  int st = SGP_OK;
+  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+    set_err("hipStreamCreate failed");
+    delete c;
+    return SGP_EHIP;
+  }
+  c->stream = c->own;
+  c->slab_syrk_cap = syrk_slab_doubles(np_, mp);
+  c->slab_con_cap = (np_ / SGP_TILE) * (mp / SGP_TILE) * (SGP_MAXD + 4);
+  st = st ? st : dalloc(&c->X, np_ * d);
+  st = st ? st : dalloc(&c->r, np_);
+  st = st ? st : dalloc(&c->K, np_ * mp);
+  st = st ? st : dalloc(&c->alpha, np_);
+  st = st ? st : dalloc(&c->zinv, np_);
+  st = st ? st : dalloc(&c->U, mp * d);
+  st = st ? st : dalloc(&c->K22, mm);
+  st = st ? st : dalloc(&c->K22inv, mm);
+  st = st ? st : dalloc(&c->Bm, mm);
+  st = st ? st : dalloc(&c->Binv, mm);
+  st = st ? st : dalloc(&c->Pm, mm);
+  st = st ? st : dalloc(&c->Xt, mm);
+  st = st ? st : dalloc(&c->T1, mm);
+  st = st ? st : dalloc(&c->M3, mm);
+  st = st ? st : dalloc(&c->dinv, mm / SGP_DB * SGP_DB);
+  st = st ? st : dalloc(&c->logd22, mp / SGP_DB);
+  st = st ? st : dalloc(&c->logdB, mp / SGP_DB);
+  st = st ? st : dalloc(&c->uvec, mp);
+  st = st ? st : dalloc(&c->cdiag, mp);
+  st = st ? st : dalloc(&c->status, 4);
+  st = st ? st : dalloc(&c->red1, sgp_vi_red1_count(m_max));
+  st = st ? st : dalloc(&c->red2, 64);
+  st = st ? st : dalloc(&c->slab_syrk, c->slab_syrk_cap);
+  st = st ? st : dalloc(&c->slab_con, c->slab_con_cap);
+  st = st ? st : dalloc(&c->slab_small, SLAB_SMALL);
+  st = st ? st : dalloc(&c->sc, SC_N);
+  if (st) {
+    ctx_free(c);
+    delete c;
+    return st;
+  }
+  // X: column-major with ld = n_pad, zero padded
+  std::vector<double> hx((size_t)(np_ * d), 0.0);
+  for (int q = 0; q < d; ++q)
+    for (int64_t i = 0; i < n; ++i) hx[(size_t)(i + q * np_)] = X[i + q * ldx];
+  std::vector<double> hr((size_t)np_, 0.0);
+  for (int64_t i = 0; i < n; ++i) hr[(size_t)i] = y[i] - mu[i];
+  hipError_t e = hipMemcpy(c->X, hx.data(), sizeof(double) * hx.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c->r, hr.data(), sizeof(double) * hr.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemset(c->K, 0, sizeof(double) * np_ * mp);
+  if (e != hipSuccess) {
+    set_err("HIP error '%s' uploading data", hipGetErrorString(e));
+    ctx_free(c);
+    delete c;
+    return SGP_EHIP;
+  }
+  *out = c;
+  return SGP_OK;
+}
+
+int sgp_ctx_destroy(sgp_ctx* c) {
+  if (!c) return SGP_OK;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  ctx_free(c);
+  delete c;
+  return SGP_OK;
+}
+
+int sgp_ctx_set_stream(sgp_ctx* c, void* s) {
+  if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
+  c->stream = s ? (hipStream_t)s : c->own;
+  return SGP_OK;
+}
+
+int sgp_ctx_set_data(sgp_ctx* c, const double* y, const double* mu) {
+  if (!c || !y || !mu) { set_err("invalid arguments"); return SGP_EINVAL; }
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<double> hr((size_t)c->n_pad, 0.0);
+  for (int64_t i = 0; i < c->n; ++i) hr[(size_t)i] = y[i] - mu[i];
+  HIPCHK(hipMemcpyAsync(c->r, hr.data(), sizeof(double) * hr.size(), hipMemcpyHostToDevice,
+                        c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return SGP_OK;
+}
+
+int64_t sgp_ctx_rows(const sgp_ctx* c) { return c ? c->n : -1; }
+
+int sgp_ctx_enable_timing(sgp_ctx* c, int enable) {
+  if (!c) return SGP_EINVAL;
+  c->timing = enable != 0;
+  return SGP_OK;
+}
+
+int sgp_ctx_timings(sgp_ctx* c, char* names, int64_t names_len, double* ms, int max_n,
+                    int* count) {
+  if (!c || !count) return SGP_EINVAL;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  std::string all;
+  int k = 0;
+  for (const Timer& t : c->timers) {
+    if (k >= max_n) break;
+    float v = 0.f;
+    HIPCHK(hipEventElapsedTime(&v, t.a, t.b));
+    if (ms) ms[k] = v;
+    all += t.name;
+    all += '\n';
+    ++k;
+  }
+  *count = k;
+  if (names && names_len > 0) {
+    strncpy(names, all.c_str(), (size_t)names_len - 1);
+    names[names_len - 1] = 0;
+  }
+  return SGP_OK;
+}
+
+// ------------------------------------------------------------------------- VI phases
+int64_t sgp_vi_red1_count(int64_t m) {
+  const int64_t mp = round_up(m, SGP_TILE);
+  return mp * mp + mp + 8;
+}
+
+int64_t sgp_vi_red2_count(int kernel, int d) { return num_ls(kernel, d) + 5; }
+
+int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
+                  int64_t ldu, double delta, double* red1) {
+  KernParams kp;
+  int st = check_eval_args(c, kernel, theta, U, m, ldu, delta, &kp);
+  if (st) return st;
+  if (!red1) { set_err("red1 is NULL"); return SGP_EINVAL; }
+  HIPCHK(hipSetDevice(c->device));
+  timers_reset(c);
+  c->kp = kp;
+  c->m = m;
+  c->mp = round_up(m, SGP_TILE);
+  c->delta = delta;
+  st = upload_knots(c, U, m, ldu);
+  if (st) return st;
+  HIPCHK(hipMemsetAsync(c->status, 0, sizeof(int) * 4, c->stream));
+  {
+    Scope t(c, "build_knm");
+    HIPCHK(launch_build_knm(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp, m, c->mp, c->K,
+                            c->stream));
+  }
+  {
+    Scope t(c, "syrk");
+    HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_vi_red1_count(m), c->stream));
+    HIPCHK(launch_syrk_aug(c->K, c->n_pad, c->mp, c->r, nullptr, c->slab_syrk,
+                           c->slab_syrk_cap, red1, c->stream));
+  }
+  c->phase = 1;
+  return SGP_OK;
+}
+
+// m x m algebra shared by VI (and FITC): K22 and Bm = K22 + S * s_scale factored and inverted.
+static int dense_stage(sgp_ctx* c, const double* S, double s_scale, double diag_sub) {
+  const int64_t mp = c->mp, mm = mp * mp;
+  Scope t(c, "dense_mm");
+  HIPCHK(launch_build_kmm(c->kp, c->U, c->mp, c->m, mp, diag_sub, c->K22, c->stream));
+  HIPCHK(dense_axpby(1.0, c->K22, s_scale, S, c->Bm, mm, c->stream));
+  HIPCHK(dense_potrf(c->K22, mp, mp, c->dinv, c->logd22, c->status, c->stream));
+  HIPCHK(dense_trtri(c->K22, mp, mp, c->dinv, c->Xt, mp, c->T1, c->stream));
+  HIPCHK(dense_inv_from_trtri(c->Xt, mp, c->K22inv, c->stream));
+  HIPCHK(dense_potrf(c->Bm, mp, mp, c->dinv, c->logdB, c->status + 1, c->stream));
+  HIPCHK(dense_trtri(c->Bm, mp, mp, c->dinv, c->Xt, mp, c->T1, c->stream));
+  HIPCHK(dense_inv_from_trtri(c->Xt, mp, c->Binv, c->stream));
+  HIPCHK(launch_sum_small(c->logd22, mp / SGP_DB, c->sc + SC_LD22, c->stream));
+  HIPCHK(launch_sum_small(c->logdB, mp / SGP_DB, c->sc + SC_LDB, c->stream));
+  return SGP_OK;
+}
+
+int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned flags,
+                  double* red2) {
+  if (!c || !red1 || !red2) { set_err("invalid arguments"); return SGP_EINVAL; }
+  if (c->phase != 1) { set_err("sgp_vi_phase2 called before sgp_vi_phase1"); return SGP_EINVAL; }
+  if (n_global < c->n) { set_err("n_global < local rows"); return SGP_EINVAL; }
+  HIPCHK(hipSetDevice(c->device));
+  const KernParams& kp = c->kp;
+  const int64_t mp = c->mp, mm = mp * mp;
+  const double z = kp.tau2 + c->delta;
+  const double* S = red1;
+  const double* t = red1 + mm;
+  c->n_global = n_global;
+  c->flags = flags;
+  HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->stream));
+  int st = dense_stage(c, S, 1.0 / z, kp.tau2);
+  if (st) return st;
+  {
+    Scope tm(c, "mm_vectors");
+    HIPCHK(dense_gemv(c->Binv, mp, t, 1.0 / z, c->uvec, c->stream));         // u = Binv t / z
+    HIPCHK(launch_dot(t, c->uvec, mp, c->slab_small, c->sc + SC_TU, c->stream));
+    HIPCHK(launch_dot(c->K22inv, S, mm, c->slab_small, c->sc + SC_TRKS, c->stream));
+    HIPCHK(launch_dot(c->Binv, S, mm, c->slab_small, c->sc + SC_TRBS, c->stream));
+    HIPCHK(hipMemcpyAsync(c->sc + SC_RR, red1 + mm + mp, sizeof(double), hipMemcpyDeviceToDevice,
+                          c->stream));
+    // P = tau^-2 K22inv - z^-1 Binv ; M3 = K22inv S K22inv
+    HIPCHK(dense_axpby(1.0 / kp.tau2, c->K22inv, -1.0 / z, c->Binv, c->Pm, mm, c->stream));
+    HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->K22inv, mp, S, mp, 0.0, c->T1,
+                         mp, c->stream));
+    HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->T1, mp, c->K22inv, mp, 0.0,
+                         c->M3, mp, c->stream));
+    HIPCHK(launch_diag(c->K22inv, mp, mp, c->cdiag, c->stream));
+  }
+  {
+    Scope tm(c, "contract_kmm");
+    int nb = 0;
+    HIPCHK(launch_contract_kmm(kp, c->U, c->mp, c->m, mp, c->uvec, c->K22inv, c->Binv, c->M3,
+                               -0.5, 0.5, -1.0 / (2.0 * kp.tau2), c->slab_small, &nb,
+                               c->stream));
+    HIPCHK(launch_colsum(c->slab_small, nb, kp.P - 1, c->sc + SC_G22, c->stream));
+  }
+  HIPCHK(hipMemsetAsync(red2, 0, sizeof(double) * sgp_vi_red2_count(kp.kernel, kp.d), c->stream));
+  {
+    Scope tm(c, "alpha");
+    int nb = 0;
+    HIPCHK(launch_alpha(c->K, c->n_pad, mp, c->r, c->uvec, 1.0 / z, nullptr, c->alpha,
+                        c->slab_small, &nb, c->stream));
+    HIPCHK(launch_colsum(c->slab_small, nb, 1, red2, c->stream));
+  }
+  {
+    Scope tm(c, "contract_knm");
+    int64_t nrec = 0, nwg = 0;
+    HIPCHK(launch_contract_knm(kp, c->K, c->Pm, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp,
+                               c->m, mp, c->alpha, c->uvec, c->cdiag, c->slab_con, &nrec, &nwg,
+                               c->stream));
+    HIPCHK(launch_colsum(c->slab_con, nwg, nrec, red2 + 1, c->stream));
+  }
+  c->phase = 2;
+  return SGP_OK;
+}
+
+int sgp_vi_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
+  if (!c || !red2 || !obj || !grad) { set_err("invalid arguments"); return SGP_EINVAL; }
+  if (c->phase != 2) { set_err("sgp_vi_finish called before sgp_vi_phase2"); return SGP_EINVAL; }
+  HIPCHK(hipSetDevice(c->device));
+  const KernParams& kp = c->kp;
+  const int L = kp.L;
+  double sc[SC_N], r2[SGP_MAXD + 8];
+  int status[4];
+  const int64_t n2 = sgp_vi_red2_count(kp.kernel, kp.d);
+  HIPCHK(hipMemcpyAsync(sc, c->sc, sizeof(sc), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(r2, red2, sizeof(double) * n2, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(status, c->status, sizeof(status), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->phase = 0;
+  if (status[0] || status[1]) {
+    set_err("chol(): the leading minor of order %d of %s is not positive definite",
+            status[0] ? status[0] : status[1],
+            status[0] ? "Sigma22" : "Sigma22 + t(Sigma12) %*% ZSig12");
+    return SGP_ENOTPD;
+  }
+  const double n = (double)c->n_global;
+  const double z = kp.tau2 + c->delta;
+  const double ld22 = 2.0 * sc[SC_LD22], ldB = 2.0 * sc[SC_LDB];
+  const double rr = sc[SC_RR], tu = sc[SC_TU], trKS = sc[SC_TRKS], trBS = sc[SC_TRBS];
+  // elbo_fun (vi_functions.R:102-118)
+  const double quad = -0.5 * rr / z + 0.5 * tu / z;
+  const double logdet22 = (c->flags & SGP_FLAG_R_DET) ? log(exp(ld22)) : ld22;
+  const double det_part = -0.5 * (n * log(z) - logdet22 + ldB);
+  const double trace_term = -(1.0 / (2.0 * kp.tau2)) * (n * (kp.sig2 + c->delta) - trKS);
+  *obj = quad + det_part - (n / 2.0) * log(2.0 * M_PI) + trace_term;
+  // delbo_dcov_par (vi_functions.R:259-419) in adjoint form
+  const double aTa = r2[0], e_sig = r2[1];
+  const double c_sum = r2[2 + L], c_cnt = r2[3 + L], c_dg = r2[4 + L];
+  const double trSinv = n / z - trBS / (z * z);
+  const double trW = 0.5 * (aTa - trSinv);
+  grad[0] = 2.0 * e_sig + sc[SC_G22] - n * kp.sig2 / kp.tau2;
+  for (int q = 0; q < L; ++q) grad[1 + q] = r2[2 + q] + sc[SC_G22 + 1 + q];
+  grad[L + 1] = 2.0 * kp.tau2 * (c_sum - (c_cnt - c->delta * c_dg) / kp.tau2) +
+                2.0 * kp.tau2 * trW - 2.0 * trace_term;
+  return SGP_OK;
+}
+
+int sgp_eval_vi(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
+                int64_t ldu, double delta, unsigned flags, double* obj, double* grad) {
+  if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
+  int st = sgp_vi_phase1(c, kernel, theta, U, m, ldu, delta, c->red1);
+  if (st) return st;
+  st = sgp_vi_phase2(c, c->red1, c->n, flags, c->red2);
+  if (st) return st;
+  return sgp_vi_finish(c, c->red2, obj, grad);
+}
+
+int sgp_eval_fitc(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
+                  int64_t ldu, double delta, unsigned flags, double* obj, double* grad) {
+  (void)c; (void)kernel; (void)theta; (void)U; (void)m; (void)ldu; (void)delta; (void)flags;
+  (void)obj; (void)grad;
+  set_err("sgp_eval_fitc: not available in this build");
+  return SGP_EINVAL;
+}
+
+}  // extern "C"

@@ -1,0 +1,247 @@
+// Covariance-matrix builders and their theta-derivatives on gfx950.
+//
+// Reference semantics (luisdamiano/sparseRGPs):
+//   make_cov_matC / make_cov_mat_ardC   src/covariance_functionsC.cpp:72-169, 191-252
+//   dsig_dthetaC / dsig_dtheta_ardC     src/covariance_function_derivativesC.cpp:307-552, 555-722
+// The reference fills each matrix with a scalar double loop that copies two rows and looks
+// parameters up by name per pair; here one thread owns one (i, j) pair per iteration, rows
+// are staged in LDS, knots live in registers and stores are coalesced along the output's
+// contiguous dimension.  These kernels are HBM-write-bound (8 B stored per pair).
+#include "sgp_internal.h"
+
+namespace {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// kernel value from raw coordinate differences (xi - uj computed per coordinate)
+__device__ __forceinline__ double kvalue(const KernParams& kp, const double* xi,
+                                         const double* uj) {
+  double s = 0.0;
+  if (kp.kernel == 0) {
+    for (int c = 0; c < kp.d; ++c) { double t = xi[c] - uj[c]; s = fma(t, t, s); }
+    return kp.sig2 * exp(kp.coef * s);
+  } else if (kp.kernel == 1) {
+    for (int c = 0; c < kp.d; ++c) { double t = (xi[c] - uj[c]) * kp.rl[c]; s = fma(t, t, s); }
+    return kp.sig2 * exp(-s / 2.0);
+  } else {
+    for (int c = 0; c < kp.d; ++c) s += fabs(xi[c] - uj[c]);
+    return kp.sig2 * exp(kp.coef * s);
+  }
+}
+
+// d K / d log theta_param for one pair (covariance_function_derivativesC.cpp:35-171, 232-301)
+__device__ __forceinline__ double dkvalue(const KernParams& kp, const double* xi,
+                                          const double* uj, int param, bool sym) {
+  const int d = kp.d;
+  if (param == kp.P - 1) {  // tau: 2 tau^2 iff all(x1 == x2)   (l.157-163)
+    if (kp.kernel == 2 && !sym) return 0.0;   // exp cross-mode returns zeros (l.520)
+    bool eq = true;
+    for (int c = 0; c < d; ++c) eq = eq && (xi[c] == uj[c]);
+    return eq ? 2.0 * kp.tau * kp.tau : 0.0;
+  }
+  if (kp.kernel == 0) {
+    double s = 0.0;
+    for (int c = 0; c < d; ++c) { double t = xi[c] - uj[c]; s = fma(t, t, s); }
+    double e = exp(kp.coef * s);
+    if (param == 0) return 2.0 * kp.sigma * e * kp.sigma;                       // l.47
+    return (kp.sig2 * e) * ((1.0 / (kp.l[0] * kp.l[0] * kp.l[0])) * s) * kp.l[0];  // l.98-99
+  } else if (kp.kernel == 1) {
+    double s = 0.0;
+    for (int c = 0; c < d; ++c) { double t = (xi[c] - uj[c]) * kp.rl[c]; s = fma(t, t, s); }
+    double e = exp(-(s / 2.0));
+    if (param == 0) return 2.0 * kp.sigma * e * kp.sigma;                       // l.78
+    const int c = param - 1;
+    const double lc = kp.l[c];
+    const double dc = xi[c] - uj[c];
+    return (kp.sig2 * e) * ((1.0 / (lc * lc * lc)) * (dc * dc)) * lc;          // l.133-134
+  } else {  // exp: derivatives use the L2 distance (quirk Q12, l.244, 264)
+    double s = 0.0;
+    for (int c = 0; c < d; ++c) { double t = xi[c] - uj[c]; s = fma(t, t, s); }
+    double dist = sqrt(s);
+    double e = exp(-(1.0 / kp.l[0]) * dist);
+    if (param == 0) return 2.0 * kp.sigma * e * kp.sigma;
+    return (kp.sig2 * e) * ((1.0 / (kp.l[0] * kp.l[0])) * dist) * kp.l[0];
+  }
+}
+
+// Layer-1 filler: out (n x np, column-major).  Block = 64 rows x 4 column lanes.
+template <bool DERIV>
+__global__ void __launch_bounds__(256) k_fill(KernParams kp, const double* __restrict__ x,
+                                              int64_t n, int64_t ldx,
+                                              const double* __restrict__ xp, int64_t np,
+                                              int64_t ldxp, int sym, int param,
+                                              double* __restrict__ out, int64_t ldo,
+                                              int cols_per_block) {
+  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  const int64_t j0 = (int64_t)blockIdx.y * cols_per_block;
+  double xi[SGP_MAXD], uj[SGP_MAXD];
+  if (i < n)
+    for (int c = 0; c < kp.d; ++c) xi[c] = x[i + c * ldx];
+  for (int64_t jj = threadIdx.y; jj < cols_per_block; jj += 4) {
+    const int64_t j = j0 + jj;
+    if (j >= np) break;
+    for (int c = 0; c < kp.d; ++c) uj[c] = xp[j + c * ldxp];
+    if (i >= n) continue;
+    double v;
+    if (DERIV) {
+      v = dkvalue(kp, xi, uj, param, sym != 0);
+    } else {
+      v = kvalue(kp, xi, uj);
+      if (sym && i == j) v = v + kp.tau2 + kp.delta;   // covariance_functionsC.cpp:91
+    }
+    out[i + j * ldo] = v;
+  }
+}
+
+// K12 row-major (n_pad x mp).  Block: 64 knot columns (lanes) x 4 row groups; each block
+// owns 64 rows.  Row coordinates are staged in LDS and broadcast; knots stay in registers.
+__global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* __restrict__ X,
+                                                   int64_t ldx, int64_t n,
+                                                   const double* __restrict__ U, int64_t ldu,
+                                                   int64_t m, int64_t mp,
+                                                   double* __restrict__ K) {
+  __shared__ double xs[64 * SGP_MAXD];
+  const int d = kp.d;
+  const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  const int64_t i0 = (int64_t)blockIdx.y * 64;
+  const int tid = threadIdx.y * 64 + threadIdx.x;
+  for (int e = tid; e < 64 * d; e += 256) {
+    const int r = e % 64, c = e / 64;
+    const int64_t i = i0 + r;
+    xs[r * d + c] = (i < n) ? X[i + c * ldx] : 0.0;
+  }
+  double uj[SGP_MAXD];
+  const bool jv = j < m;
+  for (int c = 0; c < d; ++c) uj[c] = jv ? U[j + c * ldu] : 0.0;
+  __syncthreads();
+  for (int r = threadIdx.y; r < 64; r += 4) {
+    const int64_t i = i0 + r;
+    double v = 0.0;
+    if (jv && i < n) v = kvalue(kp, &xs[r * d], uj);
+    K[i * mp + j] = v;
+  }
+}
+
+// K22 (mp x mp, row-major) with diagonal ((sig2 + tau2 + delta) - diag_sub), identity padding.
+__global__ void __launch_bounds__(256) k_build_kmm(KernParams kp, const double* __restrict__ U,
+                                                   int64_t ldu, int64_t m, int64_t mp,
+                                                   double diag_sub, double* __restrict__ K22) {
+  const int64_t k = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  const int64_t j = (int64_t)blockIdx.y * 4 + threadIdx.y;
+  if (j >= mp || k >= mp) return;
+  double v;
+  if (j < m && k < m) {
+    double uj[SGP_MAXD], uk[SGP_MAXD];
+    for (int c = 0; c < kp.d; ++c) { uj[c] = U[j + c * ldu]; uk[c] = U[k + c * ldu]; }
+    v = kvalue(kp, uj, uk);
+    if (j == k) v = ((v + kp.tau2) + kp.delta) - diag_sub;
+  } else {
+    v = (j == k) ? 1.0 : 0.0;
+  }
+  K22[j * mp + k] = v;
+}
+
+// sum_{j,k<m} G22_jk dK22^p_jk, G22 = a u_j u_k + b (Ainv - Binv)_jk + c M3_jk.
+// Per block partial sums of P-1 entries (all parameters except tau, whose dK22 is 0 on the
+// Gaussian paths, vi_functions.R:313-316).
+__global__ void __launch_bounds__(256) k_contract_kmm(KernParams kp, const double* __restrict__ U,
+                                                      int64_t ldu, int64_t m, int64_t mp,
+                                                      const double* __restrict__ uvec,
+                                                      const double* __restrict__ Ainv,
+                                                      const double* __restrict__ Binv,
+                                                      const double* __restrict__ M3, double a,
+                                                      double b, double c,
+                                                      double* __restrict__ slab) {
+  __shared__ double red[4][SGP_MAXD + 2];
+  const int np = kp.P - 1;
+  double acc[SGP_MAXD + 1];
+  for (int p = 0; p < np; ++p) acc[p] = 0.0;
+  const int64_t total = m * m;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t j = e / m, k = e % m;
+    double uj[SGP_MAXD], uk[SGP_MAXD];
+    for (int q = 0; q < kp.d; ++q) { uj[q] = U[j + q * ldu]; uk[q] = U[k + q * ldu]; }
+    const int64_t o = j * mp + k;
+    const double g = a * uvec[j] * uvec[k] + b * (Ainv[o] - Binv[o]) + c * M3[o];
+    const double kv = kvalue(kp, uj, uk);
+    const double gk = g * kv;
+    acc[0] += 2.0 * gk;                                   // sigma: dK/dlog sigma = 2K
+    if (kp.kernel == 0) {
+      double s = 0.0;
+      for (int q = 0; q < kp.d; ++q) { double t = uj[q] - uk[q]; s = fma(t, t, s); }
+      acc[1] += gk * s * kp.rl2[0];
+    } else {
+      for (int q = 0; q < kp.d; ++q) {
+        double t = (uj[q] - uk[q]) * kp.rl[q];
+        acc[1 + q] += gk * t * t;
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int p = 0; p < np; ++p) {
+    double v = wave_sum(acc[p]);
+    if (lane == 0) red[w][p] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < np)
+    slab[(int64_t)blockIdx.x * np + threadIdx.x] =
+        red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+}  // namespace
+
+hipError_t launch_fill_cov(const KernParams& kp, const double* x, int64_t n, int64_t ldx,
+                           const double* xp, int64_t np, int64_t ldxp, bool sym, double* out,
+                           int64_t ldo, hipStream_t s) {
+  const int cpb = 64;
+  dim3 grid((unsigned)((n + 63) / 64), (unsigned)((np + cpb - 1) / cpb));
+  if (n == 0 || np == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fill<false>, grid, dim3(64, 4), 0, s, kp, x, n, ldx, xp, np, ldxp,
+                     sym ? 1 : 0, 0, out, ldo, cpb);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_dcov(const KernParams& kp, const double* x, int64_t n, int64_t ldx,
+                            const double* xp, int64_t np, int64_t ldxp, bool sym, int param,
+                            double* out, int64_t ldo, hipStream_t s) {
+  const int cpb = 64;
+  dim3 grid((unsigned)((n + 63) / 64), (unsigned)((np + cpb - 1) / cpb));
+  if (n == 0 || np == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fill<true>, grid, dim3(64, 4), 0, s, kp, x, n, ldx, xp, np, ldxp,
+                     sym ? 1 : 0, param, out, ldo, cpb);
+  return hipGetLastError();
+}
+
+hipError_t launch_build_knm(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
+                            int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
+                            double* K, hipStream_t s) {
+  dim3 grid((unsigned)(mp / 64), (unsigned)(n_pad / 64));
+  hipLaunchKernelGGL(k_build_knm, grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K);
+  return hipGetLastError();
+}
+
+hipError_t launch_build_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,
+                            int64_t mp, double diag_sub, double* K22, hipStream_t s) {
+  dim3 grid((unsigned)(mp / 64), (unsigned)((mp + 3) / 4));
+  hipLaunchKernelGGL(k_build_kmm, grid, dim3(64, 4), 0, s, kp, U, ldu, m, mp, diag_sub, K22);
+  return hipGetLastError();
+}
+
+hipError_t launch_contract_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,
+                               int64_t mp, const double* uvec, const double* Ainv,
+                               const double* Binv, const double* M3, double a, double b,
+                               double c, double* slab, int* nblocks, hipStream_t s) {
+  int64_t total = m * m;
+  int nb = (int)((total + 255) / 256);
+  if (nb > 1024) nb = 1024;
+  if (nb < 1) nb = 1;
+  *nblocks = nb;
+  hipLaunchKernelGGL(k_contract_kmm, dim3(nb), dim3(256), 0, s, kp, U, ldu, m, mp, uvec, Ainv,
+                     Binv, M3, a, b, c, slab);
+  return hipGetLastError();
+}

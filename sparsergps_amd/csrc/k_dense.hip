@@ -1,0 +1,288 @@
+// m x m dense algebra and row reductions for the sparse-GP evaluation on gfx950.
+//
+// The reference calls base-R chol()/solve() (LAPACK dpotrf/dgesv) on the m x m matrices
+// Sigma22 and Sigma22 + t(Sigma12) %*% (B * Sigma12) (R/vi_functions.R:96, 231, 239).  Here:
+//   dense_potrf  right-looking blocked Cholesky, 64-wide panels: the 64x64 diagonal block is
+//                factored (and inverted) in LDS by one workgroup, the panel solve and the
+//                trailing SYRK are f64-MFMA GEMMs (k_gemm64 in k_mfma.hip);
+//   dense_trtri  blocked triangular inverse by block rows (two GEMMs per block row);
+//   X^T X        gives the SPD inverse.
+// Reductions are two-stage with fixed order (deterministic, run-to-run bit-identical).
+#include "sgp_internal.h"
+
+namespace {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ double block_sum(double v, double* sh) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_sum(v);
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  double t = 0.0;
+  const int nw = blockDim.x >> 6;
+  for (int q = 0; q < nw; ++q) t += sh[q];
+  __syncthreads();
+  return t;
+}
+
+// Factor the 64x64 diagonal block kb of A in LDS; write L (lower) back, inv(L) to dinv,
+// sum log(L_ii) to logd[kb].  First failing pivot -> status = global index + 1.
+__global__ void __launch_bounds__(256) k_potrf_diag(double* A, int64_t lda, int kb,
+                                                    double* __restrict__ dinv,
+                                                    double* __restrict__ logd,
+                                                    int* __restrict__ status) {
+  __shared__ double a[64][65];
+  __shared__ double x[64][65];
+  const int tid = threadIdx.x;
+  const int64_t o = (int64_t)kb * 64;
+  for (int e = tid; e < 64 * 64; e += 256) {
+    const int i = e >> 6, j = e & 63;
+    a[i][j] = (j <= i) ? A[(o + i) * lda + o + j] : 0.0;
+    x[i][j] = 0.0;
+  }
+  __syncthreads();
+  for (int k = 0; k < 64; ++k) {
+    if (tid == 0) {
+      double p = a[k][k];
+      if (!(p > 0.0) || !isfinite(p)) {
+        atomicCAS(status, 0, (int)(o + k + 1));
+      }
+      a[k][k] = sqrt(p);
+    }
+    __syncthreads();
+    const double piv = a[k][k];
+    if (tid < 63 - k) a[k + 1 + tid][k] /= piv;
+    __syncthreads();
+    const int rem = 63 - k;
+    for (int e = tid; e < rem * rem; e += 256) {
+      const int i = k + 1 + e / rem, j = k + 1 + e % rem;
+      if (j <= i) a[i][j] -= a[i][k] * a[j][k];
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < 64 * 64; e += 256) {
+    const int i = e >> 6, j = e & 63;
+    if (j <= i) A[(o + i) * lda + o + j] = a[i][j];
+  }
+  if (tid == 0) {
+    double s = 0.0;
+    for (int k = 0; k < 64; ++k) s += log(a[k][k]);
+    logd[kb] = s;
+  }
+  // triangular inverse by rows: x[i][j] = -(sum_{k=j}^{i-1} a[i][k] x[k][j]) / a[i][i]
+  const int jj = tid >> 2, part = tid & 3;
+  for (int i = 0; i < 64; ++i) {
+    double s = 0.0;
+    if (jj < i)
+      for (int k = jj + part; k < i; k += 4) s = fma(a[i][k], x[k][jj], s);
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    if (part == 0 && jj < i) x[i][jj] = -s / a[i][i];
+    if (tid == 0) x[i][i] = 1.0 / a[i][i];
+    __syncthreads();
+  }
+  double* D = dinv + (int64_t)kb * 64 * 64;
+  for (int e = tid; e < 64 * 64; e += 256) D[e] = x[e >> 6][e & 63];
+}
+
+__global__ void __launch_bounds__(256) k_copy_block(const double* __restrict__ src,
+                                                    double* __restrict__ dst, int64_t ldd) {
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) dst[(e >> 6) * ldd + (e & 63)] = src[e];
+}
+
+__global__ void __launch_bounds__(256) k_axpby(double a, const double* __restrict__ A, double b,
+                                               const double* __restrict__ B,
+                                               double* __restrict__ C, int64_t count) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < count;
+       e += (int64_t)gridDim.x * 256)
+    C[e] = a * A[e] + b * B[e];
+}
+
+// y = scale * A x, one wave per row
+__global__ void __launch_bounds__(256) k_gemv(const double* __restrict__ A, int64_t mp,
+                                              const double* __restrict__ x, double scale,
+                                              double* __restrict__ y) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= mp) return;
+  double s = 0.0;
+  for (int64_t j = lane; j < mp; j += 64) s = fma(A[row * mp + j], x[j], s);
+  s = wave_sum(s);
+  if (lane == 0) y[row] = scale * s;
+}
+
+// alpha_i = (r_i - K_i u) * invz ; per-block sum of alpha^2.  u staged in LDS.
+__global__ void __launch_bounds__(256) k_alpha(const double* __restrict__ K, int64_t n_pad,
+                                               int64_t mp, const double* __restrict__ r,
+                                               const double* __restrict__ u, double invz,
+                                               const double* __restrict__ invz_vec,
+                                               double* __restrict__ alpha,
+                                               double* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) double su[];
+  __shared__ double sh[4];
+  for (int64_t j = threadIdx.x; j < mp; j += 256) su[j] = u[j];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double a2 = 0.0;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < n_pad; row += (int64_t)gridDim.x * 4) {
+    const double2* Kr = reinterpret_cast<const double2*>(K + row * mp);
+    double s = 0.0;
+    for (int64_t q = lane; q < mp / 2; q += 64) {
+      const double2 kv = Kr[q];
+      s = fma(kv.x, su[2 * q], s);
+      s = fma(kv.y, su[2 * q + 1], s);
+    }
+    s = wave_sum(s);
+    const double iz = invz_vec ? invz_vec[row] : invz;
+    const double al = (r[row] - s) * iz;
+    if (lane == 0) alpha[row] = al;
+    a2 = fma(al, al, a2);
+  }
+  // every lane of a wave holds the same a2 -> take lane 0's
+  if (lane == 0) sh[w] = a2;
+  __syncthreads();
+  if (threadIdx.x == 0) slab[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+__global__ void __launch_bounds__(256) k_dot_partial(const double* __restrict__ a,
+                                                     const double* __restrict__ b, int64_t count,
+                                                     double* __restrict__ partial) {
+  __shared__ double sh[4];
+  double s = 0.0;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < count;
+       e += (int64_t)gridDim.x * 256)
+    s = b ? fma(a[e], b[e], s) : s + a[e];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+__global__ void __launch_bounds__(256) k_sum_vec(const double* __restrict__ v, int64_t count,
+                                                 double* __restrict__ out) {
+  __shared__ double sh[4];
+  double s = 0.0;
+  for (int64_t e = threadIdx.x; e < count; e += 256) s += v[e];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+// out[k] = sum_r slab[r*ncol + k]; one block per column
+__global__ void __launch_bounds__(256) k_colsum(const double* __restrict__ slab, int64_t nrows,
+                                                int64_t ncol, double* __restrict__ out) {
+  __shared__ double sh[4];
+  const int64_t k = blockIdx.x;
+  double s = 0.0;
+  for (int64_t r = threadIdx.x; r < nrows; r += 256) s += slab[r * ncol + k];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) out[k] = s;
+}
+
+__global__ void __launch_bounds__(256) k_diag(const double* __restrict__ A, int64_t mp,
+                                              int64_t lda, double* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j < mp) out[j] = A[j * lda + j];
+}
+
+}  // namespace
+
+hipError_t dense_potrf(double* A, int64_t mp, int64_t lda, double* dinv, double* logd,
+                       int* status, hipStream_t s) {
+  const int nb = (int)(mp / SGP_DB);
+  for (int kb = 0; kb < nb; ++kb) {
+    hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(256), 0, s, A, lda, kb, dinv, logd, status);
+    const int64_t rem = mp - (int64_t)(kb + 1) * SGP_DB;
+    if (rem > 0) {
+      double* A21 = A + (int64_t)(kb + 1) * SGP_DB * lda + (int64_t)kb * SGP_DB;
+      double* A22 = A + (int64_t)(kb + 1) * SGP_DB * lda + (int64_t)(kb + 1) * SGP_DB;
+      const double* Dk = dinv + (int64_t)kb * SGP_DB * SGP_DB;
+      hipError_t e = launch_gemm64(false, true, false, rem, SGP_DB, SGP_DB, 1.0, A21, lda, Dk,
+                                   SGP_DB, 0.0, A21, lda, s);
+      if (e != hipSuccess) return e;
+      e = launch_gemm64(false, true, true, rem, rem, SGP_DB, -1.0, A21, lda, A21, lda, 1.0, A22,
+                        lda, s);
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipGetLastError();
+}
+
+hipError_t dense_trtri(const double* L, int64_t mp, int64_t lda, const double* dinv, double* X,
+                       int64_t ldx, double* T, hipStream_t s) {
+  const int nb = (int)(mp / SGP_DB);
+  hipError_t e = hipMemsetAsync(X, 0, sizeof(double) * mp * ldx, s);
+  if (e != hipSuccess) return e;
+  for (int ib = 0; ib < nb; ++ib) {
+    const double* Di = dinv + (int64_t)ib * SGP_DB * SGP_DB;
+    double* Xii = X + (int64_t)ib * SGP_DB * ldx + (int64_t)ib * SGP_DB;
+    hipLaunchKernelGGL(k_copy_block, dim3(1), dim3(256), 0, s, Di, Xii, ldx);
+    if (ib > 0) {
+      const int64_t w = (int64_t)ib * SGP_DB;
+      e = launch_gemm64(false, false, false, SGP_DB, w, w, 1.0, L + w * lda, lda, X, ldx, 0.0, T,
+                        mp, s);
+      if (e != hipSuccess) return e;
+      e = launch_gemm64(false, false, false, SGP_DB, w, SGP_DB, -1.0, Di, SGP_DB, T, mp, 0.0,
+                        X + w * ldx, ldx, s);
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipGetLastError();
+}
+
+hipError_t dense_inv_from_trtri(const double* X, int64_t mp, double* Ainv, hipStream_t s) {
+  return launch_gemm64(true, false, false, mp, mp, mp, 1.0, X, mp, X, mp, 0.0, Ainv, mp, s);
+}
+
+hipError_t dense_axpby(double a, const double* A, double b, const double* B, double* C,
+                       int64_t count, hipStream_t s) {
+  int nb = (int)((count + 255) / 256);
+  if (nb > 4096) nb = 4096;
+  hipLaunchKernelGGL(k_axpby, dim3(nb), dim3(256), 0, s, a, A, b, B, C, count);
+  return hipGetLastError();
+}
+
+hipError_t dense_gemv(const double* A, int64_t mp, const double* x, double scale, double* y,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_gemv, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, s, A, mp, x, scale,
+                     y);
+  return hipGetLastError();
+}
+
+hipError_t launch_alpha(const double* K, int64_t n_pad, int64_t mp, const double* r,
+                        const double* u, double invz, const double* invz_vec, double* alpha,
+                        double* slab, int* nblocks, hipStream_t s) {
+  int64_t nb = (n_pad + 3) / 4;
+  if (nb > 2048) nb = 2048;
+  *nblocks = (int)nb;
+  hipLaunchKernelGGL(k_alpha, dim3((unsigned)nb), dim3(256), sizeof(double) * mp, s, K, n_pad,
+                     mp, r, u, invz, invz_vec, alpha, slab);
+  return hipGetLastError();
+}
+
+hipError_t launch_dot(const double* a, const double* b, int64_t count, double* partial,
+                      double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_dot_partial, dim3(256), dim3(256), 0, s, a, b, count, partial);
+  hipLaunchKernelGGL(k_sum_vec, dim3(1), dim3(256), 0, s, partial, (int64_t)256, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_colsum(const double* slab, int64_t nrows, int64_t ncol, double* out,
+                         hipStream_t s) {
+  if (ncol <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_colsum, dim3((unsigned)ncol), dim3(256), 0, s, slab, nrows, ncol, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_diag(const double* A, int64_t mp, int64_t lda, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_diag, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s, A, mp, lda,
+                     out);
+  return hipGetLastError();
+}
+
+hipError_t launch_sum_small(const double* v, int64_t count, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_sum_vec, dim3(1), dim3(256), 0, s, v, count, out);
+  return hipGetLastError();
+}

@@ -1,0 +1,533 @@
+// fp64 matrix-core (v_mfma_f64_16x16x4_f64) kernels for gfx950.
+//
+//  k_syrk      S = K^T diag(w) K over n rows (split-K over row chunks, deterministic slabs),
+//              plus t = K^T diag(w) r and rr = r^T diag(w) r.  Replaces the reference's
+//              `t(Sigma12) %*% ((1/Z) * Sigma12)` (R/vi_functions.R:96, 231, 239).
+//  k_contract  G = alpha u^T + K P fused with the d K12/d log(theta) contraction: the GEMM
+//              result never leaves registers; the epilogue recomputes K_ij and the pairwise
+//              distances and reduces sum_ij G_ij dK_ij/dtheta_p for every p at once.  Replaces
+//              the reference's per-parameter loop of ~13 n x m^2 products
+//              (R/vi_functions.R:259-419).
+//  k_gemm64    small generic GEMM for the m x m dense algebra.
+//
+// MFMA f64 16x16x4 lane maps (cdna_hip_programming.md Sec.3):
+//   A: lane l holds A[l&15][l>>4];  B: lane l holds B[l>>4][l&15];
+//   C/D: register r of lane l is C[(l>>4) + 4r][l&15].
+#include "sgp_internal.h"
+
+namespace {
+
+constexpr int T128 = 128;
+constexpr int BK = 16;
+constexpr int SB = 144;   // LDS row stride (doubles) of [k][128] operand images: 2*144 % 64 == 32
+constexpr int SA = 18;    // LDS row stride of the [128][16] A image: conflict-free f64 reads
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// bijective XCD-aware remap: work items that share operands get consecutive ids on one XCD
+__device__ __forceinline__ int64_t xcd_remap(int64_t orig, int64_t nwg) {
+  const int64_t x = orig % 8, q = nwg / 8, r = nwg % 8;
+  const int64_t base = (x < r) ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  return base + orig / 8;
+}
+
+__device__ __forceinline__ void load8(const double* __restrict__ g, double2 (&v)[4]) {
+  const double2* p = reinterpret_cast<const double2*>(g);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = p[q];
+}
+__device__ __forceinline__ void store8(double* s, const double2 (&v)[4]) {
+  double2* p = reinterpret_cast<double2*>(s);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) p[q] = v[q];
+}
+
+// ============================================================================ SYRK
+// grid = splits * T (T = lower 128-tiles); block 256 = 4 waves as 2x2 of 64x64.
+__global__ void __launch_bounds__(256, 2)
+k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __restrict__ r,
+       const double* __restrict__ w, int64_t chunk, int T, int nb,
+       double* __restrict__ slab_s, double* __restrict__ slab_t, double* __restrict__ slab_rr) {
+  __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
+  __shared__ __attribute__((aligned(16))) double Kb[2][BK * SB];
+  __shared__ double rw[2][BK];
+  __shared__ double rr_acc;
+
+  const int64_t nwg = (int64_t)gridDim.x;
+  const int64_t wgid = xcd_remap(blockIdx.x, nwg);
+  const int split = (int)(wgid / T);
+  const int tile = (int)(wgid % T);
+  int ta = (int)((sqrtf(8.0f * tile + 1.0f) - 1.0f) * 0.5f);
+  while ((ta + 1) * (ta + 2) / 2 <= tile) ++ta;
+  while (ta * (ta + 1) / 2 > tile) --ta;
+  const int tb = tile - ta * (ta + 1) / 2;
+  const bool diag = (ta == tb);
+  const bool sepB = !diag || (w != nullptr);
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int64_t rbeg = (int64_t)split * chunk;
+  int64_t rend = rbeg + chunk;
+  if (rend > n_pad) rend = n_pad;
+  const int nsteps = (int)((rend - rbeg) / BK);
+
+  d4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+
+  // loader mapping: 16 rows x 128 cols, 8 doubles per thread
+  const int lrow = tid >> 4, lcol = (tid & 15) * 8;
+  const double* gA = K + ta * (int64_t)T128 + lcol;
+  const double* gB = K + tb * (int64_t)T128 + lcol;
+  double2 va[4], vb[4];
+  double vr = 0.0;
+  double tacc = 0.0;  // t partial for column (tid) when diag
+  if (tid == 0) rr_acc = 0.0;
+
+  auto gload = [&](int step) {
+    const int64_t row = rbeg + (int64_t)step * BK + lrow;
+    load8(gA + row * mp, va);
+    if (sepB) load8(gB + row * mp, vb);
+    if (tid < BK) {
+      const int64_t rr = rbeg + (int64_t)step * BK + tid;
+      const double rv = r[rr];
+      vr = (w != nullptr) ? w[rr] * rv : rv;
+    }
+  };
+  auto sstore = [&](int buf, int step) {
+    if (w != nullptr) {
+      const double wi = w[rbeg + (int64_t)step * BK + lrow];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { va[q].x *= wi; va[q].y *= wi; }
+    }
+    store8(&Ka[buf][lrow * SB + lcol], va);
+    if (sepB) store8(&Kb[buf][lrow * SB + lcol], vb);
+    if (tid < BK) rw[buf][tid] = vr;
+  };
+
+  if (nsteps > 0) {
+    gload(0);
+    sstore(0, 0);
+  }
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
+    if (step + 1 < nsteps) gload(step + 1);
+    const double* As = Ka[cur];
+    const double* Bs = sepB ? Kb[cur] : Ka[cur];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int krow = kk * 4 + (lane >> 4);
+      double af[4], bf[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        af[f] = As[krow * SB + wr * 64 + f * 16 + (lane & 15)];
+        bf[f] = Bs[krow * SB + wc * 64 + f * 16 + (lane & 15)];
+      }
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
+    }
+    if (diag && tid < T128) {
+      // t_a += sum_i (w_i r_i) K_ia over this step's rows (unscaled operand image)
+      const double* Bu = sepB ? Kb[cur] : Ka[cur];
+#pragma unroll
+      for (int q = 0; q < BK; ++q) tacc = fma(rw[cur][q], Bu[q * SB + tid], tacc);
+    }
+    if (diag && ta == 0 && tid == 255) {
+      double s = 0.0;
+      for (int q = 0; q < BK; ++q) {
+        const int64_t rr = rbeg + (int64_t)step * BK + q;
+        s += rw[cur][q] * r[rr];
+      }
+      rr_acc += s;
+    }
+    if (step + 1 < nsteps) sstore(cur ^ 1, step + 1);
+    __syncthreads();
+  }
+
+  double* out = slab_s + ((int64_t)split * T + tile) * (T128 * T128);
+#pragma unroll
+  for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
+        const int col = wc * 64 + fn * 16 + (lane & 15);
+        out[row * T128 + col] = acc[fm][fn][q];
+      }
+  if (diag && tid < T128) slab_t[((int64_t)split * nb + ta) * T128 + tid] = tacc;
+  if (diag && ta == 0 && tid == 255) slab_rr[split] = rr_acc;
+}
+
+// S (mp x mp full) from the per-split lower tiles; red = [S, t, rr]
+__global__ void __launch_bounds__(256)
+k_syrk_reduce(const double* __restrict__ slab_s, int splits, int T, int64_t mp,
+              double* __restrict__ red) {
+  const int tile = blockIdx.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;  // element of the 128x128 tile
+  int ta = (int)((sqrtf(8.0f * tile + 1.0f) - 1.0f) * 0.5f);
+  while ((ta + 1) * (ta + 2) / 2 <= tile) ++ta;
+  while (ta * (ta + 1) / 2 > tile) --ta;
+  const int tb = tile - ta * (ta + 1) / 2;
+  double s = 0.0;
+  for (int sp = 0; sp < splits; ++sp) s += slab_s[((int64_t)sp * T + tile) * (T128 * T128) + e];
+  const int64_t a = (int64_t)ta * T128 + e / T128;
+  const int64_t b = (int64_t)tb * T128 + e % T128;
+  red[a * mp + b] = s;
+  red[b * mp + a] = s;
+}
+
+__global__ void __launch_bounds__(256)
+k_syrk_reduce_t(const double* __restrict__ slab_t, const double* __restrict__ slab_rr,
+                int splits, int nb, int64_t mp, double* __restrict__ red) {
+  const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (a < mp) {
+    const int ta = (int)(a / T128), col = (int)(a % T128);
+    double s = 0.0;
+    for (int sp = 0; sp < splits; ++sp) s += slab_t[((int64_t)sp * nb + ta) * T128 + col];
+    red[mp * mp + a] = s;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    double s = 0.0;
+    for (int sp = 0; sp < splits; ++sp) s += slab_rr[sp];
+    red[mp * mp + mp] = s;
+  }
+}
+
+// ============================================================================ contraction
+template <int DT>
+__global__ void __launch_bounds__(256, 2)
+k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict__ P,
+           const double* __restrict__ X, int64_t ldx, int64_t n, int64_t n_pad,
+           const double* __restrict__ U, int64_t ldu, int64_t m, int64_t mp,
+           const double* __restrict__ alpha, const double* __restrict__ uvec,
+           const double* __restrict__ cdiag, double* __restrict__ slab, int nrec) {
+  constexpr int A_SZ = T128 * SA;   // 2304
+  constexpr int B_SZ = BK * SB;     // 2304
+  __shared__ __attribute__((aligned(16))) double lds[2 * (A_SZ + B_SZ)];
+  __shared__ double red[4][SGP_MAXD + 4];
+
+  const int64_t ntj = mp / T128;
+  const int64_t nwg = (n_pad / T128) * ntj;
+  const int64_t wgid = xcd_remap(blockIdx.x, nwg);
+  const int64_t ti = wgid / ntj, tj = wgid % ntj;
+  const int64_t i0 = ti * T128, j0 = tj * T128;
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+
+  d4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+
+  // A loader: 128 rows x 16 k, thread -> (row = tid>>1, 8 doubles at (tid&1)*8)
+  const int arow = tid >> 1, acol = (tid & 1) * 8;
+  const double* gA = K + (i0 + arow) * mp + acol;
+  // B loader: 16 k x 128 cols, thread -> (k = tid>>4, 8 doubles at (tid&15)*8)
+  const int bk = tid >> 4, bcol = (tid & 15) * 8;
+  const double* gB = P + (int64_t)bk * mp + j0 + bcol;
+  double2 va[4], vb[4];
+  const int nsteps = (int)(mp / BK);
+
+  auto gload = [&](int step) {
+    load8(gA + (int64_t)step * BK, va);
+    load8(gB + (int64_t)step * BK * mp, vb);
+  };
+  auto sstore = [&](int buf) {
+    double* As = lds + buf * (A_SZ + B_SZ);
+    double* Bs = As + A_SZ;
+    store8(&As[arow * SA + acol], va);
+    store8(&Bs[bk * SB + bcol], vb);
+  };
+
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
+    if (step + 1 < nsteps) gload(step + 1);
+    const double* As = lds + cur * (A_SZ + B_SZ);
+    const double* Bs = As + A_SZ;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int kx = kk * 4 + (lane >> 4);
+      double af[4], bf[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        af[f] = As[(wr * 64 + f * 16 + (lane & 15)) * SA + kx];
+        bf[f] = Bs[kx * SB + wc * 64 + f * 16 + (lane & 15)];
+      }
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
+    }
+    if (step + 1 < nsteps) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---------------- epilogue: G = alpha u^T + acc; contract with dK/dlog(theta) ----------
+  const int d = kp.d;
+  const bool ard = (kp.kernel == 1);
+  const double sig2 = kp.sig2, coef = kp.coef, rl2s = kp.rl2[0];
+  double* s_alpha = lds;                    // 128
+  double* s_u = s_alpha + T128;             // 128
+  double* s_cd = s_u + T128;                // 128
+  double* s_rl = s_cd + T128;               // SGP_MAXD
+  double* s_x = s_rl + SGP_MAXD;            // 128 x d   (row-major [row][c])
+  double* s_uc = s_x + T128 * d;            // 128 x d
+  for (int e = tid; e < T128; e += 256) {
+    s_alpha[e] = alpha[i0 + e];
+    const int64_t j = j0 + e;
+    s_u[e] = (j < m) ? uvec[j] : 0.0;
+    s_cd[e] = (j < m) ? cdiag[j] : 0.0;
+  }
+  if (tid < SGP_MAXD) s_rl[tid] = (tid < d) ? kp.rl[tid] : 0.0;
+  for (int e = tid; e < T128 * d; e += 256) {
+    const int rr = e % T128, c = e / T128;
+    const int64_t i = i0 + rr, j = j0 + rr;
+    s_x[rr * d + c] = (i < n) ? X[i + c * ldx] : 0.0;
+    s_uc[rr * d + c] = (j < m) ? U[j + c * ldu] : 0.0;
+  }
+  __syncthreads();
+
+  const int L = kp.L;
+  double e_sig = 0.0, c_sum = 0.0, c_cnt = 0.0, c_dg = 0.0;
+  double e_l[DT];
+#pragma unroll
+  for (int c = 0; c < DT; ++c) e_l[c] = 0.0;
+
+  for (int fn = 0; fn < 4; ++fn) {
+    const int col = wc * 64 + fn * 16 + (lane & 15);
+    const bool cvalid = (j0 + col) < m;
+    double uj[DT];
+#pragma unroll
+    for (int c = 0; c < DT; ++c) uj[c] = (c < d) ? s_uc[col * d + c] : 0.0;
+    const double ucol = s_u[col];
+    const double cd = s_cd[col];
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
+        const bool valid = cvalid && ((i0 + row) < n);
+        const double G = fma(s_alpha[row], ucol, acc[fm][fn][q]);
+        const double* xr = &s_x[row * d];
+        double s = 0.0;
+        bool eq = true;
+#pragma unroll
+        for (int c = 0; c < DT; ++c) {
+          if (c < d) {
+            const double dc = xr[c] - uj[c];
+            eq = eq && (dc == 0.0);
+            const double tc = ard ? dc * s_rl[c] : dc;
+            s = fma(tc, tc, s);
+          }
+        }
+        const double kv = ard ? sig2 * exp(-s / 2.0) : sig2 * exp(coef * s);
+        const double gk = valid ? G * kv : 0.0;
+        e_sig += gk;
+        if (ard) {
+#pragma unroll
+          for (int c = 0; c < DT; ++c) {
+            if (c < d) {
+              const double tc = (xr[c] - uj[c]) * s_rl[c];
+              e_l[c] = fma(gk, tc * tc, e_l[c]);
+            }
+          }
+        } else {
+          e_l[0] = fma(gk, s * rl2s, e_l[0]);
+        }
+        if (valid && eq) {
+          c_sum += G;
+          c_cnt += 1.0;
+          c_dg += cd;
+        }
+      }
+  }
+
+  // record = [e_sig, e_l[0..L-1], c_sum, c_cnt, c_dg]
+  double v;
+  v = wave_sum(e_sig);
+  if (lane == 0) red[wv][0] = v;
+#pragma unroll
+  for (int c = 0; c < DT; ++c) {
+    if (c < L) {
+      v = wave_sum(e_l[c]);
+      if (lane == 0) red[wv][1 + c] = v;
+    }
+  }
+  v = wave_sum(c_sum);
+  if (lane == 0) red[wv][1 + L] = v;
+  v = wave_sum(c_cnt);
+  if (lane == 0) red[wv][2 + L] = v;
+  v = wave_sum(c_dg);
+  if (lane == 0) red[wv][3 + L] = v;
+  __syncthreads();
+  if (tid < nrec)
+    slab[wgid * nrec + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+}
+
+// ============================================================================ generic 64x64 GEMM
+constexpr int GA = 18;   // [64][16] A image stride
+constexpr int GB = 80;   // [16][64] B image stride: 2*80 % 64 == 32
+template <bool TA, bool TB>
+__global__ void __launch_bounds__(256)
+k_gemm64(int64_t M, int64_t N, int64_t Kd, double alpha, const double* __restrict__ A,
+         int64_t lda, const double* __restrict__ B, int64_t ldb, double beta,
+         double* C, int64_t ldc, int lower_only) {
+  __shared__ double As[64 * GA];
+  __shared__ double Bs[16 * GB];
+  const int64_t tn = blockIdx.x, tm = blockIdx.y;
+  if (lower_only && tm < tn) return;
+  const int64_t i0 = tm * 64, j0 = tn * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  d4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int64_t k0 = 0; k0 < Kd; k0 += 16) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + q * 256;
+      int row, kk;
+      if (!TA) { row = e >> 4; kk = e & 15; } else { kk = e >> 6; row = e & 63; }
+      const double av = TA ? A[(k0 + kk) * lda + i0 + row] : A[(i0 + row) * lda + k0 + kk];
+      As[row * GA + kk] = av;
+      int col, kb;
+      if (!TB) { kb = e >> 6; col = e & 63; } else { col = e >> 4; kb = e & 15; }
+      const double bv = TB ? B[(j0 + col) * ldb + k0 + kb] : B[(k0 + kb) * ldb + j0 + col];
+      Bs[kb * GB + col] = bv;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int kx = kk * 4 + (lane >> 4);
+      double af[2], bf[2];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        af[f] = As[(wr * 32 + f * 16 + (lane & 15)) * GA + kx];
+        bf[f] = Bs[kx * GB + wc * 32 + f * 16 + (lane & 15)];
+      }
+#pragma unroll
+      for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 2; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = i0 + wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
+        const int64_t col = j0 + wc * 32 + fn * 16 + (lane & 15);
+        double v = alpha * acc[fm][fn][q];
+        if (beta != 0.0) v = fma(beta, C[row * ldc + col], v);
+        C[row * ldc + col] = v;
+      }
+}
+
+struct SyrkPlan {
+  int nb, T, splits;
+  int64_t chunk;
+};
+
+SyrkPlan syrk_plan(int64_t n_pad, int64_t mp) {
+  SyrkPlan p;
+  p.nb = (int)(mp / T128);
+  p.T = p.nb * (p.nb + 1) / 2;
+  int64_t want = (1024 + p.T - 1) / p.T;
+  const int64_t max_splits = n_pad / BK;
+  if (want > max_splits) want = max_splits;
+  if (want < 1) want = 1;
+  int64_t chunk = (n_pad + want - 1) / want;
+  chunk = (chunk + BK - 1) / BK * BK;
+  p.chunk = chunk;
+  p.splits = (int)((n_pad + chunk - 1) / chunk);
+  return p;
+}
+
+}  // namespace
+
+int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp) {
+  SyrkPlan p = syrk_plan(n_pad, mp);
+  return (int64_t)p.splits * p.T * T128 * T128 + (int64_t)p.splits * p.nb * T128 + p.splits;
+}
+
+hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const double* r,
+                           const double* w, double* slab, int64_t slab_cap, double* red,
+                           hipStream_t s) {
+  SyrkPlan p = syrk_plan(n_pad, mp);
+  double* slab_s = slab;
+  double* slab_t = slab_s + (int64_t)p.splits * p.T * T128 * T128;
+  double* slab_rr = slab_t + (int64_t)p.splits * p.nb * T128;
+  if (slab_rr + p.splits > slab + slab_cap) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_syrk, dim3((unsigned)(p.splits * p.T)), dim3(256), 0, s, K, n_pad, mp,
+                     r, w, p.chunk, p.T, p.nb, slab_s, slab_t, slab_rr);
+  hipLaunchKernelGGL(k_syrk_reduce, dim3(T128 * T128 / 256, p.T), dim3(256), 0, s, slab_s,
+                     p.splits, p.T, mp, red);
+  hipLaunchKernelGGL(k_syrk_reduce_t, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s,
+                     slab_t, slab_rr, p.splits, p.nb, mp, red);
+  return hipGetLastError();
+}
+
+hipError_t launch_contract_knm(const KernParams& kp, const double* K, const double* P,
+                               const double* X, int64_t ldx, int64_t n, int64_t n_pad,
+                               const double* U, int64_t ldu, int64_t m, int64_t mp,
+                               const double* alpha, const double* uvec,
+                               const double* coinc_diag, double* slab, int64_t* nrec_out,
+                               int64_t* nwg_out, hipStream_t s) {
+  const int64_t nwg = (n_pad / T128) * (mp / T128);
+  const int nrec = kp.L + 4;
+  *nrec_out = nrec;
+  *nwg_out = nwg;
+  if (kp.d <= 8) {
+    hipLaunchKernelGGL(k_contract<8>, dim3((unsigned)nwg), dim3(256), 0, s, kp, K, P, X, ldx,
+                       n, n_pad, U, ldu, m, mp, alpha, uvec, coinc_diag, slab, nrec);
+  } else {
+    hipLaunchKernelGGL(k_contract<SGP_MAXD>, dim3((unsigned)nwg), dim3(256), 0, s, kp, K, P, X,
+                       ldx, n, n_pad, U, ldu, m, mp, alpha, uvec, coinc_diag, slab, nrec);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm64(bool transA, bool transB, bool lower_only, int64_t M, int64_t N,
+                         int64_t K, double alpha, const double* A, int64_t lda,
+                         const double* B, int64_t ldb, double beta, double* C, int64_t ldc,
+                         hipStream_t s) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  dim3 grid((unsigned)(N / 64), (unsigned)(M / 64));
+  const int lo = lower_only ? 1 : 0;
+  if (!transA && !transB)
+    hipLaunchKernelGGL((k_gemm64<false, false>), grid, dim3(256), 0, s, M, N, K, alpha, A, lda,
+                       B, ldb, beta, C, ldc, lo);
+  else if (!transA && transB)
+    hipLaunchKernelGGL((k_gemm64<false, true>), grid, dim3(256), 0, s, M, N, K, alpha, A, lda, B,
+                       ldb, beta, C, ldc, lo);
+  else if (transA && !transB)
+    hipLaunchKernelGGL((k_gemm64<true, false>), grid, dim3(256), 0, s, M, N, K, alpha, A, lda, B,
+                       ldb, beta, C, ldc, lo);
+  else
+    hipLaunchKernelGGL((k_gemm64<true, true>), grid, dim3(256), 0, s, M, N, K, alpha, A, lda, B,
+                       ldb, beta, C, ldc, lo);
+  return hipGetLastError();
+}

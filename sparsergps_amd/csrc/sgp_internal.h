@@ -1,0 +1,107 @@
+// Internal declarations shared by the HIP translation units of libsgp.so.
+// Device code targets gfx950 (MI355X / CDNA4) only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SGP_MAXD 32          // largest input dimension d supported by the fused kernels
+#define SGP_TILE 128         // n x m tile edge of the MFMA kernels (rows and knots padded to it)
+#define SGP_DB 64            // block edge of the m x m dense routines
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// Covariance-function parameters in the form the kernels use.
+//   sqexp: K = sig2 * exp(coef * sum_c d_c^2),            coef = -1/(2 l^2)
+//   ard:   K = sig2 * exp(-0.5 * sum_c (d_c * rl_c)^2),    rl_c = 1/l_c
+//   exp:   K = sig2 * exp(coef * sum_c |d_c|),             coef = -1/l
+// d_c = x_c - u_c on the raw coordinates (so exact coincidence stays exact).
+struct KernParams {
+  int kernel;            // 0 sqexp, 1 ard, 2 exp
+  int d;
+  int L;                 // number of length scales: 1 or d
+  int P;                 // number of hyperparameters: L + 2
+  double sigma, sig2, tau, tau2, delta;
+  double coef;
+  double l[SGP_MAXD];
+  double rl[SGP_MAXD];   // 1/l_c (sqexp/exp: rl[0] = 1/l)
+  double rl2[SGP_MAXD];  // 1/l_c^2
+};
+
+// ---------------------------------------------------------------- k_cov.hip
+// Layer-1 fillers, column-major output (R layout).  x/xp are column-major on device.
+hipError_t launch_fill_cov(const KernParams& kp, const double* x, int64_t n, int64_t ldx,
+                           const double* xp, int64_t np, int64_t ldxp, bool sym, double* out,
+                           int64_t ldo, hipStream_t s);
+hipError_t launch_fill_dcov(const KernParams& kp, const double* x, int64_t n, int64_t ldx,
+                            const double* xp, int64_t np, int64_t ldxp, bool sym, int param,
+                            double* out, int64_t ldo, hipStream_t s);
+// K12 (n_pad x mp, row-major, ld = mp).  Rows >= n and columns >= m are written as 0.
+hipError_t launch_build_knm(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
+                            int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
+                            double* K, hipStream_t s);
+// K22 = Kuu + diag_add on the diagonal, padded with identity (mp x mp, row-major).
+// diag value = ((sig2 + tau2 + delta) - diag_sub) exactly like R's make_cov(...) - tau^2 I.
+hipError_t launch_build_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,
+                            int64_t mp, double diag_sub, double* K22, hipStream_t s);
+// sum_{j,k<m} G22_jk * dK22^p_jk for every parameter p != tau, where
+// G22 = a*u u^T + b*(Ainv - Binv) + c*M3.  Writes P partial sums per block into slab.
+hipError_t launch_contract_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,
+                               int64_t mp, const double* uvec, const double* Ainv,
+                               const double* Binv, const double* M3, double a, double b,
+                               double c, double* slab, int* nblocks, hipStream_t s);
+
+// ---------------------------------------------------------------- k_mfma.hip
+// S_aug partials: S = K^T diag(w) K (lower 128-tiles), t = K^T diag(w) r, rr = r^T diag(w) r.
+// w == nullptr means w = 1.  Writes per-(split,tile) slabs, then reduces into
+// red = [S (mp x mp, full symmetric), t (mp), rr, n_local].
+hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const double* r,
+                           const double* w, double* slab, int64_t slab_cap, double* red,
+                           hipStream_t s);
+int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp);
+// Contraction: G = alpha u^T + K P (K: n_pad x mp, P: mp x mp); accumulates per 128x128 tile
+//   sum G*K, sum G*K*w_l(d) per length scale, and the tau-coincidence sums.
+//   coinc_diag = diag(K22inv) (mp).  Per-tile records go to slab[wgid * nrec].
+hipError_t launch_contract_knm(const KernParams& kp, const double* K, const double* P,
+                               const double* X, int64_t ldx, int64_t n, int64_t n_pad,
+                               const double* U, int64_t ldu, int64_t m, int64_t mp,
+                               const double* alpha, const double* uvec,
+                               const double* coinc_diag, double* slab, int64_t* nrec_out,
+                               int64_t* nwg_out, hipStream_t s);
+// generic m x m GEMM on f64 MFMA: C = alpha*op(A)*op(B) + beta*C, sizes multiples of 64.
+hipError_t launch_gemm64(bool transA, bool transB, bool lower_only, int64_t M, int64_t N,
+                         int64_t K, double alpha, const double* A, int64_t lda,
+                         const double* B, int64_t ldb, double beta, double* C, int64_t ldc,
+                         hipStream_t s);
+
+// ---------------------------------------------------------------- k_dense.hip
+// In-place blocked Cholesky of the lower triangle of A (mp x mp, mp % 64 == 0).
+// dinv receives inverse diagonal blocks (mp/64 blocks of 64x64), logd per-block sums of
+// log(L_ii); status[0] = 0 or (global pivot index + 1) of the first failing pivot.
+hipError_t dense_potrf(double* A, int64_t mp, int64_t lda, double* dinv, double* logd,
+                       int* status, hipStream_t s);
+// X = L^{-1} (lower), using the dinv blocks of dense_potrf.  X must be mp x mp.
+hipError_t dense_trtri(const double* L, int64_t mp, int64_t lda, const double* dinv, double* X,
+                       int64_t ldx, double* T, hipStream_t s);
+// Ainv = X^T X
+hipError_t dense_inv_from_trtri(const double* X, int64_t mp, double* Ainv, hipStream_t s);
+// C = a*A + b*B elementwise over mp x mp
+hipError_t dense_axpby(double a, const double* A, double b, const double* B, double* C,
+                       int64_t count, hipStream_t s);
+// y = scale * A x  (A: mp x mp row-major)
+hipError_t dense_gemv(const double* A, int64_t mp, const double* x, double scale, double* y,
+                      hipStream_t s);
+// alpha_i = (r_i - sum_j K_ij u_j) * invz_i  (invz scalar if invz_vec == nullptr),
+// writes per-block partial sum of alpha_i^2 into slab.
+hipError_t launch_alpha(const double* K, int64_t n_pad, int64_t mp, const double* r,
+                        const double* u, double invz, const double* invz_vec, double* alpha,
+                        double* slab, int* nblocks, hipStream_t s);
+// out[0] = sum_i a_i * b_i over count (b == nullptr: sum a_i); deterministic two-stage.
+hipError_t launch_dot(const double* a, const double* b, int64_t count, double* partial,
+                      double* out, hipStream_t s);
+// out[k] = sum over rows r < nrows of slab[r*ncol + k], k < ncol; deterministic.
+hipError_t launch_colsum(const double* slab, int64_t nrows, int64_t ncol, double* out,
+                         hipStream_t s);
+// diag extraction: out[j] = A[j*lda + j]
+hipError_t launch_diag(const double* A, int64_t mp, int64_t lda, double* out, hipStream_t s);
+// sum of per-block logs -> out
+hipError_t launch_sum_small(const double* v, int64_t count, double* out, hipStream_t s);
