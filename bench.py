@@ -1,0 +1,186 @@
+#!/usr/bin/env python
+"""Benchmark: sparse-GP objective+gradient evals/sec at n=1e6, m=1024, d=8 (BASELINE.json).
+
+One step = one full evaluation of the reference's optimizer-iteration body
+(norm_grad_ascent_vi, R/vi_functions.R:1089-1128): build K12/K22 at (theta, U), the Titsias
+ELBO and its gradient w.r.t. all P = 10 log-hyperparameters (knots fixed), on synthetic C3
+inputs already resident in HBM.  N > 1: the n rows are split into N contiguous blocks (C4),
+one process per GPU, RCCL all-reduce of the two reduction buffers (sparsergps_amd/dist.py);
+total work is fixed, so scaling is "strong".
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N > 1 under torch.distributed.run, one rank per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix peak (AMD spec)
+HBM_PEAK_GBS = 8000.0
+
+
+def make_problem(config, n=None, m=None):
+    """Synthetic inputs of SURVEY.md 8(d) (numpy PCG64 streams); no reference files read."""
+    from oracle.sgp_oracle import make_gaussian_problem  # generator only (data, not the checker)
+    return make_gaussian_problem(config, n=n, m=m)
+
+
+def cpu_baseline(sizes=(500, 1000, 2000), n_target=1_000_000, m=1024):
+    """Time the literal CPU restatement of the reference (oracle/) on row samples of C3 and
+    extrapolate linearly in n (the reference's per-eval cost is a + b*n at fixed m)."""
+    from threadpoolctl import threadpool_info
+
+    from oracle import sgp_oracle as O
+    ts = []
+    for ns in sizes:
+        P = O.make_gaussian_problem("C3", n=ns, m=m)
+        t0 = time.perf_counter()
+        O.elbo_eval(P["cov_par"], "ard", P["U"], P["X"], P["y"], P["mu"], P["delta"])
+        O.delbo_dcov_par(P["cov_par"], "ard", P["U"], P["X"], P["y"], P["mu"], P["delta"])
+        ts.append(time.perf_counter() - t0)
+    A = np.vstack([np.ones(len(sizes)), np.asarray(sizes, dtype=np.float64)]).T
+    (a, b), *_ = np.linalg.lstsq(A, np.asarray(ts), rcond=None)
+    resid = float(np.max(np.abs(A @ np.array([a, b]) - np.asarray(ts))))
+    t_target = a + b * n_target
+    threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    return {
+        "value": 1.0 / t_target,
+        "unit": "evals/s",
+        "cores": int(threads),
+        "kind": "port",
+        "sample": (f"oracle/sgp_oracle.py elbo_eval+delbo_dcov_par (literal restatement of "
+                   f"vi_functions.R, numpy+OpenBLAS) on C3 rows n={list(sizes)}, m={m}, d=8: "
+                   f"t={[round(t, 3) for t in ts]} s; least-squares t(n)=a+b*n, a={a:.3f}s, "
+                   f"b={b:.3e}s/row, max resid {resid:.3f}s; extrapolated to n={n_target}: "
+                   f"{t_target:.1f} s/eval"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C3", choices=["C2", "C3"])
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--m", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    import sparsergps_amd as S
+    from sparsergps_amd.dist import HipRowBackend, RowShardedVI, shard_rows
+
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    P = make_problem(args.config, n=args.n, m=args.m)
+    n, m, d = P["X"].shape[0], P["U"].shape[0], P["X"].shape[1]
+    cov_fun = P["cov_fun"]
+    names = S.param_names(cov_fun, d)
+    theta0 = np.array([P["cov_par"][k] for k in names])
+    s0, s1 = shard_rows(n, world, rank)
+    n_loc = s1 - s0
+
+    backend = HipRowBackend(P["X"][s0:s1], P["y"][s0:s1], P["mu"][s0:s1], m, local_rank, cov_fun)
+    runner = RowShardedVI(backend, n, None)
+    ctx = backend.ctx
+    del P["X"]
+
+    # an optimizer-like trajectory: theta moves every step (no result can be reused)
+    def theta_at(k):
+        return theta0 * np.exp(1e-3 * np.sin(np.arange(theta0.size) + k))
+
+    for k in range(args.warmup):
+        runner.eval(theta_at(k), P["U"], P["delta"])
+
+    ctx.enable_timing(True)
+    phase_ms = {}
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    obj = None
+    for k in range(args.steps):
+        obj, grad = runner.eval(theta_at(args.warmup + k), P["U"], P["delta"])
+        for name, ms in ctx.timings():
+            phase_ms[name] = phase_ms.get(name, 0.0) + ms
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ctx.enable_timing(False)
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    phase_avg = {k: v / args.steps for k, v in phase_ms.items()}
+
+    # roofline of the dominant kernel: fused GEMM + gradient contraction (2 n_loc m^2 MFMA flops)
+    t_con = phase_avg.get("contract_knm", float("nan")) * 1e-3
+    flops = 2.0 * n_loc * m * m
+    achieved = flops / t_con / 1e12 if t_con > 0 else float("nan")
+    traffic = None
+    tp = os.path.join(ROOT, "profiles", "pmc_traffic_contract_knm.json")
+    if os.path.exists(tp):
+        try:
+            rec = json.load(open(tp))
+            if rec.get("n") == n_loc and rec.get("m") == m:
+                traffic = rec.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        out = {
+            "metric": "sparse-GP objective+gradient evals/sec at n=1e6, m=1024, d=8",
+            "value": args.steps / elapsed,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SURVEY.md 8(d) C3 generator: X,U~U(0,10)^8, y=sum sin(x)/sqrt(8)+N(0,.25))",
+            "config": {"workload": f"{args.config}: Titsias VI ELBO + gradient, n={n}, m={m}, d={d}, "
+                                   f"{cov_fun}, P={len(names)}, knots fixed",
+                       "n": n, "m": m, "d": d, "kernel": cov_fun,
+                       "parallelism": f"rows{world}" if world > 1 else "single"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
+                         "traffic": traffic, "kernel": "contract_knm (k_contract<8>)",
+                         "flops_per_launch": flops},
+            "phases_ms": {k: round(v, 4) for k, v in phase_avg.items()},
+            "objective": obj,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    backend.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

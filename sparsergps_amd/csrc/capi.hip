@@ -517,11 +517,16 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
     HIPCHK(launch_build_knm(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp, m, c->mp, c->K,
                             c->stream));
   }
+  HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_vi_red1_count(m), c->stream));
   {
     Scope t(c, "syrk");
-    HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_vi_red1_count(m), c->stream));
     HIPCHK(launch_syrk_aug(c->K, c->n_pad, c->mp, c->r, nullptr, c->slab_syrk,
-                           c->slab_syrk_cap, red1, c->stream));
+                           c->slab_syrk_cap, red1, c->stream, 1));
+  }
+  {
+    Scope t(c, "syrk_reduce");
+    HIPCHK(launch_syrk_aug(c->K, c->n_pad, c->mp, c->r, nullptr, c->slab_syrk,
+                           c->slab_syrk_cap, red1, c->stream, 2));
   }
   c->phase = 1;
   return SGP_OK;
@@ -592,12 +597,15 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
                         c->slab_small, &nb, c->stream));
     HIPCHK(launch_colsum(c->slab_small, nb, 1, red2, c->stream));
   }
+  int64_t nrec = 0, nwg = 0;
   {
     Scope tm(c, "contract_knm");
-    int64_t nrec = 0, nwg = 0;
     HIPCHK(launch_contract_knm(kp, c->K, c->Pm, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp,
                                c->m, mp, c->alpha, c->uvec, c->cdiag, c->slab_con, &nrec, &nwg,
                                c->stream));
+  }
+  {
+    Scope tm(c, "contract_reduce");
     HIPCHK(launch_colsum(c->slab_con, nwg, nrec, red2 + 1, c->stream));
   }
   c->phase = 2;

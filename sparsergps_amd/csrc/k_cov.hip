@@ -98,30 +98,46 @@ __global__ void __launch_bounds__(256) k_fill(KernParams kp, const double* __res
 }
 
 // K12 row-major (n_pad x mp).  Block: 64 knot columns (lanes) x 4 row groups; each block
-// owns 64 rows.  Row coordinates are staged in LDS and broadcast; knots stay in registers.
+// owns 64 rows.  Row coordinates (pre-scaled by 1/l_c for ARD) are staged in LDS and read as
+// wave-wide broadcasts; the lane's knot stays in registers; one coalesced 512-B store per row.
+template <bool ARD, int DT>
 __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* __restrict__ X,
                                                    int64_t ldx, int64_t n,
                                                    const double* __restrict__ U, int64_t ldu,
                                                    int64_t m, int64_t mp,
                                                    double* __restrict__ K) {
-  __shared__ double xs[64 * SGP_MAXD];
+  __shared__ __attribute__((aligned(16))) double xs[64 * DT];
   const int d = kp.d;
   const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
   const int64_t i0 = (int64_t)blockIdx.y * 64;
   const int tid = threadIdx.y * 64 + threadIdx.x;
-  for (int e = tid; e < 64 * d; e += 256) {
-    const int r = e % 64, c = e / 64;
+  for (int e = tid; e < 64 * DT; e += 256) {
+    const int r = e / DT, c = e % DT;
     const int64_t i = i0 + r;
-    xs[r * d + c] = (i < n) ? X[i + c * ldx] : 0.0;
+    double v = 0.0;
+    if (c < d && i < n) v = ARD ? X[i + c * ldx] * kp.rl[c] : X[i + c * ldx];
+    xs[e] = v;
   }
-  double uj[SGP_MAXD];
+  double uj[DT];
   const bool jv = j < m;
-  for (int c = 0; c < d; ++c) uj[c] = jv ? U[j + c * ldu] : 0.0;
+#pragma unroll
+  for (int c = 0; c < DT; ++c)
+    uj[c] = (jv && c < d) ? (ARD ? U[j + c * ldu] * kp.rl[c] : U[j + c * ldu]) : 0.0;
+  const double sig2 = kp.sig2;
+  const double scale = ARD ? -0.5 : kp.coef;
   __syncthreads();
   for (int r = threadIdx.y; r < 64; r += 4) {
     const int64_t i = i0 + r;
-    double v = 0.0;
-    if (jv && i < n) v = kvalue(kp, &xs[r * d], uj);
+    const double2* xr = reinterpret_cast<const double2*>(&xs[r * DT]);
+    double s = 0.0;
+#pragma unroll
+    for (int c2 = 0; c2 < DT / 2; ++c2) {
+      const double2 xv = xr[c2];
+      const double t0 = xv.x - uj[2 * c2], t1 = xv.y - uj[2 * c2 + 1];
+      s = fma(t0, t0, s);
+      s = fma(t1, t1, s);
+    }
+    const double v = (jv && i < n) ? sig2 * sgp_exp_nonpos(scale * s) : 0.0;
     K[i * mp + j] = v;
   }
 }
@@ -221,7 +237,15 @@ hipError_t launch_build_knm(const KernParams& kp, const double* X, int64_t ldx, 
                             int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
                             double* K, hipStream_t s) {
   dim3 grid((unsigned)(mp / 64), (unsigned)(n_pad / 64));
-  hipLaunchKernelGGL(k_build_knm, grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K);
+  const bool ard = kp.kernel == 1;
+  if (kp.kernel == 2) return hipErrorInvalidValue;
+  if (kp.d <= 8) {
+    if (ard) hipLaunchKernelGGL((k_build_knm<true, 8>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K);
+    else hipLaunchKernelGGL((k_build_knm<false, 8>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K);
+  } else {
+    if (ard) hipLaunchKernelGGL((k_build_knm<true, SGP_MAXD>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K);
+    else hipLaunchKernelGGL((k_build_knm<false, SGP_MAXD>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K);
+  }
   return hipGetLastError();
 }
 

@@ -30,64 +30,101 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
   return t;
 }
 
-// Factor the 64x64 diagonal block kb of A in LDS; write L (lower) back, inv(L) to dinv,
-// sum log(L_ii) to logd[kb].  First failing pivot -> status = global index + 1.
+// Factor the 64x64 diagonal block kb of A and invert its factor in ONE right-looking pass.
+// Thread t owns the 4x4 register blocks (bi, bj) = (t>>4, t&15) of both L (in place of A) and
+// X = L^{-1}; column k of A and row k of X are broadcast through double-buffered LDS, so each
+// of the 64 steps costs a single barrier.  Writes L (lower) back, X to dinv, sum log(L_ii) to
+// logd[kb]; the first failing pivot sets status = global index + 1 (R's chol() error).
 __global__ void __launch_bounds__(256) k_potrf_diag(double* A, int64_t lda, int kb,
                                                     double* __restrict__ dinv,
                                                     double* __restrict__ logd,
                                                     int* __restrict__ status) {
-  __shared__ double a[64][65];
-  __shared__ double x[64][65];
+  __shared__ double colv[2][64];
+  __shared__ double xrow[2][64];
+  __shared__ double piv_s[64];
+  __shared__ double red[4];
   const int tid = threadIdx.x;
+  const int bi = tid >> 4, bj = tid & 15;
+  const bool lower = bi >= bj;
   const int64_t o = (int64_t)kb * 64;
-  for (int e = tid; e < 64 * 64; e += 256) {
-    const int i = e >> 6, j = e & 63;
-    a[i][j] = (j <= i) ? A[(o + i) * lda + o + j] : 0.0;
-    x[i][j] = 0.0;
-  }
-  __syncthreads();
-  for (int k = 0; k < 64; ++k) {
-    if (tid == 0) {
-      double p = a[k][k];
-      if (!(p > 0.0) || !isfinite(p)) {
-        atomicCAS(status, 0, (int)(o + k + 1));
+  double a[4][4], x[4][4];
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int i = 4 * bi + ii, j = 4 * bj + jj;
+      a[ii][jj] = (lower && j <= i) ? A[(o + i) * lda + o + j] : 0.0;
+      x[ii][jj] = (i == j) ? 1.0 : 0.0;
+    }
+  for (int kb4 = 0; kb4 < 16; ++kb4) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int k = 4 * kb4 + kk;
+      const int b = k & 1;
+      // publish column k of A (rows >= k) and row k of X (cols <= k)
+      if (bj == kb4 && bi >= kb4) {
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) colv[b][4 * bi + ii] = a[ii][kk];
       }
-      a[k][k] = sqrt(p);
+      if (bi == kb4 && bj <= kb4) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) xrow[b][4 * bj + jj] = x[kk][jj];
+      }
+      __syncthreads();
+      const double p2 = colv[b][k];
+      const double piv = sqrt(p2);
+      const double rp = 1.0 / piv;
+      if (tid == 0) {
+        piv_s[k] = piv;
+        if (!(p2 > 0.0) || !isfinite(p2)) atomicCAS(status, 0, (int)(o + k + 1));
+      }
+      if (lower) {
+        double li[4], lj[4], xk[4];
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) li[ii] = colv[b][4 * bi + ii] * rp;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          lj[jj] = colv[b][4 * bj + jj] * rp;
+          xk[jj] = xrow[b][4 * bj + jj] * rp;
+        }
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+          const int i = 4 * bi + ii;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * bj + jj;
+            if (i > k && j > k && j <= i) a[ii][jj] = fma(-li[ii], lj[jj], a[ii][jj]);
+            if (j == k && i > k) a[ii][jj] = li[ii];
+            if (j == k && i == k) a[ii][jj] = piv;
+            if (i == k && j <= k) x[ii][jj] = xk[jj];
+            if (i > k && j <= k) x[ii][jj] = fma(-li[ii], xk[jj], x[ii][jj]);
+          }
+        }
+      }
     }
-    __syncthreads();
-    const double piv = a[k][k];
-    if (tid < 63 - k) a[k + 1 + tid][k] /= piv;
-    __syncthreads();
-    const int rem = 63 - k;
-    for (int e = tid; e < rem * rem; e += 256) {
-      const int i = k + 1 + e / rem, j = k + 1 + e % rem;
-      if (j <= i) a[i][j] -= a[i][k] * a[j][k];
-    }
-    __syncthreads();
   }
-  for (int e = tid; e < 64 * 64; e += 256) {
-    const int i = e >> 6, j = e & 63;
-    if (j <= i) A[(o + i) * lda + o + j] = a[i][j];
-  }
-  if (tid == 0) {
-    double s = 0.0;
-    for (int k = 0; k < 64; ++k) s += log(a[k][k]);
-    logd[kb] = s;
-  }
-  // triangular inverse by rows: x[i][j] = -(sum_{k=j}^{i-1} a[i][k] x[k][j]) / a[i][i]
-  const int jj = tid >> 2, part = tid & 3;
-  for (int i = 0; i < 64; ++i) {
-    double s = 0.0;
-    if (jj < i)
-      for (int k = jj + part; k < i; k += 4) s = fma(a[i][k], x[k][jj], s);
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    if (part == 0 && jj < i) x[i][jj] = -s / a[i][i];
-    if (tid == 0) x[i][i] = 1.0 / a[i][i];
-    __syncthreads();
+  if (lower) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int i = 4 * bi + ii, j = 4 * bj + jj;
+        if (j <= i) A[(o + i) * lda + o + j] = a[ii][jj];
+      }
   }
   double* D = dinv + (int64_t)kb * 64 * 64;
-  for (int e = tid; e < 64 * 64; e += 256) D[e] = x[e >> 6][e & 63];
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int i = 4 * bi + ii, j = 4 * bj + jj;
+      D[i * 64 + j] = (lower && j <= i) ? x[ii][jj] : 0.0;
+    }
+  __syncthreads();
+  double lg = (tid < 64) ? log(piv_s[tid]) : 0.0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) lg += __shfl_xor(lg, off, 64);
+  if (tid == 0) logd[kb] = lg;
 }
 
 __global__ void __launch_bounds__(256) k_copy_block(const double* __restrict__ src,

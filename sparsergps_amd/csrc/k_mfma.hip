@@ -66,7 +66,6 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
   while (ta * (ta + 1) / 2 > tile) --ta;
   const int tb = tile - ta * (ta + 1) / 2;
   const bool diag = (ta == tb);
-  const bool sepB = !diag || (w != nullptr);
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wr = wv >> 1, wc = wv & 1;
@@ -83,44 +82,48 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
 
   // loader mapping: 16 rows x 128 cols, 8 doubles per thread
   const int lrow = tid >> 4, lcol = (tid & 15) * 8;
-  const double* gA = K + ta * (int64_t)T128 + lcol;
-  const double* gB = K + tb * (int64_t)T128 + lcol;
-  double2 va[4], vb[4];
-  double vr = 0.0;
+  const double2* gA = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + ta * (int64_t)T128 + lcol);
+  const double2* gB = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + tb * (int64_t)T128 + lcol);
+  const int64_t gstep = BK * mp / 2;   // double2 stride of one k-step
+  double2 va0, va1, va2, va3, vb0, vb1, vb2, vb3;
+  double vr = 0.0, wi = 1.0;
   double tacc = 0.0;  // t partial for column (tid) when diag
   if (tid == 0) rr_acc = 0.0;
 
-  auto gload = [&](int step) {
-    const int64_t row = rbeg + (int64_t)step * BK + lrow;
-    load8(gA + row * mp, va);
-    if (sepB) load8(gB + row * mp, vb);
-    if (tid < BK) {
-      const int64_t rr = rbeg + (int64_t)step * BK + tid;
-      const double rv = r[rr];
-      vr = (w != nullptr) ? w[rr] * rv : rv;
-    }
-  };
-  auto sstore = [&](int buf, int step) {
-    if (w != nullptr) {
-      const double wi = w[rbeg + (int64_t)step * BK + lrow];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) { va[q].x *= wi; va[q].y *= wi; }
-    }
-    store8(&Ka[buf][lrow * SB + lcol], va);
-    if (sepB) store8(&Kb[buf][lrow * SB + lcol], vb);
-    if (tid < BK) rw[buf][tid] = vr;
-  };
+#define SYRK_GLOAD(step)                                                        \
+  {                                                                             \
+    const int64_t o_ = (int64_t)(step) * gstep;                                 \
+    va0 = gA[o_]; va1 = gA[o_ + 1]; va2 = gA[o_ + 2]; va3 = gA[o_ + 3];         \
+    vb0 = gB[o_]; vb1 = gB[o_ + 1]; vb2 = gB[o_ + 2]; vb3 = gB[o_ + 3];         \
+    if (w != nullptr) wi = w[rbeg + (int64_t)(step) * BK + lrow];               \
+    if (tid < BK) {                                                             \
+      const int64_t rr_ = rbeg + (int64_t)(step) * BK + tid;                    \
+      const double rv_ = r[rr_];                                                \
+      vr = (w != nullptr) ? w[rr_] * rv_ : rv_;                                 \
+    }                                                                           \
+  }
+#define SYRK_SSTORE(buf)                                                        \
+  {                                                                             \
+    double2* pa_ = reinterpret_cast<double2*>(&Ka[buf][lrow * SB + lcol]);      \
+    double2* pb_ = reinterpret_cast<double2*>(&Kb[buf][lrow * SB + lcol]);      \
+    pa_[0] = make_double2(va0.x * wi, va0.y * wi);                              \
+    pa_[1] = make_double2(va1.x * wi, va1.y * wi);                              \
+    pa_[2] = make_double2(va2.x * wi, va2.y * wi);                              \
+    pa_[3] = make_double2(va3.x * wi, va3.y * wi);                              \
+    pb_[0] = vb0; pb_[1] = vb1; pb_[2] = vb2; pb_[3] = vb3;                     \
+    if (tid < BK) rw[buf][tid] = vr;                                            \
+  }
 
   if (nsteps > 0) {
-    gload(0);
-    sstore(0, 0);
+    SYRK_GLOAD(0);
+    SYRK_SSTORE(0);
   }
   __syncthreads();
   for (int step = 0; step < nsteps; ++step) {
     const int cur = step & 1;
-    if (step + 1 < nsteps) gload(step + 1);
+    if (step + 1 < nsteps) SYRK_GLOAD(step + 1);
     const double* As = Ka[cur];
-    const double* Bs = sepB ? Kb[cur] : Ka[cur];
+    const double* Bs = Kb[cur];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int krow = kk * 4 + (lane >> 4);
@@ -138,9 +141,8 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
     }
     if (diag && tid < T128) {
       // t_a += sum_i (w_i r_i) K_ia over this step's rows (unscaled operand image)
-      const double* Bu = sepB ? Kb[cur] : Ka[cur];
 #pragma unroll
-      for (int q = 0; q < BK; ++q) tacc = fma(rw[cur][q], Bu[q * SB + tid], tacc);
+      for (int q = 0; q < BK; ++q) tacc = fma(rw[cur][q], Bs[q * SB + tid], tacc);
     }
     if (diag && ta == 0 && tid == 255) {
       double s = 0.0;
@@ -150,9 +152,11 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
       }
       rr_acc += s;
     }
-    if (step + 1 < nsteps) sstore(cur ^ 1, step + 1);
+    if (step + 1 < nsteps) SYRK_SSTORE(cur ^ 1);
     __syncthreads();
   }
+#undef SYRK_GLOAD
+#undef SYRK_SSTORE
 
   double* out = slab_s + ((int64_t)split * T + tile) * (T128 * T128);
 #pragma unroll
@@ -234,30 +238,35 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
 
   // A loader: 128 rows x 16 k, thread -> (row = tid>>1, 8 doubles at (tid&1)*8)
   const int arow = tid >> 1, acol = (tid & 1) * 8;
-  const double* gA = K + (i0 + arow) * mp + acol;
+  const double2* gA = reinterpret_cast<const double2*>(K + (i0 + arow) * mp + acol);
   // B loader: 16 k x 128 cols, thread -> (k = tid>>4, 8 doubles at (tid&15)*8)
   const int bk = tid >> 4, bcol = (tid & 15) * 8;
-  const double* gB = P + (int64_t)bk * mp + j0 + bcol;
-  double2 va[4], vb[4];
+  const double2* gB = reinterpret_cast<const double2*>(P + (int64_t)bk * mp + j0 + bcol);
+  const int64_t bstep = BK * mp / 2;
+  double2 va0, va1, va2, va3, vb0, vb1, vb2, vb3;
   const int nsteps = (int)(mp / BK);
 
-  auto gload = [&](int step) {
-    load8(gA + (int64_t)step * BK, va);
-    load8(gB + (int64_t)step * BK * mp, vb);
-  };
-  auto sstore = [&](int buf) {
-    double* As = lds + buf * (A_SZ + B_SZ);
-    double* Bs = As + A_SZ;
-    store8(&As[arow * SA + acol], va);
-    store8(&Bs[bk * SB + bcol], vb);
-  };
+#define CON_GLOAD(step)                                                          \
+  {                                                                              \
+    const int64_t oa_ = (int64_t)(step) * (BK / 2), ob_ = (int64_t)(step) * bstep; \
+    va0 = gA[oa_]; va1 = gA[oa_ + 1]; va2 = gA[oa_ + 2]; va3 = gA[oa_ + 3];      \
+    vb0 = gB[ob_]; vb1 = gB[ob_ + 1]; vb2 = gB[ob_ + 2]; vb3 = gB[ob_ + 3];      \
+  }
+#define CON_SSTORE(buf)                                                          \
+  {                                                                              \
+    double* As_ = lds + (buf) * (A_SZ + B_SZ);                                   \
+    double2* pa_ = reinterpret_cast<double2*>(&As_[arow * SA + acol]);           \
+    double2* pb_ = reinterpret_cast<double2*>(&As_[A_SZ + bk * SB + bcol]);      \
+    pa_[0] = va0; pa_[1] = va1; pa_[2] = va2; pa_[3] = va3;                      \
+    pb_[0] = vb0; pb_[1] = vb1; pb_[2] = vb2; pb_[3] = vb3;                      \
+  }
 
-  gload(0);
-  sstore(0);
+  CON_GLOAD(0);
+  CON_SSTORE(0);
   __syncthreads();
   for (int step = 0; step < nsteps; ++step) {
     const int cur = step & 1;
-    if (step + 1 < nsteps) gload(step + 1);
+    if (step + 1 < nsteps) CON_GLOAD(step + 1);
     const double* As = lds + cur * (A_SZ + B_SZ);
     const double* Bs = As + A_SZ;
 #pragma unroll
@@ -275,88 +284,87 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
         for (int fn = 0; fn < 4; ++fn)
           acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
     }
-    if (step + 1 < nsteps) sstore(cur ^ 1);
+    if (step + 1 < nsteps) CON_SSTORE(cur ^ 1);
     __syncthreads();
   }
+#undef CON_GLOAD
+#undef CON_SSTORE
 
   // ---------------- epilogue: G = alpha u^T + acc; contract with dK/dlog(theta) ----------
+  // K_ij is read back from HBM (built once by k_build_knm; same values the GEMM used);
+  // coordinates are pre-scaled by 1/l_c (ARD) so each length-scale weight is one sub + mul.
   const int d = kp.d;
   const bool ard = (kp.kernel == 1);
-  const double sig2 = kp.sig2, coef = kp.coef, rl2s = kp.rl2[0];
+  const double rl2s = kp.rl2[0];
   double* s_alpha = lds;                    // 128
   double* s_u = s_alpha + T128;             // 128
   double* s_cd = s_u + T128;                // 128
-  double* s_rl = s_cd + T128;               // SGP_MAXD
-  double* s_x = s_rl + SGP_MAXD;            // 128 x d   (row-major [row][c])
-  double* s_uc = s_x + T128 * d;            // 128 x d
+  double* s_xs = s_cd + T128;               // 128 x d   ([row][c], scaled)
+  double* s_us = s_xs + T128 * d;           // 128 x d   ([col][c], scaled)
   for (int e = tid; e < T128; e += 256) {
     s_alpha[e] = alpha[i0 + e];
     const int64_t j = j0 + e;
     s_u[e] = (j < m) ? uvec[j] : 0.0;
     s_cd[e] = (j < m) ? cdiag[j] : 0.0;
   }
-  if (tid < SGP_MAXD) s_rl[tid] = (tid < d) ? kp.rl[tid] : 0.0;
   for (int e = tid; e < T128 * d; e += 256) {
     const int rr = e % T128, c = e / T128;
     const int64_t i = i0 + rr, j = j0 + rr;
-    s_x[rr * d + c] = (i < n) ? X[i + c * ldx] : 0.0;
-    s_uc[rr * d + c] = (j < m) ? U[j + c * ldu] : 0.0;
+    const double sc = ard ? kp.rl[c] : 1.0;
+    s_xs[rr * d + c] = (i < n) ? X[i + c * ldx] * sc : 0.0;
+    s_us[rr * d + c] = (j < m) ? U[j + c * ldu] * sc : 0.0;
   }
   __syncthreads();
 
   const int L = kp.L;
+  const double* Kt = K + i0 * mp + j0;
   double e_sig = 0.0, c_sum = 0.0, c_cnt = 0.0, c_dg = 0.0;
   double e_l[DT];
 #pragma unroll
   for (int c = 0; c < DT; ++c) e_l[c] = 0.0;
 
+#pragma unroll
   for (int fn = 0; fn < 4; ++fn) {
     const int col = wc * 64 + fn * 16 + (lane & 15);
     const bool cvalid = (j0 + col) < m;
     double uj[DT];
 #pragma unroll
-    for (int c = 0; c < DT; ++c) uj[c] = (c < d) ? s_uc[col * d + c] : 0.0;
+    for (int c = 0; c < DT; ++c) uj[c] = (c < d) ? s_us[col * d + c] : 0.0;
     const double ucol = s_u[col];
-    const double cd = s_cd[col];
 #pragma unroll
-    for (int fm = 0; fm < 4; ++fm)
+    for (int fm = 0; fm < 4; ++fm) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
         const bool valid = cvalid && ((i0 + row) < n);
         const double G = fma(s_alpha[row], ucol, acc[fm][fn][q]);
-        const double* xr = &s_x[row * d];
+        const double gk = valid ? G * Kt[(int64_t)row * mp + col] : 0.0;
+        e_sig += gk;
+        const double* xr = &s_xs[row * d];
         double s = 0.0;
-        bool eq = true;
 #pragma unroll
         for (int c = 0; c < DT; ++c) {
           if (c < d) {
-            const double dc = xr[c] - uj[c];
-            eq = eq && (dc == 0.0);
-            const double tc = ard ? dc * s_rl[c] : dc;
-            s = fma(tc, tc, s);
+            const double t = xr[c] - uj[c];
+            const double tt = t * t;
+            s += tt;
+            if (ard) e_l[c] = fma(gk, tt, e_l[c]);
           }
         }
-        const double kv = ard ? sig2 * exp(-s / 2.0) : sig2 * exp(coef * s);
-        const double gk = valid ? G * kv : 0.0;
-        e_sig += gk;
-        if (ard) {
-#pragma unroll
-          for (int c = 0; c < DT; ++c) {
-            if (c < d) {
-              const double tc = (xr[c] - uj[c]) * s_rl[c];
-              e_l[c] = fma(gk, tc * tc, e_l[c]);
-            }
+        if (!ard) e_l[0] = fma(gk, s * rl2s, e_l[0]);
+        if (valid && s == 0.0) {
+          // rare path: tau's dK12 rule needs all(x_i == u_j) on the raw coordinates
+          bool eq = true;
+          for (int c = 0; c < d; ++c) eq = eq && (X[(i0 + row) + c * ldx] == U[(j0 + col) + c * ldu]);
+          if (eq) {
+            c_sum += G;
+            c_cnt += 1.0;
+            c_dg += s_cd[col];
           }
-        } else {
-          e_l[0] = fma(gk, s * rl2s, e_l[0]);
-        }
-        if (valid && eq) {
-          c_sum += G;
-          c_cnt += 1.0;
-          c_dg += cd;
         }
       }
+    }
+    __builtin_amdgcn_sched_barrier(0);
   }
 
   // record = [e_sig, e_l[0..L-1], c_sum, c_cnt, c_dg]
@@ -452,14 +460,24 @@ struct SyrkPlan {
 };
 
 SyrkPlan syrk_plan(int64_t n_pad, int64_t mp) {
+  // One resident "round" = 256 CUs x 2 workgroups (216 VGPRs, 74 KB LDS each).  Pick the
+  // split count so splits * T fills an integer number of rounds as fully as possible.
+  constexpr int64_t kSlots = 512;
   SyrkPlan p;
   p.nb = (int)(mp / T128);
   p.T = p.nb * (p.nb + 1) / 2;
-  int64_t want = (1024 + p.T - 1) / p.T;
-  const int64_t max_splits = n_pad / BK;
-  if (want > max_splits) want = max_splits;
-  if (want < 1) want = 1;
-  int64_t chunk = (n_pad + want - 1) / want;
+  const int64_t max_splits = n_pad / BK > 0 ? n_pad / BK : 1;
+  int64_t best = 1;
+  double best_fill = 0.0;
+  for (int64_t rounds = 1; rounds <= 4; ++rounds) {
+    int64_t sp = rounds * kSlots / p.T;
+    if (sp < 1) sp = 1;
+    if (sp > max_splits) sp = max_splits;
+    const double fill = (double)(sp * p.T) / (double)(((sp * p.T + kSlots - 1) / kSlots) * kSlots);
+    if (fill > best_fill + 1e-9) { best_fill = fill; best = sp; }
+    if (best_fill >= 0.95) break;
+  }
+  int64_t chunk = (n_pad + best - 1) / best;
   chunk = (chunk + BK - 1) / BK * BK;
   p.chunk = chunk;
   p.splits = (int)((n_pad + chunk - 1) / chunk);
@@ -475,18 +493,21 @@ int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp) {
 
 hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const double* r,
                            const double* w, double* slab, int64_t slab_cap, double* red,
-                           hipStream_t s) {
+                           hipStream_t s, int part) {
   SyrkPlan p = syrk_plan(n_pad, mp);
   double* slab_s = slab;
   double* slab_t = slab_s + (int64_t)p.splits * p.T * T128 * T128;
   double* slab_rr = slab_t + (int64_t)p.splits * p.nb * T128;
   if (slab_rr + p.splits > slab + slab_cap) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_syrk, dim3((unsigned)(p.splits * p.T)), dim3(256), 0, s, K, n_pad, mp,
-                     r, w, p.chunk, p.T, p.nb, slab_s, slab_t, slab_rr);
-  hipLaunchKernelGGL(k_syrk_reduce, dim3(T128 * T128 / 256, p.T), dim3(256), 0, s, slab_s,
-                     p.splits, p.T, mp, red);
-  hipLaunchKernelGGL(k_syrk_reduce_t, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s,
-                     slab_t, slab_rr, p.splits, p.nb, mp, red);
+  if (part & 1)
+    hipLaunchKernelGGL(k_syrk, dim3((unsigned)(p.splits * p.T)), dim3(256), 0, s, K, n_pad, mp,
+                       r, w, p.chunk, p.T, p.nb, slab_s, slab_t, slab_rr);
+  if (part & 2) {
+    hipLaunchKernelGGL(k_syrk_reduce, dim3(T128 * T128 / 256, p.T), dim3(256), 0, s, slab_s,
+                       p.splits, p.T, mp, red);
+    hipLaunchKernelGGL(k_syrk_reduce_t, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s,
+                       slab_t, slab_rr, p.splits, p.nb, mp, red);
+  }
   return hipGetLastError();
 }
 
