@@ -99,7 +99,7 @@ typedef struct sgp_ctx sgp_ctx;
 int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_t ldx, int d,
                    const double* y, const double* mu, int64_t m_max);
 int sgp_ctx_destroy(sgp_ctx* ctx);
-/* launch on this hipStream_t (NULL = the context's own stream) */
+/* launch on this hipStream_t; NULL selects the context's own (non-blocking) stream */
 int sgp_ctx_set_stream(sgp_ctx* ctx, void* hip_stream);
 /* replace y / mu (e.g. Laplace pseudo-data); host buffers of length n */
 int sgp_ctx_set_data(sgp_ctx* ctx, const double* y, const double* mu);

@@ -14,6 +14,8 @@ tests (tests/test_dist.py).
 """
 from __future__ import annotations
 
+import contextlib
+
 import numpy as np
 
 
@@ -39,8 +41,14 @@ class HipRowBackend:
         self.red1 = torch.zeros(self.ctx.vi_red1_count(m_max), dtype=torch.float64, device=self.dev)
         self.red2 = torch.zeros(self.ctx.vi_red2_count(cov_fun), dtype=torch.float64, device=self.dev)
         self.nparams = self.red2.numel() - 3
-        # launch on torch's current stream so RCCL collectives are ordered with our kernels
-        self.ctx.set_stream(torch.cuda.current_stream(self.dev).cuda_stream)
+        # A dedicated (non-null) stream shared by libsgp's launches and torch.distributed:
+        # RowShardedVI issues its collectives under stream_context(), so every all-reduce is
+        # ordered after the kernels that produced its buffer, with no host synchronisation.
+        self.stream = torch.cuda.Stream(device=self.dev)
+        self.ctx.set_stream(self.stream.cuda_stream)
+
+    def stream_context(self):
+        return self.torch.cuda.stream(self.stream)
 
     def phase1(self, theta, U, delta):
         n1 = self.ctx.vi_red1_count(np.asarray(U).shape[0])
@@ -72,10 +80,11 @@ class RowShardedVI:
 
     def eval(self, theta, U, delta=1e-6):
         b = self.backend
-        red1 = b.phase1(theta, U, delta)
-        if self.world > 1:
-            self.dist.all_reduce(red1, group=self.group)
-        red2 = b.phase2(red1, self.n_global)
-        if self.world > 1:
-            self.dist.all_reduce(red2, group=self.group)
-        return b.finish(red2)
+        with (b.stream_context() if hasattr(b, "stream_context") else contextlib.nullcontext()):
+            red1 = b.phase1(theta, U, delta)
+            if self.world > 1:
+                self.dist.all_reduce(red1, group=self.group)
+            red2 = b.phase2(red1, self.n_global)
+            if self.world > 1:
+                self.dist.all_reduce(red2, group=self.group)
+            return b.finish(red2)

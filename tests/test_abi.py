@@ -1,0 +1,126 @@
+"""C-ABI checks that need no GPU: libsgp.so builds for gfx950, loads, exports every symbol
+include/sgp.h declares, and its host-only entry points behave (values, errors)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import sgp_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "sgp.h")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from sparsergps_amd import _lib
+    return _lib.lib()
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(sgp_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_expected_api():
+    names = declared_functions()
+    for must in ("sgp_make_cov", "sgp_dsig_dtheta", "sgp_ctx_create", "sgp_eval_vi",
+                 "sgp_vi_phase1", "sgp_vi_phase2", "sgp_vi_finish", "sgp_last_error"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(lib):
+    from sparsergps_amd import _lib
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+        assert name in _lib.PROTOTYPES, f"{name} missing from the ctypes prototype table"
+
+
+def test_lib_is_built_for_gfx950():
+    from sparsergps_amd._build import LIB
+    blob = open(LIB, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_versions_and_counts(lib):
+    assert lib.sgp_abi_version() == 1
+    assert lib.sgp_num_params(0, 3) == 3 and lib.sgp_num_params(1, 8) == 10
+    assert lib.sgp_num_params(2, 4) == 3 and lib.sgp_num_params(7, 1) == -1
+    assert lib.sgp_vi_red1_count(1024) == 1024 * 1024 + 1024 + 8
+    assert lib.sgp_vi_red1_count(20) == 128 * 128 + 128 + 8
+    assert lib.sgp_vi_red2_count(1, 8) == 13 and lib.sgp_vi_red2_count(0, 3) == 6
+
+
+def _theta(cp, kernel, d):
+    from sparsergps_amd.covariance import theta_vector
+    return theta_vector(cp, kernel, d, None, need_tau=True)
+
+
+@pytest.mark.parametrize("kernel", ["sqexp", "exp", "ard"])
+def test_pair_functions_match_oracle(lib, kernel):
+    from sparsergps_amd import _lib
+    rng = np.random.default_rng(5)
+    d = 3
+    if kernel == "ard":
+        cp = {"sigma": 1.4, "l1": 0.7, "l2": 1.1, "l3": 2.0, "tau": 0.3}
+        names = ["sigma", "l1", "l2", "l3", "tau"]
+    else:
+        cp = {"sigma": 1.4, "l": 0.9, "tau": 0.3}
+        names = ["sigma", "l", "tau"]
+    th = _theta(cp, kernel, d)
+    kid = _lib.KERNELS[kernel]
+    for _ in range(5):
+        x1 = rng.uniform(0, 3, size=d)
+        x2 = x1.copy() if _ == 0 else rng.uniform(0, 3, size=d)
+        a, b = x1.reshape(1, -1), x2.reshape(1, -1)
+        if kernel == "ard":
+            ref = O.make_cov_mat_ardC(a, b, cp, "ard", 0, ["l1", "l2", "l3"])[0, 0]
+        else:
+            ref = O.make_cov_matC(a, b, cp, kernel, 0)[0, 0]
+        got = lib.sgp_kernel_pair(kid, _lib.dptr(x1), _lib.dptr(x2), d, _lib.dptr(th))
+        assert abs(got - ref) <= 1e-14 * abs(ref)
+        for p, nm in enumerate(names):
+            if kernel == "ard":
+                dref = O.dsig_dtheta_ardC(a, b, cp, "ard", nm, ["l1", "l2", "l3"])[0, 0]
+            else:
+                dref = O.dsig_dthetaC(a, b if kernel != "exp" or nm != "tau" else None, cp, kernel, nm)[0, 0] \
+                    if not (kernel == "exp" and nm == "tau") else (2 * 0.09 if np.array_equal(x1, x2) else 0.0)
+            dgot = lib.sgp_dkernel_pair(kid, _lib.dptr(x1), _lib.dptr(x2), d, _lib.dptr(th), p)
+            assert abs(dgot - dref) <= 1e-13 * max(1e-300, abs(dref)), (nm, dgot, dref)
+
+
+def test_errors_without_gpu(lib):
+    from sparsergps_amd import _lib
+    x = np.zeros((4, 2), order="F")
+    out = np.zeros((4, 4), order="F")
+    th = np.array([1.0, 1.0, 0.5])
+    st = lib.sgp_make_cov(0, 9, _lib.dptr(x), 4, 4, None, 0, 0, 2, _lib.dptr(th), 1e-6, _lib.dptr(out), 4)
+    assert st == _lib.SGP_EINVAL and b"invalid covariance function" in lib.sgp_last_error()
+    bad = np.array([1.0, -2.0, 0.5])
+    st = lib.sgp_make_cov(0, 0, _lib.dptr(x), 4, 4, None, 0, 0, 2, _lib.dptr(bad), 1e-6, _lib.dptr(out), 4)
+    assert st == _lib.SGP_EINVAL and b"length scale" in lib.sgp_last_error()
+    st = lib.sgp_dsig_dtheta(0, 0, _lib.dptr(x), 4, 4, None, 0, 0, 2, _lib.dptr(th), 5, _lib.dptr(out), 4)
+    assert st == _lib.SGP_EINVAL and b"parameter" in lib.sgp_last_error()
+    h = C.c_void_p()
+    y = np.zeros(4)
+    st = lib.sgp_ctx_create(C.byref(h), 0, _lib.dptr(x), 4, 4, 99, _lib.dptr(y), _lib.dptr(y), 8)
+    assert st == _lib.SGP_EINVAL
+    assert lib.sgp_eval_vi(None, 0, None, None, 1, 1, 1e-6, 0, None, None) == _lib.SGP_EINVAL
+    assert lib.sgp_ctx_destroy(None) == _lib.SGP_OK
+
+
+def test_product_path_fails_loudly_without_gpu():
+    """No silent CPU fallback: on a host without a HIP device the product path raises."""
+    from sparsergps_amd import _lib
+    n = C.c_int(0)
+    st = _lib.lib().sgp_device_count(C.byref(n))
+    if st == _lib.SGP_OK and n.value > 0:
+        pytest.skip("a GPU is visible")
+    import sparsergps_amd as S
+    with pytest.raises(RuntimeError):
+        S.make_cov_matC(np.ones((3, 1)), None, {"sigma": 1, "l": 1, "tau": 0.1}, "sqexp", 1e-6)
+    with pytest.raises(RuntimeError):
+        S.SparseGPContext(np.ones((3, 1)), np.ones(3), 0.0, 4)

@@ -1,0 +1,94 @@
+"""Multi-rank row sharding on CPU: world_size 2 (and 3) over gloo.
+
+The product backend (HipRowBackend) needs a GPU; here the same driver
+(sparsergps_amd.dist.RowShardedVI) runs the numpy model of libsgp's phase protocol
+(tests/adjoint_ref.py) on each rank's row block, with the two all-reduces going through
+torch.distributed/gloo, and the result must equal the single-process literal oracle.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from sparsergps_amd.dist import RowShardedVI, shard_rows
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class NumpyBackend:
+    """Test backend: numpy phases, torch CPU tensors as the reduction buffers."""
+
+    def __init__(self, X, y, mu, cov_fun):
+        import adjoint_ref
+        self.rk = adjoint_ref.NumpyVIRank(X, y, mu)
+        self.cov_fun = cov_fun
+
+    def phase1(self, theta, U, delta):
+        return torch.from_numpy(self.rk.phase1(self.cov_fun, theta, U, delta))
+
+    def phase2(self, red1, n_global):
+        return torch.from_numpy(self.rk.phase2(red1.numpy(), n_global))
+
+    def finish(self, red2):
+        return self.rk.finish(red2.numpy())
+
+
+def _worker(rank, world, port, cfg, n, m, coinc, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import sgp_oracle as O
+        P = O.make_gaussian_problem(cfg, n=n, m=m)
+        U = P["U"].copy()
+        if coinc:
+            U[:3] = P["X"][[0, n // 2, n - 1]]
+        s0, s1 = shard_rows(n, world, rank)
+        be = NumpyBackend(P["X"][s0:s1], P["y"][s0:s1], P["mu"][s0:s1], P["cov_fun"])
+        runner = RowShardedVI(be, n)
+        theta = np.array(list(P["cov_par"].values()))
+        obj, grad = runner.eval(theta, U, P["delta"])
+        if rank == 0:
+            o = O.elbo_eval(P["cov_par"], P["cov_fun"], U, P["X"], P["y"], P["mu"], P["delta"])
+            g = O.delbo_dcov_par(P["cov_par"], P["cov_fun"], U, P["X"], P["y"], P["mu"], P["delta"])
+            gv = np.array(list(g["gradient"].values()))
+            q.put((abs(obj - o) / abs(o), float(np.max(np.abs(grad - gv) / np.maximum(1, np.abs(gv))))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,cfg,n,m,coinc", [(2, "C2", 301, 17, False), (2, "C3", 250, 11, True),
+                                                  (3, "C2", 200, 9, True)])
+def test_row_sharded_vi_gloo(world, cfg, n, m, coinc):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, n, m, coinc, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    rel_obj, rel_grad = q.get(timeout=5)
+    assert rel_obj < 1e-12 and rel_grad < 1e-10
+
+
+def test_shard_rows_partition():
+    for n in (1, 7, 1000, 1_000_000):
+        for w in (1, 2, 3, 8):
+            blocks = [shard_rows(n, w, r) for r in range(w)]
+            assert blocks[0][0] == 0 and blocks[-1][1] == n
+            assert all(blocks[i][1] == blocks[i + 1][0] for i in range(w - 1))
+            sizes = [b - a for a, b in blocks]
+            assert max(sizes) - min(sizes) <= 1
+    assert shard_rows(1_000_000, 8, 3) == (375_000, 500_000)    # C4: 8 blocks of 125 000

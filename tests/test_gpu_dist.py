@@ -1,0 +1,58 @@
+"""Row-sharded evaluation through the real HIP backend (device-pointer phase API of libsgp),
+2 ranks on the box's single GPU, reductions over gloo (the 8-GPU RCCL run is the driver's)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import sgp_oracle as O
+        from sparsergps_amd.dist import HipRowBackend, RowShardedVI, shard_rows
+        P = O.make_gaussian_problem("C3", n=3001, m=200)
+        U = P["U"].copy()
+        U[:2] = P["X"][[5, 2999]]                     # coincident knots on both shards
+        s0, s1 = shard_rows(3001, world, rank)
+        be = HipRowBackend(P["X"][s0:s1], P["y"][s0:s1], P["mu"][s0:s1], 200, 0, "ard")
+        theta = np.array(list(P["cov_par"].values()))
+        obj, grad = RowShardedVI(be, 3001).eval(theta, U, P["delta"])
+        be.close()
+        if rank == 0:
+            o = O.elbo_eval(P["cov_par"], "ard", U, P["X"], P["y"], P["mu"], P["delta"])
+            g = np.array(list(O.delbo_dcov_par(P["cov_par"], "ard", U, P["X"], P["y"], P["mu"],
+                                               P["delta"])["gradient"].values()))
+            q.put((abs(obj - o) / abs(o), float(np.max(np.abs(grad - g) / np.maximum(1, np.abs(g))))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_one_gpu_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    rel_obj, rel_grad = q.get(timeout=5)
+    assert rel_obj < 1e-9 and rel_grad < 1e-7
