@@ -126,6 +126,17 @@ int sgp_vi_phase1(sgp_ctx* ctx, int kernel, const double* theta, const double* U
 int sgp_vi_phase2(sgp_ctx* ctx, const double* red1, int64_t n_global, unsigned flags, double* red2);
 int sgp_vi_finish(sgp_ctx* ctx, const double* red2, double* obj, double* grad);
 
+/* Multi-GPU FITC (three steps, two all-reduces): red1 = [S_D, t, r'D^-1 r, sum log Z],
+ * red2 = [S_omega, ..., sum omega, contraction records]; sgp_fitc_finish runs the replicated
+ * m x m tail on the device and returns the objective and gradient. */
+int64_t sgp_fitc_red1_count(int64_t m);
+int64_t sgp_fitc_red2_count(int kernel, int d, int64_t m);
+int sgp_fitc_phase1(sgp_ctx* ctx, int kernel, const double* theta, const double* U, int64_t m,
+                    int64_t ldu, double delta, double* red1);
+int sgp_fitc_phase2(sgp_ctx* ctx, const double* red1, int64_t n_global, unsigned flags,
+                    double* red2);
+int sgp_fitc_finish(sgp_ctx* ctx, const double* red2, double* obj, double* grad);
+
 /* Per-kernel timing of the last evaluation (HIP events on the launch stream).
  * names: '\n'-separated kernel-phase names; ms: their durations (max n entries). */
 int sgp_ctx_enable_timing(sgp_ctx* ctx, int enable);

@@ -7,11 +7,13 @@ from ._build import build
 from ._lib import NotPositiveDefinite, SGPError
 from .covariance import (cov_fun_expC, cov_fun_sqrd_exp_ardC, cov_fun_sqrd_expC, dsig_dtheta_ardC,
                          dsig_dthetaC, make_cov_mat_ardC, make_cov_matC)
-from .vi import SparseGPContext, delbo_dcov_par, elbo_fun, param_names, vi_eval
+from .vi import (SparseGPContext, delbo_dcov_par, dlogp_dcov_par, elbo_fun, fitc_eval, param_names,
+                 vi_eval)
 
 __all__ = [
     "build", "SGPError", "NotPositiveDefinite",
     "make_cov_matC", "make_cov_mat_ardC", "dsig_dthetaC", "dsig_dtheta_ardC",
     "cov_fun_sqrd_expC", "cov_fun_sqrd_exp_ardC", "cov_fun_expC",
     "SparseGPContext", "vi_eval", "elbo_fun", "delbo_dcov_par", "param_names",
+    "fitc_eval", "dlogp_dcov_par",
 ]

@@ -52,6 +52,12 @@ PROTOTYPES = {
                                 C.c_double, C.c_void_p]),
     "sgp_vi_phase2": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_uint, C.c_void_p]),
     "sgp_vi_finish": (C.c_int, [C.c_void_p, C.c_void_p, c_double_p, c_double_p]),
+    "sgp_fitc_red1_count": (C.c_int64, [C.c_int64]),
+    "sgp_fitc_red2_count": (C.c_int64, [C.c_int, C.c_int, C.c_int64]),
+    "sgp_fitc_phase1": (C.c_int, [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_int64, C.c_int64,
+                                  C.c_double, C.c_void_p]),
+    "sgp_fitc_phase2": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_uint, C.c_void_p]),
+    "sgp_fitc_finish": (C.c_int, [C.c_void_p, C.c_void_p, c_double_p, c_double_p]),
     "sgp_ctx_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "sgp_ctx_timings": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64, c_double_p, C.c_int, c_int_p]),
 }

@@ -11,6 +11,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -104,12 +105,17 @@ struct sgp_ctx {
   double* r = nullptr;      // y - mu, n_pad
   double* K = nullptr;      // n_pad x mp (row-major, ld = mp)
   double* alpha = nullptr;  // n_pad
-  double* zinv = nullptr;   // n_pad (FITC weights)
+  double* zinv = nullptr;   // n_pad (FITC weights 1/Z)
+  double* omega = nullptr;  // n_pad (FITC 2 W_ii)
+  double* pvec = nullptr;   // n_pad (row quadratic forms)
+  double* rowq = nullptr;   // (mp_max/128) x n_pad row-partial work
+  double* red2f = nullptr;  // internal FITC second reduction
   // knots and m x m work
   double* U = nullptr;      // mp_max x d, column-major, ld = mp_max
   double *K22 = nullptr, *K22inv = nullptr, *Bm = nullptr, *Binv = nullptr, *Pm = nullptr;
   double *Xt = nullptr, *T1 = nullptr, *M3 = nullptr;
-  double *dinv = nullptr, *logd22 = nullptr, *logdB = nullptr;
+  double *Xt22 = nullptr, *T22 = nullptr;  // K22-stage temporaries (aux stream)
+  double *dinv = nullptr, *dinv22 = nullptr, *logd22 = nullptr, *logdB = nullptr;
   double *uvec = nullptr, *cdiag = nullptr;
   int* status = nullptr;
   double *red1 = nullptr, *red2 = nullptr;
@@ -121,6 +127,16 @@ struct sgp_ctx {
   double delta = 0.0;
   unsigned flags = 0;
   int phase = 0;
+  // K22 stage runs on `aux` concurrently with phase 1 (it depends only on U and theta)
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_knots = nullptr, ev_k22 = nullptr;
+  // launch-bound Bm factorisation captured once per (mp, S pointer) and replayed
+  hipGraphExec_t g_bm = nullptr, g_k22 = nullptr;
+  hipGraph_t g_bm_graph = nullptr, g_k22_graph = nullptr;
+  int64_t g_bm_mp = -1, g_k22_mp = -1;
+  const double* g_bm_S = nullptr;
+  double g_bm_sscale = 0.0;
+  bool use_graphs = false;  // opt-in (SGP_GRAPHS=1): replay faulted in one configuration
   // timing
   bool timing = false;
   std::vector<Timer> timers;
@@ -146,20 +162,22 @@ hipEvent_t pool_event(sgp_ctx* c) {
 
 struct Scope {
   sgp_ctx* c;
+  hipStream_t s;
   size_t idx;
-  Scope(sgp_ctx* ctx, const char* name) : c(ctx), idx((size_t)-1) {
+  Scope(sgp_ctx* ctx, const char* name, hipStream_t st = nullptr)
+      : c(ctx), s(st ? st : ctx->stream), idx((size_t)-1) {
     if (!c->timing) return;
     Timer t;
     t.name = name;
     t.a = pool_event(c);
     t.b = pool_event(c);
     if (!t.a || !t.b) return;
-    hipEventRecord(t.a, c->stream);
+    (void)hipEventRecord(t.a, s);
     c->timers.push_back(t);
     idx = c->timers.size() - 1;
   }
   ~Scope() {
-    if (idx != (size_t)-1) hipEventRecord(c->timers[idx].b, c->stream);
+    if (idx != (size_t)-1) (void)hipEventRecord(c->timers[idx].b, s);
   }
 };
 
@@ -185,9 +203,17 @@ void ctx_free(sgp_ctx* c) {
   void* ptrs[] = {c->X,      c->r,     c->K,      c->alpha,   c->zinv,  c->U,    c->K22,
                   c->K22inv, c->Bm,    c->Binv,   c->Pm,      c->Xt,    c->T1,   c->M3,
                   c->dinv,   c->logd22, c->logdB, c->uvec,    c->cdiag, c->status, c->red1,
-                  c->red2,   c->slab_syrk, c->slab_con, c->slab_small, c->sc};
+                  c->red2,   c->slab_syrk, c->slab_con, c->slab_small, c->sc,
+                  c->Xt22,   c->T22,    c->dinv22, c->omega, c->pvec, c->rowq, c->red2f};
   for (void* p : ptrs)
     if (p) hipFree(p);
+  if (c->g_bm) hipGraphExecDestroy(c->g_bm);
+  if (c->g_bm_graph) hipGraphDestroy(c->g_bm_graph);
+  if (c->g_k22) hipGraphExecDestroy(c->g_k22);
+  if (c->g_k22_graph) hipGraphDestroy(c->g_k22_graph);
+  if (c->ev_knots) hipEventDestroy(c->ev_knots);
+  if (c->ev_k22) hipEventDestroy(c->ev_k22);
+  if (c->aux) hipStreamDestroy(c->aux);
   for (hipEvent_t e : c->pool) hipEventDestroy(e);
   if (c->own) hipStreamDestroy(c->own);
 }
@@ -379,6 +405,15 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
     return SGP_EHIP;
   }
   c->stream = c->own;
+  if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_knots, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_k22, hipEventDisableTiming) != hipSuccess) {
+    set_err("hipStream/hipEvent creation failed");
+    ctx_free(c);
+    delete c;
+    return SGP_EHIP;
+  }
+  if (getenv("SGP_GRAPHS") && !getenv("SGP_NO_GRAPHS")) c->use_graphs = true;
   c->slab_syrk_cap = syrk_slab_doubles(np_, mp);
   c->slab_con_cap = (np_ / SGP_TILE) * (mp / SGP_TILE) * (SGP_MAXD + 4);
   st = st ? st : dalloc(&c->X, np_ * d);
@@ -386,6 +421,9 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->K, np_ * mp);
   st = st ? st : dalloc(&c->alpha, np_);
   st = st ? st : dalloc(&c->zinv, np_);
+  st = st ? st : dalloc(&c->omega, np_);
+  st = st ? st : dalloc(&c->pvec, np_);
+  st = st ? st : dalloc(&c->rowq, np_ * (mp / SGP_TILE));
   st = st ? st : dalloc(&c->U, mp * d);
   st = st ? st : dalloc(&c->K22, mm);
   st = st ? st : dalloc(&c->K22inv, mm);
@@ -396,6 +434,9 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->T1, mm);
   st = st ? st : dalloc(&c->M3, mm);
   st = st ? st : dalloc(&c->dinv, mm / SGP_DB * SGP_DB);
+  st = st ? st : dalloc(&c->dinv22, mm / SGP_DB * SGP_DB);
+  st = st ? st : dalloc(&c->Xt22, mm);
+  st = st ? st : dalloc(&c->T22, mm);
   st = st ? st : dalloc(&c->logd22, mp / SGP_DB);
   st = st ? st : dalloc(&c->logdB, mp / SGP_DB);
   st = st ? st : dalloc(&c->uvec, mp);
@@ -403,6 +444,7 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->status, 4);
   st = st ? st : dalloc(&c->red1, sgp_vi_red1_count(m_max));
   st = st ? st : dalloc(&c->red2, 64);
+  st = st ? st : dalloc(&c->red2f, sgp_fitc_red2_count(SGP_KERNEL_ARD, SGP_MAXD, m_max));
   st = st ? st : dalloc(&c->slab_syrk, c->slab_syrk_cap);
   st = st ? st : dalloc(&c->slab_con, c->slab_con_cap);
   st = st ? st : dalloc(&c->slab_small, SLAB_SMALL);
@@ -433,8 +475,9 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
 
 int sgp_ctx_destroy(sgp_ctx* c) {
   if (!c) return SGP_OK;
-  hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->aux) (void)hipStreamSynchronize(c->aux);
   ctx_free(c);
   delete c;
   return SGP_OK;
@@ -470,6 +513,7 @@ int sgp_ctx_timings(sgp_ctx* c, char* names, int64_t names_len, double* ms, int 
   if (!c || !count) return SGP_EINVAL;
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipStreamSynchronize(c->aux));
   std::string all;
   int k = 0;
   for (const Timer& t : c->timers) {
@@ -497,6 +541,8 @@ int64_t sgp_vi_red1_count(int64_t m) {
 
 int64_t sgp_vi_red2_count(int kernel, int d) { return num_ls(kernel, d) + 5; }
 
+static int k22_stage(sgp_ctx* c, double diag_sub);
+
 int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
                   int64_t ldu, double delta, double* red1) {
   KernParams kp;
@@ -512,12 +558,16 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   st = upload_knots(c, U, m, ldu);
   if (st) return st;
   HIPCHK(hipMemsetAsync(c->status, 0, sizeof(int) * 4, c->stream));
+  HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->stream));
+  st = k22_stage(c, kp.tau2);   // aux stream, overlaps the builder and the SYRK below
+  if (st) return st;
   {
     Scope t(c, "build_knm");
     HIPCHK(launch_build_knm(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp, m, c->mp, c->K,
                             c->stream));
   }
   HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_vi_red1_count(m), c->stream));
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));   // keep the SYRK round unshared
   {
     Scope t(c, "syrk");
     HIPCHK(launch_syrk_aug(c->K, c->n_pad, c->mp, c->r, nullptr, c->slab_syrk,
@@ -532,21 +582,79 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   return SGP_OK;
 }
 
-// m x m algebra shared by VI (and FITC): K22 and Bm = K22 + S * s_scale factored and inverted.
-static int dense_stage(sgp_ctx* c, const double* S, double s_scale, double diag_sub) {
-  const int64_t mp = c->mp, mm = mp * mp;
-  Scope t(c, "dense_mm");
-  HIPCHK(launch_build_kmm(c->kp, c->U, c->mp, c->m, mp, diag_sub, c->K22, c->stream));
-  HIPCHK(dense_axpby(1.0, c->K22, s_scale, S, c->Bm, mm, c->stream));
-  HIPCHK(dense_potrf(c->K22, mp, mp, c->dinv, c->logd22, c->status, c->stream));
-  HIPCHK(dense_trtri(c->K22, mp, mp, c->dinv, c->Xt, mp, c->T1, c->stream));
-  HIPCHK(dense_inv_from_trtri(c->Xt, mp, c->K22inv, c->stream));
-  HIPCHK(dense_potrf(c->Bm, mp, mp, c->dinv, c->logdB, c->status + 1, c->stream));
-  HIPCHK(dense_trtri(c->Bm, mp, mp, c->dinv, c->Xt, mp, c->T1, c->stream));
-  HIPCHK(dense_inv_from_trtri(c->Xt, mp, c->Binv, c->stream));
-  HIPCHK(launch_sum_small(c->logd22, mp / SGP_DB, c->sc + SC_LD22, c->stream));
-  HIPCHK(launch_sum_small(c->logdB, mp / SGP_DB, c->sc + SC_LDB, c->stream));
+typedef int (*launch_seq_fn)(sgp_ctx*, hipStream_t);
+
+// Replay `fn`'s launches from a hipGraph captured once per shape (all kernel arguments are
+// context pointers, so the graph stays valid); falls back to direct launches if capture fails.
+static int run_graph(sgp_ctx* c, hipStream_t s, launch_seq_fn fn, hipGraphExec_t* exec,
+                     hipGraph_t* graph, int64_t* key) {
+  if (c->use_graphs) {
+    if (!*exec || *key != c->mp) {
+      if (*exec) { (void)hipGraphExecDestroy(*exec); *exec = nullptr; }
+      if (*graph) { (void)hipGraphDestroy(*graph); *graph = nullptr; }
+      bool ok = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess;
+      const int st = ok ? fn(c, s) : SGP_EHIP;
+      hipGraph_t g = nullptr;
+      ok = (hipStreamEndCapture(s, &g) == hipSuccess) && ok && st == SGP_OK && g;
+      if (ok) ok = hipGraphInstantiate(exec, g, nullptr, nullptr, 0) == hipSuccess;
+      if (!ok) {
+        if (g) (void)hipGraphDestroy(g);
+        *exec = nullptr;
+        c->use_graphs = false;
+        (void)hipGetLastError();
+      } else {
+        *graph = g;
+        *key = c->mp;
+      }
+    }
+    if (*exec) {
+      HIPCHK(hipGraphLaunch(*exec, s));
+      return SGP_OK;
+    }
+  }
+  return fn(c, s);
+}
+
+static int k22_factor_launches(sgp_ctx* c, hipStream_t s) {
+  const int64_t mp = c->mp;
+  HIPCHK(hipMemcpyAsync(c->K22inv, c->K22, sizeof(double) * mp * mp, hipMemcpyDeviceToDevice, s));
+  HIPCHK(dense_spd_inverse(c->K22inv, mp, c->Xt22, c->T22, c->dinv22, c->logd22, c->status, s));
+  HIPCHK(launch_sum_small(c->logd22, mp / SGP_DB, c->sc + SC_LD22, s));
+  HIPCHK(launch_diag(c->K22inv, mp, mp, c->cdiag, s));
   return SGP_OK;
+}
+
+// K22 = Kuu + (tau^2 + delta - diag_sub) I factored and inverted on the aux stream.  It
+// depends only on (U, theta), so it runs concurrently with phase 1's memory-bound builder; the
+// SYRK (whose grid fills exactly one residency round) waits for it.  A pristine copy of K22
+// goes to Bm for phase 2.
+static int k22_stage(sgp_ctx* c, double diag_sub) {
+  const int64_t mp = c->mp;
+  HIPCHK(hipEventRecord(c->ev_knots, c->stream));
+  HIPCHK(hipStreamWaitEvent(c->aux, c->ev_knots, 0));
+  Scope t(c, "k22_aux", c->aux);
+  HIPCHK(launch_build_kmm(c->kp, c->U, c->mp, c->m, mp, diag_sub, c->K22, c->aux));
+  int st = run_graph(c, c->aux, k22_factor_launches, &c->g_k22, &c->g_k22_graph, &c->g_k22_mp);
+  if (st) return st;
+  HIPCHK(hipEventRecord(c->ev_k22, c->aux));
+  return SGP_OK;
+}
+
+// Binv (holding K22 + S * s_scale) inverted in place: 48 small launches, captured into a
+// hipGraph once per shape and replayed.
+static int bm_factor_launches(sgp_ctx* c, hipStream_t s) {
+  const int64_t mp = c->mp;
+  HIPCHK(dense_spd_inverse(c->Binv, mp, c->Xt, c->T1, c->dinv, c->logdB, c->status + 1, s));
+  HIPCHK(launch_sum_small(c->logdB, mp / SGP_DB, c->sc + SC_LDB, s));
+  return SGP_OK;
+}
+
+static int bm_stage(sgp_ctx* c, const double* S, double s_scale) {
+  const int64_t mp = c->mp, mm = mp * mp;
+  Scope t(c, "dense_bm");
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
+  HIPCHK(dense_axpby(1.0, c->K22, s_scale, S, c->Binv, mm, c->stream));
+  return run_graph(c, c->stream, bm_factor_launches, &c->g_bm, &c->g_bm_graph, &c->g_bm_mp);
 }
 
 int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned flags,
@@ -559,11 +667,11 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
   const int64_t mp = c->mp, mm = mp * mp;
   const double z = kp.tau2 + c->delta;
   const double* S = red1;
+  (void)mm;
   const double* t = red1 + mm;
   c->n_global = n_global;
   c->flags = flags;
-  HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->stream));
-  int st = dense_stage(c, S, 1.0 / z, kp.tau2);
+  int st = bm_stage(c, S, 1.0 / z);
   if (st) return st;
   {
     Scope tm(c, "mm_vectors");
@@ -579,7 +687,6 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
                          mp, c->stream));
     HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->T1, mp, c->K22inv, mp, 0.0,
                          c->M3, mp, c->stream));
-    HIPCHK(launch_diag(c->K22inv, mp, mp, c->cdiag, c->stream));
   }
   {
     Scope tm(c, "contract_kmm");
@@ -589,24 +696,16 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
                                c->stream));
     HIPCHK(launch_colsum(c->slab_small, nb, kp.P - 1, c->sc + SC_G22, c->stream));
   }
-  HIPCHK(hipMemsetAsync(red2, 0, sizeof(double) * sgp_vi_red2_count(kp.kernel, kp.d), c->stream));
-  {
-    Scope tm(c, "alpha");
-    int nb = 0;
-    HIPCHK(launch_alpha(c->K, c->n_pad, mp, c->r, c->uvec, 1.0 / z, nullptr, c->alpha,
-                        c->slab_small, &nb, c->stream));
-    HIPCHK(launch_colsum(c->slab_small, nb, 1, red2, c->stream));
-  }
   int64_t nrec = 0, nwg = 0;
   {
     Scope tm(c, "contract_knm");
     HIPCHK(launch_contract_knm(kp, c->K, c->Pm, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp,
-                               c->m, mp, c->alpha, c->uvec, c->cdiag, c->slab_con, &nrec, &nwg,
-                               c->stream));
+                               c->m, mp, c->r, 1.0 / z, nullptr, c->uvec, nullptr, 1.0, c->cdiag,
+                               1, c->slab_con, &nrec, &nwg, c->stream));
   }
   {
     Scope tm(c, "contract_reduce");
-    HIPCHK(launch_colsum(c->slab_con, nwg, nrec, red2 + 1, c->stream));
+    HIPCHK(launch_colsum(c->slab_con, nwg, nrec, red2, c->stream));
   }
   c->phase = 2;
   return SGP_OK;
@@ -643,12 +742,13 @@ int sgp_vi_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
   const double trace_term = -(1.0 / (2.0 * kp.tau2)) * (n * (kp.sig2 + c->delta) - trKS);
   *obj = quad + det_part - (n / 2.0) * log(2.0 * M_PI) + trace_term;
   // delbo_dcov_par (vi_functions.R:259-419) in adjoint form
-  const double aTa = r2[0], e_sig = r2[1];
-  const double c_sum = r2[2 + L], c_cnt = r2[3 + L], c_dg = r2[4 + L];
+  // red2 = [e_sig, e_l(L), c_sum, c_cnt, c_dg, alpha^T alpha]
+  const double e_sig = r2[0];
+  const double c_sum = r2[1 + L], c_cnt = r2[2 + L], c_dg = r2[3 + L], aTa = r2[4 + L];
   const double trSinv = n / z - trBS / (z * z);
   const double trW = 0.5 * (aTa - trSinv);
   grad[0] = 2.0 * e_sig + sc[SC_G22] - n * kp.sig2 / kp.tau2;
-  for (int q = 0; q < L; ++q) grad[1 + q] = r2[2 + q] + sc[SC_G22 + 1 + q];
+  for (int q = 0; q < L; ++q) grad[1 + q] = r2[1 + q] + sc[SC_G22 + 1 + q];
   grad[L + 1] = 2.0 * kp.tau2 * (c_sum - (c_cnt - c->delta * c_dg) / kp.tau2) +
                 2.0 * kp.tau2 * trW - 2.0 * trace_term;
   return SGP_OK;
@@ -664,12 +764,184 @@ int sgp_eval_vi(sgp_ctx* c, int kernel, const double* theta, const double* U, in
   return sgp_vi_finish(c, c->red2, obj, grad);
 }
 
+// ------------------------------------------------------------------------- FITC phases
+// obj_fun_norm (laplace_approx_obj_funs.R:6-52) + dlogp_dcov_par (laplace_approx_gradient.R:
+// 720-971) in adjoint form.  Z = sigma^2 + tau^2 + delta - q,
+// q_i = K_i K22^-1 K_i^T, D = diag(Z), S_D = K^T D^-1 K, Bm = K22 + S_D, u = Bm^-1 K^T D^-1 r,
+// alpha = D^-1 (r - K u), omega_i = alpha_i^2 - (Sigma^-1)_ii,
+// G = alpha u^T - D^-1 K Bm^-1 - diag(omega) K K22^-1,
+// G22 = -1/2 u u^T + 1/2 (K22^-1 - Bm^-1) + 1/2 K22^-1 S_omega K22^-1.
+// red1 = [S_D (mp^2), t (mp), r^T D^-1 r, sum log Z]
+// red2 = [S_omega (mp^2), t_omega (mp), rr_omega, sum omega, rec_1 (L+5), rec_2 (L+5)]
+int64_t sgp_fitc_red1_count(int64_t m) { return sgp_vi_red1_count(m); }
+
+int64_t sgp_fitc_red2_count(int kernel, int d, int64_t m) {
+  const int64_t mp = round_up(m, SGP_TILE);
+  return mp * mp + mp + 8 + 2 * (num_ls(kernel, d) + 5);
+}
+
+static int64_t fitc_rec_off(int64_t mp) { return mp * mp + mp + 8; }
+
+int sgp_fitc_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
+                    int64_t ldu, double delta, double* red1) {
+  KernParams kp;
+  int st = check_eval_args(c, kernel, theta, U, m, ldu, delta, &kp);
+  if (st) return st;
+  if (!red1) { set_err("red1 is NULL"); return SGP_EINVAL; }
+  HIPCHK(hipSetDevice(c->device));
+  timers_reset(c);
+  c->kp = kp;
+  c->m = m;
+  c->mp = round_up(m, SGP_TILE);
+  c->delta = delta;
+  const int64_t mp = c->mp, mm = mp * mp;
+  st = upload_knots(c, U, m, ldu);
+  if (st) return st;
+  HIPCHK(hipMemsetAsync(c->status, 0, sizeof(int) * 4, c->stream));
+  HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->stream));
+  st = k22_stage(c, kp.tau2);   // K22 = Kuu + delta I, same as the VI path (laplace_gradient_ascent.R:1238-1257)
+  if (st) return st;
+  {
+    Scope t(c, "build_knm");
+    HIPCHK(launch_build_knm(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp, m, mp, c->K,
+                            c->stream));
+  }
+  HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_fitc_red1_count(m), c->stream));
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
+  {
+    Scope t(c, "rowquad_q");
+    HIPCHK(launch_rowquad_knm(kp, c->K, c->K22inv, c->n, c->n_pad, m, mp, c->r, 0.0, nullptr,
+                              nullptr, nullptr, c->rowq, c->pvec, c->stream));
+    int nb = 0;
+    HIPCHK(launch_fitc_z(c->pvec, c->n, c->n_pad, kp.sig2 + kp.tau2 + delta, c->zinv,
+                         c->slab_small, &nb, c->stream));
+    HIPCHK(launch_colsum(c->slab_small, nb, 1, red1 + mm + mp + 1, c->stream));
+  }
+  {
+    Scope t(c, "syrk");
+    HIPCHK(launch_syrk_aug(c->K, c->n_pad, mp, c->r, c->zinv, c->slab_syrk, c->slab_syrk_cap,
+                           red1, c->stream, 3));
+  }
+  c->phase = 11;
+  return SGP_OK;
+}
+
+int sgp_fitc_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned flags,
+                    double* red2) {
+  if (!c || !red1 || !red2) { set_err("invalid arguments"); return SGP_EINVAL; }
+  if (c->phase != 11) { set_err("sgp_fitc_phase2 called before sgp_fitc_phase1"); return SGP_EINVAL; }
+  if (n_global < c->n) { set_err("n_global < local rows"); return SGP_EINVAL; }
+  HIPCHK(hipSetDevice(c->device));
+  const KernParams& kp = c->kp;
+  const int64_t mp = c->mp, mm = mp * mp;
+  const double* S = red1;
+  const double* t = red1 + mm;
+  c->n_global = n_global;
+  c->flags = flags;
+  int st = bm_stage(c, S, 1.0);
+  if (st) return st;
+  HIPCHK(hipMemsetAsync(red2, 0, sizeof(double) * sgp_fitc_red2_count(kp.kernel, kp.d, c->m),
+                        c->stream));
+  {
+    Scope tm(c, "mm_vectors");
+    HIPCHK(dense_gemv(c->Binv, mp, t, 1.0, c->uvec, c->stream));             // u = Bm^-1 t
+    HIPCHK(launch_dot(t, c->uvec, mp, c->slab_small, c->sc + SC_TU, c->stream));
+    HIPCHK(hipMemcpyAsync(c->sc + SC_RR, red1 + mm + mp, 2 * sizeof(double),
+                          hipMemcpyDeviceToDevice, c->stream));               // rr_w, sum log Z
+  }
+  {
+    Scope tm(c, "rowquad_p");
+    HIPCHK(launch_rowquad_knm(kp, c->K, c->Binv, c->n, c->n_pad, c->m, mp, c->r, 0.0, c->zinv,
+                              c->uvec, c->alpha, c->rowq, c->pvec, c->stream));
+    int nb = 0;
+    HIPCHK(launch_fitc_omega(c->alpha, c->zinv, c->pvec, c->n, c->n_pad, c->omega,
+                             c->slab_small, &nb, c->stream));
+    HIPCHK(launch_colsum(c->slab_small, nb, 1, red2 + mm + mp + 1, c->stream));
+  }
+  {
+    Scope tm(c, "syrk_omega");
+    HIPCHK(launch_syrk_aug(c->K, c->n_pad, mp, c->r, c->omega, c->slab_syrk, c->slab_syrk_cap,
+                           red2, c->stream, 3));
+    // the SYRK reduce wrote rr_omega at mm + mp; keep sum(omega) at mm + mp + 1
+  }
+  const int64_t off = fitc_rec_off(mp);
+  int64_t nrec = 0, nwg = 0;
+  {
+    Scope tm(c, "contract_knm");
+    // pass 1: G1 = alpha u^T - diag(1/Z) K Bm^-1
+    HIPCHK(launch_contract_knm(kp, c->K, c->Binv, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp,
+                               c->m, mp, c->r, 0.0, c->zinv, c->uvec, c->zinv, -1.0, nullptr, 0,
+                               c->slab_con, &nrec, &nwg, c->stream));
+    HIPCHK(launch_colsum(c->slab_con, nwg, nrec, red2 + off, c->stream));
+    // pass 2: G2 = -diag(omega) K K22^-1
+    HIPCHK(launch_contract_knm(kp, c->K, c->K22inv, c->X, c->n_pad, c->n, c->n_pad, c->U,
+                               c->mp, c->m, mp, c->r, 0.0, nullptr, nullptr, c->omega, -1.0,
+                               nullptr, 0, c->slab_con, &nrec, &nwg, c->stream));
+    HIPCHK(launch_colsum(c->slab_con, nwg, nrec, red2 + off + nrec, c->stream));
+  }
+  c->phase = 12;
+  return SGP_OK;
+}
+
+int sgp_fitc_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
+  if (!c || !red2 || !obj || !grad) { set_err("invalid arguments"); return SGP_EINVAL; }
+  if (c->phase != 12) { set_err("sgp_fitc_finish called before sgp_fitc_phase2"); return SGP_EINVAL; }
+  HIPCHK(hipSetDevice(c->device));
+  const KernParams& kp = c->kp;
+  const int L = kp.L;
+  const int64_t mp = c->mp;
+  {
+    Scope tm(c, "contract_kmm");
+    // M3 = K22^-1 S_omega K22^-1 ; G22 = -1/2 uu^T + 1/2 (K22^-1 - Bm^-1) + 1/2 M3
+    HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->K22inv, mp, red2, mp, 0.0,
+                         c->T1, mp, c->stream));
+    HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->T1, mp, c->K22inv, mp, 0.0,
+                         c->M3, mp, c->stream));
+    int nb = 0;
+    HIPCHK(launch_contract_kmm(kp, c->U, c->mp, c->m, mp, c->uvec, c->K22inv, c->Binv, c->M3,
+                               -0.5, 0.5, 0.5, c->slab_small, &nb, c->stream));
+    HIPCHK(launch_colsum(c->slab_small, nb, kp.P - 1, c->sc + SC_G22, c->stream));
+  }
+  double sc[SC_N], r2[2 * (SGP_MAXD + 5) + 2];
+  int status[4];
+  const int64_t off = fitc_rec_off(mp);
+  const int nrec = L + 5;
+  HIPCHK(hipMemcpyAsync(sc, c->sc, sizeof(sc), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(r2, red2 + mp * mp + mp + 1, sizeof(double), hipMemcpyDeviceToHost,
+                        c->stream));
+  HIPCHK(hipMemcpyAsync(r2 + 1, red2 + off, sizeof(double) * 2 * nrec, hipMemcpyDeviceToHost,
+                        c->stream));
+  HIPCHK(hipMemcpyAsync(status, c->status, sizeof(status), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->phase = 0;
+  if (status[0] || status[1]) {
+    set_err("chol(): the leading minor of order %d of %s is not positive definite",
+            status[0] ? status[0] : status[1],
+            status[0] ? "Sigma22" : "Sigma22 + t(Sigma12) %*% ZSig12");
+    return SGP_ENOTPD;
+  }
+  const double n = (double)c->n_global;
+  const double ld22 = 2.0 * sc[SC_LD22], ldB = 2.0 * sc[SC_LDB];
+  const double rr = sc[SC_RR], sumlogz = sc[SC_RR + 1], tu = sc[SC_TU];
+  const double logdet22 = (c->flags & SGP_FLAG_R_DET) ? log(exp(ld22)) : ld22;
+  *obj = -0.5 * rr + 0.5 * tu - 0.5 * (sumlogz - logdet22 + ldB) - (n / 2.0) * log(2.0 * M_PI);
+  const double sum_omega = r2[0];
+  const double* a = r2 + 1;
+  const double* b = r2 + 1 + nrec;
+  grad[0] = 2.0 * (a[0] + b[0]) + sc[SC_G22] + kp.sig2 * sum_omega;
+  for (int q = 0; q < L; ++q) grad[1 + q] = a[1 + q] + b[1 + q] + sc[SC_G22 + 1 + q];
+  grad[L + 1] = 2.0 * kp.tau2 * (a[1 + L] + b[1 + L]) + kp.tau2 * sum_omega;
+  return SGP_OK;
+}
+
 int sgp_eval_fitc(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
                   int64_t ldu, double delta, unsigned flags, double* obj, double* grad) {
-  (void)c; (void)kernel; (void)theta; (void)U; (void)m; (void)ldu; (void)delta; (void)flags;
-  (void)obj; (void)grad;
-  set_err("sgp_eval_fitc: not available in this build");
-  return SGP_EINVAL;
+  if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
+  int st = sgp_fitc_phase1(c, kernel, theta, U, m, ldu, delta, c->red1);
+  if (st) return st;
+  st = sgp_fitc_phase2(c, c->red1, c->n, flags, c->red2f);
+  if (st) return st;
+  return sgp_fitc_finish(c, c->red2f, obj, grad);
 }
 
 }  // extern "C"

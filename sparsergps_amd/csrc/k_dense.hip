@@ -127,6 +127,215 @@ __global__ void __launch_bounds__(256) k_potrf_diag(double* A, int64_t lda, int 
   if (tid == 0) logd[kb] = lg;
 }
 
+// ---------------------------------------------------------------- blocked Gauss-Jordan
+// 1/sqrt(p) for p > 0: hardware rsq seed + two Newton steps (full double accuracy).
+__device__ __forceinline__ double rsqrt_nr(double p) {
+  double y = __builtin_amdgcn_rsq(p);
+  y = y * fma(-0.5 * p * y, y, 1.5);
+  y = y * fma(-0.5 * p * y, y, 1.5);
+  return y;
+}
+
+// Pivot step k of the SPD Gauss-Jordan inverse: P = inv(A_kk) for the current 64x64 pivot
+// block (a Schur complement, SPD).  Register-blocked Cholesky + triangular inverse with one
+// barrier per column (branch-free rank-1 updates), then P = X^T X through LDS.
+// logd[k] = sum log L_ii of the pivot block; a bad pivot sets status = global index + 1.
+__global__ void __launch_bounds__(256) k_gj_pivot(const double* __restrict__ A, int64_t lda,
+                                                  int k, double* __restrict__ P,
+                                                  double* __restrict__ logd,
+                                                  int* __restrict__ status) {
+  __shared__ double colv[2][64];
+  __shared__ double xrow[2][64];
+  __shared__ double piv_s[64];
+  __shared__ double Xs[64][65];
+  const int tid = threadIdx.x;
+  const int bi = tid >> 4, bj = tid & 15;
+  const int64_t o = (int64_t)k * 64;
+  double a[4][4], x[4][4];
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int i = 4 * bi + ii, j = 4 * bj + jj;
+      a[ii][jj] = A[(o + i) * lda + o + j];
+      x[ii][jj] = (i == j) ? 1.0 : 0.0;
+    }
+  for (int kb4 = 0; kb4 < 16; ++kb4) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int kc = 4 * kb4 + kk;
+      const int b = kc & 1;
+      if (bj == kb4) {
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) colv[b][4 * bi + ii] = a[ii][kk];
+      }
+      if (bi == kb4) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) xrow[b][4 * bj + jj] = x[kk][jj];
+      }
+      __syncthreads();
+      const double p2 = colv[b][kc];
+      const double rp = rsqrt_nr(p2);
+      if (tid == 0) {
+        piv_s[kc] = p2 * rp;
+        if (!(p2 > 0.0) || !isfinite(p2)) atomicCAS(status, 0, (int)(o + kc + 1));
+      }
+      double li[4], lj[4], xk[4];
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int i = 4 * bi + ii;
+        li[ii] = (i > kc) ? colv[b][i] * rp : 0.0;
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int j = 4 * bj + jj;
+        lj[jj] = (j > kc) ? colv[b][j] * rp : 0.0;
+        xk[jj] = xrow[b][j] * rp;          // X[kc][j] = 0 for j > kc
+      }
+      // trailing update of A (only j > kc, i > kc change) and of the rows i > kc of X
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          a[ii][jj] = fma(-li[ii], lj[jj], a[ii][jj]);
+          x[ii][jj] = fma(-li[ii], xk[jj], x[ii][jj]);
+        }
+      if (bi == kb4) {                    // row kc of X is final
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) x[kk][jj] = xk[jj];
+      }
+    }
+  }
+  // P = X^T X  (X = L^{-1} lower triangular)
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int i = 4 * bi + ii, j = 4 * bj + jj;
+      Xs[i][j] = (j <= i) ? x[ii][jj] : 0.0;
+    }
+  __syncthreads();
+  double pacc[4][4];
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) pacc[ii][jj] = 0.0;
+  for (int kr = 0; kr < 64; ++kr) {
+    double xa[4], xb[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { xa[q] = Xs[kr][4 * bi + q]; xb[q] = Xs[kr][4 * bj + q]; }
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) pacc[ii][jj] = fma(xa[ii], xb[jj], pacc[ii][jj]);
+  }
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) P[(4 * bi + ii) * 64 + 4 * bj + jj] = pacc[ii][jj];
+  double lg = (tid < 64) ? log(piv_s[tid]) : 0.0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) lg += __shfl_xor(lg, off, 64);
+  if (tid == 0) logd[k] = lg;
+}
+
+// R = P * A[k-block rows, all columns] (64 x mp) and C = A[all rows, k-block cols] (mp x 64).
+// One workgroup per 64-column block j.
+__global__ void __launch_bounds__(256) k_gj_panel(const double* __restrict__ A, int64_t lda,
+                                                  int k, const double* __restrict__ P,
+                                                  double* __restrict__ R, double* __restrict__ Cb) {
+  __shared__ double Ps[64][65];
+  __shared__ double Bs[64][65];
+  const int tid = threadIdx.x;
+  const int j = blockIdx.x;
+  const int64_t o = (int64_t)k * 64, oj = (int64_t)j * 64;
+  for (int e = tid; e < 4096; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    Ps[r][c] = P[e];
+    Bs[r][c] = A[(o + r) * lda + oj + c];
+    Cb[(oj + r) * 64 + c] = A[(oj + r) * lda + o + c];
+  }
+  __syncthreads();
+  const int bi = tid >> 4, bj = tid & 15;
+  double acc[4][4];
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) acc[ii][jj] = 0.0;
+  for (int q = 0; q < 64; ++q) {
+    double pa[4], bb[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { pa[t] = Ps[4 * bi + t][q]; bb[t] = Bs[q][4 * bj + t]; }
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) acc[ii][jj] = fma(pa[ii], bb[jj], acc[ii][jj]);
+  }
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) R[(int64_t)(4 * bi + ii) * (lda) + oj + 4 * bj + jj] = acc[ii][jj];
+}
+
+// Gauss-Jordan update of every 64x64 tile (i, j) for pivot block k (f64 MFMA, K = 64):
+//   i == k: A_kj = R_j (A_kk = P);   j == k: A_ik = -C_i P;   else A_ij -= C_i R_j.
+__global__ void __launch_bounds__(256) k_gj_update(double* __restrict__ A, int64_t lda, int k,
+                                                   const double* __restrict__ P,
+                                                   const double* __restrict__ R,
+                                                   const double* __restrict__ Cb) {
+  __shared__ double As[64][66];   // C_i (64 x 64)
+  __shared__ double Bs[64][66];   // R_j or P
+  const int ti = blockIdx.y, tj = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t oi = (int64_t)ti * 64, oj = (int64_t)tj * 64;
+  if (ti == k) {
+    for (int e = tid; e < 4096; e += 256) {
+      const int r = e >> 6, c = e & 63;
+      A[(oi + r) * lda + oj + c] = (tj == k) ? P[e] : R[(int64_t)r * lda + oj + c];
+    }
+    return;
+  }
+  const bool colk = (tj == k);
+  for (int e = tid; e < 4096; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    As[r][c] = Cb[(oi + r) * 64 + c];
+    Bs[r][c] = colk ? P[e] : R[(int64_t)r * lda + oj + c];
+  }
+  __syncthreads();
+  const int wr = wv >> 1, wc = wv & 1;
+  d4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+  for (int kk = 0; kk < 16; ++kk) {
+    const int kx = kk * 4 + (lane >> 4);
+    double af[2], bf[2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      af[f] = As[wr * 32 + f * 16 + (lane & 15)][kx];
+      bf[f] = Bs[kx][wc * 32 + f * 16 + (lane & 15)];
+    }
+#pragma unroll
+    for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < 2; ++fn)
+        acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
+  }
+#pragma unroll
+  for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = oi + wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
+        const int64_t col = oj + wc * 32 + fn * 16 + (lane & 15);
+        double* dst = &A[row * lda + col];
+        *dst = colk ? -acc[fm][fn][q] : (*dst - acc[fm][fn][q]);
+      }
+}
+
 __global__ void __launch_bounds__(256) k_copy_block(const double* __restrict__ src,
                                                     double* __restrict__ dst, int64_t ldd) {
   for (int e = threadIdx.x; e < 64 * 64; e += 256) dst[(e >> 6) * ldd + (e & 63)] = src[e];
@@ -224,7 +433,61 @@ __global__ void __launch_bounds__(256) k_diag(const double* __restrict__ A, int6
   if (j < mp) out[j] = A[j * lda + j];
 }
 
+__global__ void __launch_bounds__(256) k_fitc_z(const double* __restrict__ q, int64_t n,
+                                                int64_t n_pad, double c0, double* __restrict__ w,
+                                                double* __restrict__ slab) {
+  __shared__ double sh[4];
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * 256) {
+    if (i < n) {
+      const double z = c0 - q[i];
+      w[i] = 1.0 / z;
+      s += log(z);
+    } else {
+      w[i] = 0.0;
+    }
+  }
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) slab[blockIdx.x] = s;
+}
+
+__global__ void __launch_bounds__(256) k_fitc_omega(const double* __restrict__ alpha,
+                                                    const double* __restrict__ w,
+                                                    const double* __restrict__ p, int64_t n,
+                                                    int64_t n_pad, double* __restrict__ omega,
+                                                    double* __restrict__ slab) {
+  __shared__ double sh[4];
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * 256) {
+    double o = 0.0;
+    if (i < n) o = alpha[i] * alpha[i] - (w[i] - w[i] * w[i] * p[i]);
+    omega[i] = o;
+    s += o;
+  }
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) slab[blockIdx.x] = s;
+}
+
 }  // namespace
+
+hipError_t launch_fitc_z(const double* q, int64_t n, int64_t n_pad, double c0, double* w,
+                         double* slab, int* nblocks, hipStream_t s) {
+  int nb = (int)((n_pad + 255) / 256);
+  if (nb > 1024) nb = 1024;
+  *nblocks = nb;
+  hipLaunchKernelGGL(k_fitc_z, dim3(nb), dim3(256), 0, s, q, n, n_pad, c0, w, slab);
+  return hipGetLastError();
+}
+
+hipError_t launch_fitc_omega(const double* alpha, const double* w, const double* p, int64_t n,
+                             int64_t n_pad, double* omega, double* slab, int* nblocks,
+                             hipStream_t s) {
+  int nb = (int)((n_pad + 255) / 256);
+  if (nb > 1024) nb = 1024;
+  *nblocks = nb;
+  hipLaunchKernelGGL(k_fitc_omega, dim3(nb), dim3(256), 0, s, alpha, w, p, n, n_pad, omega, slab);
+  return hipGetLastError();
+}
 
 hipError_t dense_potrf(double* A, int64_t mp, int64_t lda, double* dinv, double* logd,
                        int* status, hipStream_t s) {
@@ -265,6 +528,17 @@ hipError_t dense_trtri(const double* L, int64_t mp, int64_t lda, const double* d
                         X + w * ldx, ldx, s);
       if (e != hipSuccess) return e;
     }
+  }
+  return hipGetLastError();
+}
+
+hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* Cb, double* P,
+                             double* logd, int* status, hipStream_t s) {
+  const int nb = (int)(mp / SGP_DB);
+  for (int k = 0; k < nb; ++k) {
+    hipLaunchKernelGGL(k_gj_pivot, dim3(1), dim3(256), 0, s, A, mp, k, P, logd, status);
+    hipLaunchKernelGGL(k_gj_panel, dim3(nb), dim3(256), 0, s, A, mp, k, P, R, Cb);
+    hipLaunchKernelGGL(k_gj_update, dim3(nb, nb), dim3(256), 0, s, A, mp, k, P, R, Cb);
   }
   return hipGetLastError();
 }

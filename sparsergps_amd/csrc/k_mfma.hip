@@ -209,13 +209,26 @@ k_syrk_reduce_t(const double* __restrict__ slab_t, const double* __restrict__ sl
 }
 
 // ============================================================================ contraction
-template <int DT>
+// One kernel, two epilogues, both on the tile T = K[i-block, :] * M[:, j-block] held in
+// f64-MFMA accumulators:
+//   EPI_GRAD     G_ij = alpha_i u_j + rs_i T_ij, contracted with dK_ij/dlog(theta) for all
+//                parameters at once (record per tile: sum G*K, sum G*K*w_c, tau-coincidence
+//                sums, alpha^T alpha);
+//   EPI_ROWQUAD  per-row partial sum_j K_ij T_ij (= diag(K M K^T) after summing the column
+//                tiles) into rowq[tj][row].
+// When uvec != nullptr, alpha_i = (r_i - K_i u) * iz_i is computed in the same k-loop from the
+// staged K values (iz_i = invz_vec ? invz_vec[i] : invz), optionally written to alpha_out.
+enum { EPI_GRAD = 0, EPI_ROWQUAD = 1 };
+
+template <int DT, int EPI>
 __global__ void __launch_bounds__(256, 2)
-k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict__ P,
+k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict__ M,
            const double* __restrict__ X, int64_t ldx, int64_t n, int64_t n_pad,
            const double* __restrict__ U, int64_t ldu, int64_t m, int64_t mp,
-           const double* __restrict__ alpha, const double* __restrict__ uvec,
-           const double* __restrict__ cdiag, double* __restrict__ slab, int nrec) {
+           const double* __restrict__ r, double invz, const double* __restrict__ invz_vec,
+           const double* __restrict__ uvec, const double* __restrict__ rs_vec, double rs,
+           const double* __restrict__ cdiag, double* __restrict__ slab, int nrec,
+           int count_a2, double* __restrict__ alpha_out, double* __restrict__ rowq) {
   constexpr int A_SZ = T128 * SA;   // 2304
   constexpr int B_SZ = BK * SB;     // 2304
   __shared__ __attribute__((aligned(16))) double lds[2 * (A_SZ + B_SZ)];
@@ -229,6 +242,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wr = wv >> 1, wc = wv & 1;
+  const bool with_u = (uvec != nullptr);
 
   d4 acc[4][4];
 #pragma unroll
@@ -241,10 +255,13 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   const double2* gA = reinterpret_cast<const double2*>(K + (i0 + arow) * mp + acol);
   // B loader: 16 k x 128 cols, thread -> (k = tid>>4, 8 doubles at (tid&15)*8)
   const int bk = tid >> 4, bcol = (tid & 15) * 8;
-  const double2* gB = reinterpret_cast<const double2*>(P + (int64_t)bk * mp + j0 + bcol);
+  const double2* gB = reinterpret_cast<const double2*>(M + (int64_t)bk * mp + j0 + bcol);
   const int64_t bstep = BK * mp / 2;
   double2 va0, va1, va2, va3, vb0, vb1, vb2, vb3;
   const int nsteps = (int)(mp / BK);
+  // alpha folded into the k-loop: each thread dots the 8 K values it stages with u.
+  const double2* gU = reinterpret_cast<const double2*>((with_u ? uvec : M) + acol);
+  double ku = 0.0;
 
 #define CON_GLOAD(step)                                                          \
   {                                                                              \
@@ -260,8 +277,18 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     pa_[0] = va0; pa_[1] = va1; pa_[2] = va2; pa_[3] = va3;                      \
     pb_[0] = vb0; pb_[1] = vb1; pb_[2] = vb2; pb_[3] = vb3;                      \
   }
+#define CON_KU(step)                                                             \
+  if (with_u) {                                                                  \
+    const double2* ur_ = gU + (int64_t)(step) * (BK / 2);                        \
+    const double2 u0 = ur_[0], u1 = ur_[1], u2 = ur_[2], u3 = ur_[3];            \
+    ku = fma(va0.x, u0.x, ku); ku = fma(va0.y, u0.y, ku);                        \
+    ku = fma(va1.x, u1.x, ku); ku = fma(va1.y, u1.y, ku);                        \
+    ku = fma(va2.x, u2.x, ku); ku = fma(va2.y, u2.y, ku);                        \
+    ku = fma(va3.x, u3.x, ku); ku = fma(va3.y, u3.y, ku);                        \
+  }
 
   CON_GLOAD(0);
+  CON_KU(0);
   CON_SSTORE(0);
   __syncthreads();
   for (int step = 0; step < nsteps; ++step) {
@@ -284,109 +311,166 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
         for (int fn = 0; fn < 4; ++fn)
           acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
     }
-    if (step + 1 < nsteps) CON_SSTORE(cur ^ 1);
+    if (step + 1 < nsteps) {
+      CON_KU(step + 1);
+      CON_SSTORE(cur ^ 1);
+    }
     __syncthreads();
   }
 #undef CON_GLOAD
 #undef CON_SSTORE
+#undef CON_KU
 
-  // ---------------- epilogue: G = alpha u^T + acc; contract with dK/dlog(theta) ----------
-  // K_ij is read back from HBM (built once by k_build_knm; same values the GEMM used);
-  // coordinates are pre-scaled by 1/l_c (ARD) so each length-scale weight is one sub + mul.
-  const int d = kp.d;
-  const bool ard = (kp.kernel == 1);
-  const double rl2s = kp.rl2[0];
+  // ---------------- alpha (per row), shared by both epilogues ----------------
   double* s_alpha = lds;                    // 128
-  double* s_u = s_alpha + T128;             // 128
+  double* s_rs = s_alpha + T128;            // 128
+  double* s_u = s_rs + T128;                // 128
   double* s_cd = s_u + T128;                // 128
   double* s_xs = s_cd + T128;               // 128 x d   ([row][c], scaled)
-  double* s_us = s_xs + T128 * d;           // 128 x d   ([col][c], scaled)
-  for (int e = tid; e < T128; e += 256) {
-    s_alpha[e] = alpha[i0 + e];
-    const int64_t j = j0 + e;
-    s_u[e] = (j < m) ? uvec[j] : 0.0;
-    s_cd[e] = (j < m) ? cdiag[j] : 0.0;
+  double* s_us = s_xs + T128 * kp.d;        // 128 x d   ([col][c], scaled)
+  ku += __shfl_xor(ku, 1, 64);                       // the two halves of row `arow`
+  double a2 = 0.0;                                    // alpha^2, counted once (tj == 0)
+  if ((tid & 1) == 0) {
+    const int64_t i = i0 + arow;
+    const double iz = invz_vec ? invz_vec[i] : invz;
+    const double al = with_u ? (r[i] - ku) * iz : 0.0;   // padded rows: r = 0, K = 0 -> 0
+    s_alpha[arow] = al;
+    s_rs[arow] = rs_vec ? rs * rs_vec[i] : rs;
+    if (tj == 0) {
+      if (count_a2 && i < n) a2 = al * al;
+      if (alpha_out) alpha_out[i] = al;
+    }
   }
-  for (int e = tid; e < T128 * d; e += 256) {
-    const int rr = e % T128, c = e / T128;
-    const int64_t i = i0 + rr, j = j0 + rr;
-    const double sc = ard ? kp.rl[c] : 1.0;
-    s_xs[rr * d + c] = (i < n) ? X[i + c * ldx] * sc : 0.0;
-    s_us[rr * d + c] = (j < m) ? U[j + c * ldu] * sc : 0.0;
-  }
-  __syncthreads();
-
-  const int L = kp.L;
   const double* Kt = K + i0 * mp + j0;
-  double e_sig = 0.0, c_sum = 0.0, c_cnt = 0.0, c_dg = 0.0;
-  double e_l[DT];
-#pragma unroll
-  for (int c = 0; c < DT; ++c) e_l[c] = 0.0;
 
+  if constexpr (EPI == EPI_ROWQUAD) {
+    __syncthreads();
+    double* s_q = s_cd;                       // [2][128] (reuses s_cd / s_xs space)
+    // per lane: 16 rows (fm, q) x 4 cols (fn) -> row sums over this wave's 64 columns
 #pragma unroll
-  for (int fn = 0; fn < 4; ++fn) {
-    const int col = wc * 64 + fn * 16 + (lane & 15);
-    const bool cvalid = (j0 + col) < m;
-    double uj[DT];
-#pragma unroll
-    for (int c = 0; c < DT; ++c) uj[c] = (c < d) ? s_us[col * d + c] : 0.0;
-    const double ucol = s_u[col];
-#pragma unroll
-    for (int fm = 0; fm < 4; ++fm) {
+    for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
-        const bool valid = cvalid && ((i0 + row) < n);
-        const double G = fma(s_alpha[row], ucol, acc[fm][fn][q]);
-        const double gk = valid ? G * Kt[(int64_t)row * mp + col] : 0.0;
-        e_sig += gk;
-        const double* xr = &s_xs[row * d];
-        double s = 0.0;
+        double v = 0.0;
 #pragma unroll
-        for (int c = 0; c < DT; ++c) {
-          if (c < d) {
-            const double t = xr[c] - uj[c];
-            const double tt = t * t;
-            s += tt;
-            if (ard) e_l[c] = fma(gk, tt, e_l[c]);
-          }
+        for (int fn = 0; fn < 4; ++fn) {
+          const int col = wc * 64 + fn * 16 + (lane & 15);
+          v = fma(Kt[(int64_t)row * mp + col], acc[fm][fn][q], v);   // K = 0 outside (n, m)
         }
-        if (!ard) e_l[0] = fma(gk, s * rl2s, e_l[0]);
-        if (valid && s == 0.0) {
-          // rare path: tau's dK12 rule needs all(x_i == u_j) on the raw coordinates
-          bool eq = true;
-          for (int c = 0; c < d; ++c) eq = eq && (X[(i0 + row) + c * ldx] == U[(j0 + col) + c * ldu]);
-          if (eq) {
-            c_sum += G;
-            c_cnt += 1.0;
-            c_dg += s_cd[col];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        v += __shfl_xor(v, 8, 64);
+        if ((lane & 15) == 0) s_q[wc * T128 + row] = v;
+      }
+    __syncthreads();
+    if (tid < T128) rowq[tj * n_pad + i0 + tid] = s_q[tid] + s_q[T128 + tid];
+    return;
+  } else {
+    // ---------------- gradient epilogue ----------------
+    const int d = kp.d;
+    const bool ard = (kp.kernel == 1);
+    const double rl2s = kp.rl2[0];
+    for (int e = tid; e < T128; e += 256) {
+      const int64_t j = j0 + e;
+      s_u[e] = (with_u && j < m) ? uvec[j] : 0.0;
+      s_cd[e] = (cdiag && j < m) ? cdiag[j] : 0.0;
+    }
+    for (int e = tid; e < T128 * d; e += 256) {
+      const int rr = e % T128, c = e / T128;
+      const int64_t i = i0 + rr, j = j0 + rr;
+      const double sc = ard ? kp.rl[c] : 1.0;
+      s_xs[rr * d + c] = (i < n) ? X[i + c * ldx] * sc : 0.0;
+      s_us[rr * d + c] = (j < m) ? U[j + c * ldu] * sc : 0.0;
+    }
+    __syncthreads();
+
+    const int L = kp.L;
+    double e_sig = 0.0, c_sum = 0.0, c_cnt = 0.0, c_dg = 0.0;
+    double e_l[DT];
+#pragma unroll
+    for (int c = 0; c < DT; ++c) e_l[c] = 0.0;
+
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn) {
+      const int col = wc * 64 + fn * 16 + (lane & 15);
+      const bool cvalid = (j0 + col) < m;
+      double uj[DT];
+#pragma unroll
+      for (int c = 0; c < DT; ++c) uj[c] = (c < d) ? s_us[col * d + c] : 0.0;
+      const double ucol = s_u[col];
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
+          const bool valid = cvalid && ((i0 + row) < n);
+          const double G = fma(s_alpha[row], ucol, s_rs[row] * acc[fm][fn][q]);
+          const double gk = valid ? G * Kt[(int64_t)row * mp + col] : 0.0;
+          e_sig += gk;
+          const double* xr = &s_xs[row * d];
+          double s = 0.0;
+#pragma unroll
+          for (int c = 0; c < DT; ++c) {
+            if (c < d) {
+              const double t = xr[c] - uj[c];
+              const double tt = t * t;
+              s += tt;
+              if (ard) e_l[c] = fma(gk, tt, e_l[c]);
+            }
+          }
+          if (!ard) e_l[0] = fma(gk, s * rl2s, e_l[0]);
+          if (valid && s == 0.0) {
+            // rare path: tau's dK12 rule needs all(x_i == u_j) on the raw coordinates
+            bool eq = true;
+            for (int c = 0; c < d; ++c)
+              eq = eq && (X[(i0 + row) + c * ldx] == U[(j0 + col) + c * ldu]);
+            if (eq) {
+              c_sum += G;
+              c_cnt += 1.0;
+              c_dg += s_cd[col];
+            }
           }
         }
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
-    __builtin_amdgcn_sched_barrier(0);
-  }
 
-  // record = [e_sig, e_l[0..L-1], c_sum, c_cnt, c_dg]
-  double v;
-  v = wave_sum(e_sig);
-  if (lane == 0) red[wv][0] = v;
+    // record = [e_sig, e_l[0..L-1], c_sum, c_cnt, c_dg, alpha^T alpha]
+    double v;
+    v = wave_sum(e_sig);
+    if (lane == 0) red[wv][0] = v;
 #pragma unroll
-  for (int c = 0; c < DT; ++c) {
-    if (c < L) {
-      v = wave_sum(e_l[c]);
-      if (lane == 0) red[wv][1 + c] = v;
+    for (int c = 0; c < DT; ++c) {
+      if (c < L) {
+        v = wave_sum(e_l[c]);
+        if (lane == 0) red[wv][1 + c] = v;
+      }
     }
+    v = wave_sum(c_sum);
+    if (lane == 0) red[wv][1 + L] = v;
+    v = wave_sum(c_cnt);
+    if (lane == 0) red[wv][2 + L] = v;
+    v = wave_sum(c_dg);
+    if (lane == 0) red[wv][3 + L] = v;
+    v = wave_sum(a2);
+    if (lane == 0) red[wv][4 + L] = v;
+    __syncthreads();
+    if (tid < nrec)
+      slab[wgid * nrec + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
   }
-  v = wave_sum(c_sum);
-  if (lane == 0) red[wv][1 + L] = v;
-  v = wave_sum(c_cnt);
-  if (lane == 0) red[wv][2 + L] = v;
-  v = wave_sum(c_dg);
-  if (lane == 0) red[wv][3 + L] = v;
-  __syncthreads();
-  if (tid < nrec)
-    slab[wgid * nrec + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+}
+
+// rowq[tj][i] summed over the column tiles -> out[i] (deterministic order)
+__global__ void __launch_bounds__(256)
+k_rowq_reduce(const double* __restrict__ rowq, int64_t ntj, int64_t n_pad,
+              double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n_pad) return;
+  double s = 0.0;
+  for (int64_t t = 0; t < ntj; ++t) s += rowq[t * n_pad + i];
+  out[i] = s;
 }
 
 // ============================================================================ generic 64x64 GEMM
@@ -511,23 +595,41 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
   return hipGetLastError();
 }
 
-hipError_t launch_contract_knm(const KernParams& kp, const double* K, const double* P,
+hipError_t launch_contract_knm(const KernParams& kp, const double* K, const double* M,
                                const double* X, int64_t ldx, int64_t n, int64_t n_pad,
                                const double* U, int64_t ldu, int64_t m, int64_t mp,
-                               const double* alpha, const double* uvec,
-                               const double* coinc_diag, double* slab, int64_t* nrec_out,
-                               int64_t* nwg_out, hipStream_t s) {
+                               const double* r, double invz, const double* invz_vec,
+                               const double* uvec, const double* rs_vec, double rs,
+                               const double* coinc_diag, int count_a2, double* slab,
+                               int64_t* nrec_out, int64_t* nwg_out, hipStream_t s) {
   const int64_t nwg = (n_pad / T128) * (mp / T128);
-  const int nrec = kp.L + 4;
+  const int nrec = kp.L + 5;
   *nrec_out = nrec;
   *nwg_out = nwg;
   if (kp.d <= 8) {
-    hipLaunchKernelGGL(k_contract<8>, dim3((unsigned)nwg), dim3(256), 0, s, kp, K, P, X, ldx,
-                       n, n_pad, U, ldu, m, mp, alpha, uvec, coinc_diag, slab, nrec);
+    hipLaunchKernelGGL((k_contract<8, EPI_GRAD>), dim3((unsigned)nwg), dim3(256), 0, s, kp, K, M,
+                       X, ldx, n, n_pad, U, ldu, m, mp, r, invz, invz_vec, uvec, rs_vec, rs,
+                       coinc_diag, slab, nrec, count_a2, (double*)nullptr, (double*)nullptr);
   } else {
-    hipLaunchKernelGGL(k_contract<SGP_MAXD>, dim3((unsigned)nwg), dim3(256), 0, s, kp, K, P, X,
-                       ldx, n, n_pad, U, ldu, m, mp, alpha, uvec, coinc_diag, slab, nrec);
+    hipLaunchKernelGGL((k_contract<SGP_MAXD, EPI_GRAD>), dim3((unsigned)nwg), dim3(256), 0, s, kp,
+                       K, M, X, ldx, n, n_pad, U, ldu, m, mp, r, invz, invz_vec, uvec, rs_vec,
+                       rs, coinc_diag, slab, nrec, count_a2, (double*)nullptr, (double*)nullptr);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_rowquad_knm(const KernParams& kp, const double* K, const double* M, int64_t n,
+                              int64_t n_pad, int64_t m, int64_t mp, const double* r,
+                              double invz, const double* invz_vec, const double* uvec,
+                              double* alpha_out, double* rowq_slab, double* out,
+                              hipStream_t s) {
+  const int64_t nwg = (n_pad / T128) * (mp / T128);
+  hipLaunchKernelGGL((k_contract<8, EPI_ROWQUAD>), dim3((unsigned)nwg), dim3(256), 0, s, kp, K, M,
+                     (const double*)nullptr, (int64_t)0, n, n_pad, (const double*)nullptr,
+                     (int64_t)0, m, mp, r, invz, invz_vec, uvec, (const double*)nullptr, 1.0,
+                     (const double*)nullptr, (double*)nullptr, 0, 0, alpha_out, rowq_slab);
+  hipLaunchKernelGGL(k_rowq_reduce, dim3((unsigned)((n_pad + 255) / 256)), dim3(256), 0, s,
+                     rowq_slab, mp / T128, n_pad, out);
   return hipGetLastError();
 }
 

@@ -86,15 +86,26 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
                            const double* w, double* slab, int64_t slab_cap, double* red,
                            hipStream_t s, int part = 3);  // part: 1 = main kernel, 2 = reduce
 int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp);
-// Contraction: G = alpha u^T + K P (K: n_pad x mp, P: mp x mp); accumulates per 128x128 tile
-//   sum G*K, sum G*K*w_l(d) per length scale, and the tau-coincidence sums.
-//   coinc_diag = diag(K22inv) (mp).  Per-tile records go to slab[wgid * nrec].
-hipError_t launch_contract_knm(const KernParams& kp, const double* K, const double* P,
+// Gradient contraction on T = K M (K: n_pad x mp, M: mp x mp):
+//   G_ij = alpha_i u_j + rs_i T_ij,  alpha_i = (r_i - K_i u) * iz_i computed in the same pass
+//   (iz_i = invz_vec ? invz_vec[i] : invz; uvec == nullptr -> alpha = u = 0;
+//   rs_i = rs_vec ? rs * rs_vec[i] : rs).  Per 128x128 tile record (L + 5 doubles):
+//   [sum G*K, sum G*K*w_c (c < L), tau-coincidence sum G, count, sum diag_j, alpha^T alpha
+//   (only if count_a2)].  coinc_diag may be nullptr.
+hipError_t launch_contract_knm(const KernParams& kp, const double* K, const double* M,
                                const double* X, int64_t ldx, int64_t n, int64_t n_pad,
                                const double* U, int64_t ldu, int64_t m, int64_t mp,
-                               const double* alpha, const double* uvec,
-                               const double* coinc_diag, double* slab, int64_t* nrec_out,
-                               int64_t* nwg_out, hipStream_t s);
+                               const double* r, double invz, const double* invz_vec,
+                               const double* uvec, const double* rs_vec, double rs,
+                               const double* coinc_diag, int count_a2, double* slab,
+                               int64_t* nrec_out, int64_t* nwg_out, hipStream_t s);
+// out_i = sum_j K_ij (K M)_ij = diag(K M K^T) (n_pad); optional fused alpha as above.
+// rowq_slab: (mp/128) x n_pad work.
+hipError_t launch_rowquad_knm(const KernParams& kp, const double* K, const double* M, int64_t n,
+                              int64_t n_pad, int64_t m, int64_t mp, const double* r,
+                              double invz, const double* invz_vec, const double* uvec,
+                              double* alpha_out, double* rowq_slab, double* out,
+                              hipStream_t s);
 // generic m x m GEMM on f64 MFMA: C = alpha*op(A)*op(B) + beta*C, sizes multiples of 64.
 hipError_t launch_gemm64(bool transA, bool transB, bool lower_only, int64_t M, int64_t N,
                          int64_t K, double alpha, const double* A, int64_t lda,
@@ -110,6 +121,11 @@ hipError_t dense_potrf(double* A, int64_t mp, int64_t lda, double* dinv, double*
 // X = L^{-1} (lower), using the dinv blocks of dense_potrf.  X must be mp x mp.
 hipError_t dense_trtri(const double* L, int64_t mp, int64_t lda, const double* dinv, double* X,
                        int64_t ldx, double* T, hipStream_t s);
+// In-place inverse of an SPD matrix A (mp x mp, full storage) by blocked Gauss-Jordan with
+// 64-wide pivots; logd[k] = sum log L_ii of the k-th pivot block's Cholesky factor, so
+// log det A = 2 * sum_k logd[k].  Work: R (64 x mp), Cb (mp x 64), P (64 x 64).
+hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* Cb, double* P,
+                             double* logd, int* status, hipStream_t s);
 // Ainv = X^T X
 hipError_t dense_inv_from_trtri(const double* X, int64_t mp, double* Ainv, hipStream_t s);
 // C = a*A + b*B elementwise over mp x mp
@@ -133,3 +149,12 @@ hipError_t launch_colsum(const double* slab, int64_t nrows, int64_t ncol, double
 hipError_t launch_diag(const double* A, int64_t mp, int64_t lda, double* out, hipStream_t s);
 // sum of per-block logs -> out
 hipError_t launch_sum_small(const double* v, int64_t count, double* out, hipStream_t s);
+
+// FITC per-row helpers (k_dense.hip).
+// w_i = 1 / (c0 - q_i) for i < n (0 for padded rows); per-block sums of log(c0 - q_i) -> slab.
+hipError_t launch_fitc_z(const double* q, int64_t n, int64_t n_pad, double c0, double* w,
+                         double* slab, int* nblocks, hipStream_t s);
+// omega_i = alpha_i^2 - (w_i - w_i^2 p_i) for i < n (0 otherwise); per-block sums -> slab.
+hipError_t launch_fitc_omega(const double* alpha, const double* w, const double* p, int64_t n,
+                             int64_t n_pad, double* omega, double* slab, int* nblocks,
+                             hipStream_t s);

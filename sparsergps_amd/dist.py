@@ -28,9 +28,11 @@ def shard_rows(n, world, rank):
 
 
 class HipRowBackend:
-    """libsgp.so context over this rank's rows; reduction buffers are torch device tensors."""
+    """libsgp.so context over this rank's rows; reduction buffers are torch device tensors.
+    mode "vi" (sgp_vi_*) or "fitc" (sgp_fitc_*): both are phase1 -> sum -> phase2 -> sum ->
+    finish."""
 
-    def __init__(self, X_local, y_local, mu_local, m_max, device_index, cov_fun):
+    def __init__(self, X_local, y_local, mu_local, m_max, device_index, cov_fun, mode="vi"):
         import torch
 
         from .vi import SparseGPContext
@@ -38,9 +40,17 @@ class HipRowBackend:
         self.dev = torch.device("cuda", device_index)
         self.ctx = SparseGPContext(X_local, y_local, mu_local, m_max=m_max, device=device_index)
         self.cov_fun = cov_fun
-        self.red1 = torch.zeros(self.ctx.vi_red1_count(m_max), dtype=torch.float64, device=self.dev)
-        self.red2 = torch.zeros(self.ctx.vi_red2_count(cov_fun), dtype=torch.float64, device=self.dev)
-        self.nparams = self.red2.numel() - 3
+        self.mode = mode
+        L = self.ctx.d if cov_fun == "ard" else 1
+        self.nparams = L + 2
+        if mode == "vi":
+            n1, n2 = self.ctx.vi_red1_count(m_max), self.ctx.vi_red2_count(cov_fun)
+        elif mode == "fitc":
+            n1, n2 = self.ctx.fitc_red1_count(m_max), self.ctx.fitc_red2_count(cov_fun, m_max)
+        else:
+            raise ValueError(mode)
+        self.red1 = torch.zeros(n1, dtype=torch.float64, device=self.dev)
+        self.red2 = torch.zeros(n2, dtype=torch.float64, device=self.dev)
         # A dedicated (non-null) stream shared by libsgp's launches and torch.distributed:
         # RowShardedVI issues its collectives under stream_context(), so every all-reduce is
         # ordered after the kernels that produced its buffer, with no host synchronisation.
@@ -51,17 +61,28 @@ class HipRowBackend:
         return self.torch.cuda.stream(self.stream)
 
     def phase1(self, theta, U, delta):
-        n1 = self.ctx.vi_red1_count(np.asarray(U).shape[0])
-        buf = self.red1[:n1]
-        self.ctx.vi_phase1(theta, self.cov_fun, U, delta, buf.data_ptr())
+        m = np.asarray(U).shape[0]
+        if self.mode == "vi":
+            buf = self.red1[:self.ctx.vi_red1_count(m)]
+            self.ctx.vi_phase1(theta, self.cov_fun, U, delta, buf.data_ptr())
+        else:
+            buf = self.red1[:self.ctx.fitc_red1_count(m)]
+            self.ctx.fitc_phase1(theta, self.cov_fun, U, delta, buf.data_ptr())
+        self._m = m
         return buf
 
     def phase2(self, red1, n_global):
-        self.ctx.vi_phase2(red1.data_ptr(), n_global, self.red2.data_ptr())
-        return self.red2
+        if self.mode == "vi":
+            self.ctx.vi_phase2(red1.data_ptr(), n_global, self.red2.data_ptr())
+            return self.red2
+        buf = self.red2[:self.ctx.fitc_red2_count(self.cov_fun, self._m)]
+        self.ctx.fitc_phase2(red1.data_ptr(), n_global, buf.data_ptr())
+        return buf
 
     def finish(self, red2):
-        return self.ctx.vi_finish(red2.data_ptr(), self.nparams)
+        if self.mode == "vi":
+            return self.ctx.vi_finish(red2.data_ptr(), self.nparams)
+        return self.ctx.fitc_finish(red2.data_ptr(), self.nparams)
 
     def close(self):
         self.ctx.close()

@@ -118,6 +118,19 @@ class SparseGPContext:
         _lib.check(st)
         return obj.value, grad
 
+    def eval_fitc(self, theta, cov_fun, xu, delta=1e-6, r_det=False):
+        """FITC log marginal likelihood and d/d log(theta) (obj_fun_norm + dlogp_dcov_par)."""
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        U, m = self._knots(xu)
+        obj = C.c_double(0.0)
+        grad = np.zeros(theta.size, dtype=np.float64)
+        st = self._lib.sgp_eval_fitc(self.handle, _lib.KERNELS[cov_fun], _lib.dptr(theta),
+                                     _lib.dptr(U), m, m, float(delta),
+                                     _lib.SGP_FLAG_R_DET if r_det else 0, C.byref(obj),
+                                     _lib.dptr(grad))
+        _lib.check(st)
+        return obj.value, grad
+
     # multi-GPU phases (device buffers passed as integer pointers, e.g. tensor.data_ptr())
     def vi_red1_count(self, m):
         return int(self._lib.sgp_vi_red1_count(int(m)))
@@ -135,6 +148,30 @@ class SparseGPContext:
         _lib.check(self._lib.sgp_vi_phase2(self.handle, C.c_void_p(red1_ptr), int(n_global),
                                            _lib.SGP_FLAG_R_DET if r_det else 0,
                                            C.c_void_p(red2_ptr)))
+
+    def fitc_red1_count(self, m):
+        return int(self._lib.sgp_fitc_red1_count(int(m)))
+
+    def fitc_red2_count(self, cov_fun, m):
+        return int(self._lib.sgp_fitc_red2_count(_lib.KERNELS[cov_fun], self.d, int(m)))
+
+    def fitc_phase1(self, theta, cov_fun, xu, delta, red1_ptr):
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        U, m = self._knots(xu)
+        _lib.check(self._lib.sgp_fitc_phase1(self.handle, _lib.KERNELS[cov_fun], _lib.dptr(theta),
+                                             _lib.dptr(U), m, m, float(delta), C.c_void_p(red1_ptr)))
+
+    def fitc_phase2(self, red1_ptr, n_global, red2_ptr, r_det=False):
+        _lib.check(self._lib.sgp_fitc_phase2(self.handle, C.c_void_p(red1_ptr), int(n_global),
+                                             _lib.SGP_FLAG_R_DET if r_det else 0,
+                                             C.c_void_p(red2_ptr)))
+
+    def fitc_finish(self, red2_ptr, nparams):
+        obj = C.c_double(0.0)
+        grad = np.zeros(nparams, dtype=np.float64)
+        _lib.check(self._lib.sgp_fitc_finish(self.handle, C.c_void_p(red2_ptr), C.byref(obj),
+                                             _lib.dptr(grad)))
+        return obj.value, grad
 
     def vi_finish(self, red2_ptr, nparams):
         obj = C.c_double(0.0)
@@ -178,6 +215,37 @@ def vi_eval(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6, ctx=None, r_det=False):
     byname = dict(zip(names, g))
     grad = OrderedDict((k, float(byname[k])) for k in cov_par.keys())
     return obj, grad
+
+
+def fitc_eval(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6, ctx=None, r_det=False):
+    """One fused FITC evaluation: (log marginal likelihood, OrderedDict gradient) with Z and the
+    matrices built as norm_grad_ascent does (laplace_gradient_ascent.R:1238-1263)."""
+    xy_m = np.asarray(xy, dtype=np.float64)
+    d = 1 if xy_m.ndim == 1 else xy_m.shape[1]
+    lnames = [f"l{c + 1}" for c in range(d)] if cov_fun == "ard" else None
+    theta = theta_vector(cov_par, cov_fun, d, lnames)
+    names = param_names(cov_fun, d, lnames)
+    xu_m = np.asarray(xu, dtype=np.float64).reshape(-1, d)
+    if ctx is None:
+        ctx = _context_for(xy, y, mu, xu_m.shape[0])
+    obj, g = ctx.eval_fitc(theta, cov_fun, xu_m, delta, r_det=r_det)
+    byname = dict(zip(names, g))
+    return obj, OrderedDict((k, float(byname[k])) for k in cov_par.keys())
+
+
+def dlogp_dcov_par(cov_par, cov_fun, dcov_fun_dtheta=True, dcov_fun_dknot=None, knot_opt=None,
+                   xu=None, xy=None, y=None, ff=None, mu=None, transform=True, delta=1e-6,
+                   ctx=None):
+    """laplace_approx_gradient.R:720-971 (FITC, knots fixed): {"gradient", "trans_par"}."""
+    if dcov_fun_dknot is not None and dcov_fun_dknot is not False:
+        raise NotImplementedError("knot gradients (xu_opt='simultaneous') are not in this build")
+    if mu is None:
+        mu = np.mean(np.asarray(y, dtype=np.float64))
+    _, grad = fitc_eval(cov_par, cov_fun, xu, xy, y, _mu_vec(mu, y), delta, ctx=ctx)
+    if not dcov_fun_dtheta:
+        grad = 0
+    trans_par = OrderedDict((k, float(np.log(v))) for k, v in cov_par.items())
+    return {"gradient": grad, "trans_par": trans_par}
 
 
 def elbo_fun(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6, ctx=None, r_det=False):

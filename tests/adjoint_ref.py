@@ -86,7 +86,7 @@ class NumpyVIRank:
         alpha = (self.r - self.K @ u) / z
         G = np.outer(alpha, u) + self.K @ P
         GK = G * self.K
-        red2 = [alpha @ alpha, np.sum(GK)]
+        red2 = [np.sum(GK)]
         if self.kernel == "sqexp":
             red2.append(np.sum(GK * np.sum(self.diff ** 2, axis=2) / self.ls[0] ** 2))
         else:
@@ -94,8 +94,8 @@ class NumpyVIRank:
                 red2.append(np.sum(GK * (self.diff[:, :, c] / self.ls[c]) ** 2))
         coinc = np.all(self.diff == 0.0, axis=2)
         red2 += [np.sum(G[coinc]), float(np.sum(coinc)),
-                 float(np.sum(np.broadcast_to(np.diag(K22inv), coinc.shape)[coinc]))]
-        return np.array(red2)
+                 float(np.sum(np.broadcast_to(np.diag(K22inv), coinc.shape)[coinc])), alpha @ alpha]
+        return np.array(red2)      # [e_sig, e_l(L), c_sum, c_cnt, c_dg, alpha^T alpha]
 
     # ---- finish: objective + gradient from the reduced red2 and the replicated scalars
     def finish(self, red2):
@@ -108,12 +108,12 @@ class NumpyVIRank:
         det_part = -0.5 * (n * math.log(z) - ld22 + ldB)
         T = -(1.0 / (2 * tau2)) * (n * (sig2 + delta) - sc["trKS"])
         obj = quad + det_part - n / 2 * math.log(2 * math.pi) + T
-        aTa, e_sig = red2[0], red2[1]
-        c_sum, c_cnt, c_dg = red2[2 + L], red2[3 + L], red2[4 + L]
+        e_sig = red2[0]
+        c_sum, c_cnt, c_dg, aTa = red2[1 + L], red2[2 + L], red2[3 + L], red2[4 + L]
         trW = 0.5 * (aTa - (n / z - sc["trBS"] / z ** 2))
         grad = np.zeros(L + 2)
         grad[0] = 2 * e_sig + sc["g22"][0] - n * sig2 / tau2
-        grad[1:L + 1] = red2[2:2 + L] + sc["g22"][1:]
+        grad[1:L + 1] = red2[1:1 + L] + sc["g22"][1:]
         grad[L + 1] = 2 * tau2 * (c_sum - (c_cnt - delta * c_dg) / tau2) + 2 * tau2 * trW - 2 * T
         return obj, grad
 
@@ -123,3 +123,122 @@ def eval_vi(kernel, theta, X, y, mu, U, delta=1e-6):
     red1 = rk.phase1(kernel, theta, U, delta)
     red2 = rk.phase2(red1, X.shape[0])
     return rk.finish(red2)
+
+
+# ------------------------------------------------------------------------------ FITC model
+def eval_fitc(kernel, theta, X, y, mu, U, delta=1e-6):
+    """Adjoint-form FITC objective + gradient (mirrors sgp_fitc_* in capi.hip)."""
+    X, U = np.asarray(X, dtype=np.float64), np.asarray(U, dtype=np.float64)
+    r = np.asarray(y, dtype=np.float64) - np.asarray(mu, dtype=np.float64)
+    n, d = X.shape
+    m = U.shape[0]
+    L, sigma, tau, ls = _params(kernel, theta, d)
+    tau2, sig2 = tau ** 2, sigma ** 2
+    K, diff = _kmat(kernel, X, U, sigma, ls)
+    Kuu, dU = _kmat(kernel, U, U, sigma, ls)
+    K22 = Kuu.copy()
+    K22[np.diag_indices(m)] = ((np.diag(Kuu) + tau2) + delta) - tau2
+    K22inv = np.linalg.inv(K22)
+    q = np.sum(K * (K @ K22inv), axis=1)
+    Z = sig2 + tau2 + delta - q
+    w = 1 / Z
+    S = K.T @ (w[:, None] * K)
+    t = K.T @ (w * r)
+    rr = r @ (w * r)
+    Bm = K22 + S
+    Binv = np.linalg.inv(Bm)
+    u = Binv @ t
+    _, ld22 = np.linalg.slogdet(K22)
+    _, ldB = np.linalg.slogdet(Bm)
+    obj = -0.5 * rr + 0.5 * t @ u - 0.5 * (np.sum(np.log(Z)) - ld22 + ldB) - n / 2 * math.log(2 * math.pi)
+    alpha = w * (r - K @ u)
+    p = np.sum(K * (K @ Binv), axis=1)
+    omega = alpha ** 2 - (w - w * w * p)
+    Som = K.T @ (omega[:, None] * K)
+    G = np.outer(alpha, u) - w[:, None] * (K @ Binv) - omega[:, None] * (K @ K22inv)
+    G22 = -0.5 * np.outer(u, u) + 0.5 * (K22inv - Binv) + 0.5 * K22inv @ Som @ K22inv
+    GK = G * K
+    grad = np.zeros(L + 2)
+    grad[0] = 2 * np.sum(GK) + np.sum(G22 * 2 * Kuu) + sig2 * np.sum(omega)
+    if kernel == "sqexp":
+        grad[1] = np.sum(GK * np.sum(diff ** 2, axis=2)) / ls[0] ** 2 + \
+            np.sum(G22 * Kuu * np.sum(dU ** 2, axis=2)) / ls[0] ** 2
+    else:
+        for c in range(L):
+            grad[1 + c] = np.sum(GK * (diff[:, :, c] / ls[c]) ** 2) + np.sum(G22 * Kuu * (dU[:, :, c] / ls[c]) ** 2)
+    coinc = np.all(diff == 0.0, axis=2)
+    grad[L + 1] = 2 * tau2 * np.sum(G[coinc]) + tau2 * np.sum(omega)
+    return obj, grad
+
+
+class NumpyFITCRank:
+    """One rank of the FITC protocol (mirrors sgp_fitc_phase1/phase2/finish buffer layouts,
+    without padding): red1 = [S_D, t, rr, sum log Z], red2 = [S_omega, sum omega, rec1, rec2]."""
+
+    def __init__(self, X, y, mu):
+        self.X = np.asarray(X, dtype=np.float64)
+        self.r = np.asarray(y, dtype=np.float64) - np.asarray(mu, dtype=np.float64)
+
+    def phase1(self, kernel, theta, U, delta):
+        d = self.X.shape[1]
+        self.kernel, self.U, self.delta = kernel, np.asarray(U), delta
+        L, sigma, tau, ls = _params(kernel, theta, d)
+        self.L, self.sigma, self.tau, self.ls = L, sigma, tau, ls
+        m = self.U.shape[0]
+        self.K, self.diff = _kmat(kernel, self.X, self.U, sigma, ls)
+        Kuu, self.dU = _kmat(kernel, self.U, self.U, sigma, ls)
+        self.Kuu = Kuu
+        K22 = Kuu.copy()
+        K22[np.diag_indices(m)] = ((np.diag(Kuu) + tau ** 2) + delta) - tau ** 2
+        self.K22, self.K22inv = K22, np.linalg.inv(K22)
+        q = np.sum(self.K * (self.K @ self.K22inv), axis=1)
+        Z = sigma ** 2 + tau ** 2 + delta - q
+        self.w = 1 / Z
+        red1 = np.zeros(m * m + m + 2)
+        red1[:m * m] = (self.K.T @ (self.w[:, None] * self.K)).reshape(-1)
+        red1[m * m:m * m + m] = self.K.T @ (self.w * self.r)
+        red1[m * m + m] = self.r @ (self.w * self.r)
+        red1[m * m + m + 1] = np.sum(np.log(Z))
+        return red1
+
+    def phase2(self, red1, n_global):
+        m = self.U.shape[0]
+        S, t = red1[:m * m].reshape(m, m), red1[m * m:m * m + m]
+        self.rr, self.sumlogz, self.n_global = red1[m * m + m], red1[m * m + m + 1], n_global
+        Bm = self.K22 + S
+        self.Binv = np.linalg.inv(Bm)
+        self.ld22, self.ldB = np.linalg.slogdet(self.K22)[1], np.linalg.slogdet(Bm)[1]
+        u = self.Binv @ t
+        self.u, self.tu = u, t @ u
+        K, w = self.K, self.w
+        alpha = w * (self.r - K @ u)
+        p = np.sum(K * (K @ self.Binv), axis=1)
+        omega = alpha ** 2 - (w - w * w * p)
+        G = np.outer(alpha, u) - w[:, None] * (K @ self.Binv) - omega[:, None] * (K @ self.K22inv)
+        GK = G * K
+        rec = [np.sum(GK)]
+        if self.kernel == "sqexp":
+            rec.append(np.sum(GK * np.sum(self.diff ** 2, axis=2)) / self.ls[0] ** 2)
+        else:
+            rec += [np.sum(GK * (self.diff[:, :, c] / self.ls[c]) ** 2) for c in range(self.L)]
+        rec.append(np.sum(G[np.all(self.diff == 0.0, axis=2)]))
+        red2 = np.concatenate([(K.T @ (omega[:, None] * K)).reshape(-1), [np.sum(omega)], rec])
+        return red2
+
+    def finish(self, red2):
+        m, L = self.U.shape[0], self.L
+        Som, sum_om, rec = red2[:m * m].reshape(m, m), red2[m * m], red2[m * m + 1:]
+        n, tau2, sig2 = float(self.n_global), self.tau ** 2, self.sigma ** 2
+        obj = -0.5 * self.rr + 0.5 * self.tu - 0.5 * (self.sumlogz - self.ld22 + self.ldB) - \
+            n / 2 * math.log(2 * math.pi)
+        G22 = -0.5 * np.outer(self.u, self.u) + 0.5 * (self.K22inv - self.Binv) + \
+            0.5 * self.K22inv @ Som @ self.K22inv
+        grad = np.zeros(L + 2)
+        grad[0] = 2 * rec[0] + np.sum(G22 * 2 * self.Kuu) + sig2 * sum_om
+        if self.kernel == "sqexp":
+            grad[1] = rec[1] + np.sum(G22 * self.Kuu * np.sum(self.dU ** 2, axis=2)) / self.ls[0] ** 2
+        else:
+            for c in range(L):
+                grad[1 + c] = rec[1 + c] + np.sum(G22 * self.Kuu * (self.dU[:, :, c] / self.ls[c]) ** 2)
+        grad[L + 1] = 2 * tau2 * rec[1 + L] + tau2 * sum_om
+        return obj, grad

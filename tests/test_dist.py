@@ -28,9 +28,9 @@ def _free_port():
 class NumpyBackend:
     """Test backend: numpy phases, torch CPU tensors as the reduction buffers."""
 
-    def __init__(self, X, y, mu, cov_fun):
+    def __init__(self, X, y, mu, cov_fun, mode="vi"):
         import adjoint_ref
-        self.rk = adjoint_ref.NumpyVIRank(X, y, mu)
+        self.rk = (adjoint_ref.NumpyVIRank if mode == "vi" else adjoint_ref.NumpyFITCRank)(X, y, mu)
         self.cov_fun = cov_fun
 
     def phase1(self, theta, U, delta):
@@ -43,7 +43,7 @@ class NumpyBackend:
         return self.rk.finish(red2.numpy())
 
 
-def _worker(rank, world, port, cfg, n, m, coinc, q):
+def _worker(rank, world, port, cfg, n, m, coinc, q, mode="vi"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -54,26 +54,31 @@ def _worker(rank, world, port, cfg, n, m, coinc, q):
         if coinc:
             U[:3] = P["X"][[0, n // 2, n - 1]]
         s0, s1 = shard_rows(n, world, rank)
-        be = NumpyBackend(P["X"][s0:s1], P["y"][s0:s1], P["mu"][s0:s1], P["cov_fun"])
+        be = NumpyBackend(P["X"][s0:s1], P["y"][s0:s1], P["mu"][s0:s1], P["cov_fun"], mode)
         runner = RowShardedVI(be, n)
         theta = np.array(list(P["cov_par"].values()))
         obj, grad = runner.eval(theta, U, P["delta"])
         if rank == 0:
-            o = O.elbo_eval(P["cov_par"], P["cov_fun"], U, P["X"], P["y"], P["mu"], P["delta"])
-            g = O.delbo_dcov_par(P["cov_par"], P["cov_fun"], U, P["X"], P["y"], P["mu"], P["delta"])
+            fo, fg = (O.elbo_eval, O.delbo_dcov_par) if mode == "vi" else (O.fitc_obj_eval, O.dlogp_dcov_par)
+            o = fo(P["cov_par"], P["cov_fun"], U, P["X"], P["y"], P["mu"], P["delta"])
+            g = fg(P["cov_par"], P["cov_fun"], U, P["X"], P["y"], P["mu"], P["delta"])
             gv = np.array(list(g["gradient"].values()))
             q.put((abs(obj - o) / abs(o), float(np.max(np.abs(grad - gv) / np.maximum(1, np.abs(gv))))))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,cfg,n,m,coinc", [(2, "C2", 301, 17, False), (2, "C3", 250, 11, True),
-                                                  (3, "C2", 200, 9, True)])
-def test_row_sharded_vi_gloo(world, cfg, n, m, coinc):
+@pytest.mark.parametrize("world,cfg,n,m,coinc,mode", [(2, "C2", 301, 17, False, "vi"),
+                                                       (2, "C3", 250, 11, True, "vi"),
+                                                       (3, "C2", 200, 9, True, "vi"),
+                                                       (2, "C3", 240, 10, True, "fitc"),
+                                                       (3, "C2", 211, 12, False, "fitc")])
+def test_row_sharded_gloo(world, cfg, n, m, coinc, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, n, m, coinc, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, n, m, coinc, q, mode))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

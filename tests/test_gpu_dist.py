@@ -18,7 +18,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
@@ -31,24 +31,27 @@ def _worker(rank, world, port, q):
         U = P["U"].copy()
         U[:2] = P["X"][[5, 2999]]                     # coincident knots on both shards
         s0, s1 = shard_rows(3001, world, rank)
-        be = HipRowBackend(P["X"][s0:s1], P["y"][s0:s1], P["mu"][s0:s1], 200, 0, "ard")
+        be = HipRowBackend(P["X"][s0:s1], P["y"][s0:s1], P["mu"][s0:s1], 200, 0, "ard", mode)
         theta = np.array(list(P["cov_par"].values()))
         obj, grad = RowShardedVI(be, 3001).eval(theta, U, P["delta"])
         be.close()
         if rank == 0:
-            o = O.elbo_eval(P["cov_par"], "ard", U, P["X"], P["y"], P["mu"], P["delta"])
-            g = np.array(list(O.delbo_dcov_par(P["cov_par"], "ard", U, P["X"], P["y"], P["mu"],
-                                               P["delta"])["gradient"].values()))
+            fo, fg = (O.elbo_eval, O.delbo_dcov_par) if mode == "vi" else (O.fitc_obj_eval,
+                                                                            O.dlogp_dcov_par)
+            o = fo(P["cov_par"], "ard", U, P["X"], P["y"], P["mu"], P["delta"])
+            g = np.array(list(fg(P["cov_par"], "ard", U, P["X"], P["y"], P["mu"],
+                                 P["delta"])["gradient"].values()))
             q.put((abs(obj - o) / abs(o), float(np.max(np.abs(grad - g) / np.maximum(1, np.abs(g))))))
     finally:
         dist.destroy_process_group()
 
 
-def test_two_ranks_one_gpu_gloo():
+@pytest.mark.parametrize("mode", ["vi", "fitc"])
+def test_two_ranks_one_gpu_gloo(mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, mode)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:

@@ -169,3 +169,22 @@ def test_r_det_quirk(sgp):
     a, _ = sgp.vi_eval(P["cov_par"], "sqexp", P["U"], P["X"], P["y"], P["mu"], P["delta"])
     b, _ = sgp.vi_eval(P["cov_par"], "sqexp", P["U"], P["X"], P["y"], P["mu"], P["delta"], r_det=True)
     assert abs(a - b) / abs(a) < 1e-12
+
+
+def test_repeated_evals_full_knot_count(sgp):
+    """Several evaluations at m = 1024 (16 Gauss-Jordan pivots, both streams busy) with the
+    timing scopes on: regression for a replay fault seen with hipGraph capture enabled."""
+    P = _problem("C3", 20000, 1024)
+    th = np.array(list(P["cov_par"].values()))
+    with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=1024) as ctx:
+        outs = []
+        for k in range(4):
+            if k == 1:
+                ctx.enable_timing(True)
+            outs.append(ctx.eval_vi(th * (1 + 1e-3 * k), "ard", P["U"], P["delta"]))
+            if k >= 1:
+                assert any(name == "contract_knm" for name, _ in ctx.timings())
+    import adjoint_ref as A
+    o, g = A.eval_vi("ard", th * (1 + 3e-3), P["X"], P["y"], P["mu"], P["U"], P["delta"])
+    assert abs(outs[-1][0] - o) / abs(o) < 1e-9
+    assert _rel(outs[-1][1], g) < 1e-7
