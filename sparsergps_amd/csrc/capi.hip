@@ -149,7 +149,9 @@ namespace {
 constexpr int SC_LD22 = 0, SC_LDB = 1, SC_TU = 2, SC_TRKS = 3, SC_TRBS = 4, SC_RR = 5,
               SC_G22 = 8;  // SC_G22 .. SC_G22 + P - 2
 constexpr int SC_N = 64;
-constexpr int SLAB_SMALL = 4096;
+// per-block partials of the small reductions: k_contract_kmm writes up to 1024 blocks x (P-1)
+// records (P <= SGP_MAXD + 2), the dot/colsum helpers at most 1024 x 1
+constexpr int SLAB_SMALL = 1024 * (SGP_MAXD + 2);
 
 hipEvent_t pool_event(sgp_ctx* c) {
   if (c->pool_used < c->pool.size()) return c->pool[c->pool_used++];
@@ -692,7 +694,7 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
     Scope tm(c, "contract_kmm");
     int nb = 0;
     HIPCHK(launch_contract_kmm(kp, c->U, c->mp, c->m, mp, c->uvec, c->K22inv, c->Binv, c->M3,
-                               -0.5, 0.5, -1.0 / (2.0 * kp.tau2), c->slab_small, &nb,
+                               -0.5, 0.5, -1.0 / (2.0 * kp.tau2), c->slab_small, SLAB_SMALL, &nb,
                                c->stream));
     HIPCHK(launch_colsum(c->slab_small, nb, kp.P - 1, c->sc + SC_G22, c->stream));
   }
@@ -730,6 +732,12 @@ int sgp_vi_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
             status[0] ? status[0] : status[1],
             status[0] ? "Sigma22" : "Sigma22 + t(Sigma12) %*% ZSig12");
     return SGP_ENOTPD;
+  }
+  if (getenv("SGP_DEBUG_SC")) {
+    fprintf(stderr, "[sgp sc] ld22 %.17g ldB %.17g tu %.17g trKS %.17g trBS %.17g rr %.17g g22",
+            sc[SC_LD22], sc[SC_LDB], sc[SC_TU], sc[SC_TRKS], sc[SC_TRBS], sc[SC_RR]);
+    for (int q = 0; q < kp.P - 1; ++q) fprintf(stderr, " %.17g", sc[SC_G22 + q]);
+    fprintf(stderr, "\n");
   }
   const double n = (double)c->n_global;
   const double z = kp.tau2 + c->delta;
@@ -899,7 +907,7 @@ int sgp_fitc_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
                          c->M3, mp, c->stream));
     int nb = 0;
     HIPCHK(launch_contract_kmm(kp, c->U, c->mp, c->m, mp, c->uvec, c->K22inv, c->Binv, c->M3,
-                               -0.5, 0.5, 0.5, c->slab_small, &nb, c->stream));
+                               -0.5, 0.5, 0.5, c->slab_small, SLAB_SMALL, &nb, c->stream));
     HIPCHK(launch_colsum(c->slab_small, nb, kp.P - 1, c->sc + SC_G22, c->stream));
   }
   double sc[SC_N], r2[2 * (SGP_MAXD + 5) + 2];

@@ -259,12 +259,13 @@ hipError_t launch_build_kmm(const KernParams& kp, const double* U, int64_t ldu, 
 hipError_t launch_contract_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,
                                int64_t mp, const double* uvec, const double* Ainv,
                                const double* Binv, const double* M3, double a, double b,
-                               double c, double* slab, int* nblocks, hipStream_t s) {
+                               double c, double* slab, int64_t slab_cap, int* nblocks, hipStream_t s) {
   int64_t total = m * m;
   int nb = (int)((total + 255) / 256);
   if (nb > 1024) nb = 1024;
   if (nb < 1) nb = 1;
   *nblocks = nb;
+  if ((int64_t)nb * (kp.P - 1) > slab_cap) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_contract_kmm, dim3(nb), dim3(256), 0, s, kp, U, ldu, m, mp, uvec, Ainv,
                      Binv, M3, a, b, c, slab);
   return hipGetLastError();

@@ -76,7 +76,7 @@ hipError_t launch_build_kmm(const KernParams& kp, const double* U, int64_t ldu, 
 hipError_t launch_contract_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,
                                int64_t mp, const double* uvec, const double* Ainv,
                                const double* Binv, const double* M3, double a, double b,
-                               double c, double* slab, int* nblocks, hipStream_t s);
+                               double c, double* slab, int64_t slab_cap, int* nblocks, hipStream_t s);
 
 // ---------------------------------------------------------------- k_mfma.hip
 // S_aug partials: S = K^T diag(w) K (lower 128-tiles), t = K^T diag(w) r, rr = r^T diag(w) r.

@@ -18,7 +18,8 @@ def sgp():
 
 @pytest.mark.parametrize("cfg,n,m,coinc", [("C2", 300, 20, False), ("C3", 300, 20, False),
                                            ("C2", 1000, 130, False), ("C3", 400, 24, True),
-                                           ("C2", 129, 1, False)])
+                                           ("C2", 129, 1, False), ("C3", 700, 512, True),
+                                           ("C3", 1500, 1024, False)])
 def test_fitc_matches_oracle(sgp, cfg, n, m, coinc):
     P = O.make_gaussian_problem(cfg, n=n, m=m)
     U = P["U"].copy()
@@ -31,6 +32,20 @@ def test_fitc_matches_oracle(sgp, cfg, n, m, coinc):
     assert abs(obj - o) / abs(o) < EVAL_RTOL, (obj, o)
     for k in cp:
         assert abs(grad[k] - g[k]) / max(1.0, abs(g[k])) < EVAL_RTOL, (k, grad[k], g[k])
+
+
+def test_fitc_det_underflow_case(sgp):
+    """C2 with m=1024 > n: the oracle's log(det(Sigma22)) underflows to -inf (R's det()); the
+    product computes log-determinants from the factorisation, so it is checked against the
+    adjoint model instead (same algebra, numpy)."""
+    import adjoint_ref as A
+    P = O.make_gaussian_problem("C2", n=900, m=1024)
+    th = np.array(list(P["cov_par"].values()))
+    o, g = A.eval_fitc("sqexp", th, P["X"], P["y"], P["mu"], P["U"], P["delta"])
+    obj, grad = sgp.fitc_eval(P["cov_par"], "sqexp", P["U"], P["X"], P["y"], P["mu"], P["delta"])
+    assert abs(obj - o) / abs(o) < 1e-9
+    gv = np.array(list(grad.values()))
+    assert np.max(np.abs(gv - g) / np.maximum(1, np.abs(g))) < 1e-7
 
 
 def test_fitc_larger_against_adjoint_model(sgp):

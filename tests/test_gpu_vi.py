@@ -115,7 +115,8 @@ def _check_vi(sgp, P, **kw):
 
 
 @pytest.mark.parametrize("cfg,n,m", [("C2", 300, 20), ("C3", 300, 20), ("C2", 1000, 130),
-                                     ("C3", 777, 64), ("C2", 129, 1)])
+                                     ("C3", 777, 64), ("C2", 129, 1), ("C3", 700, 512),
+                                     ("C3", 1500, 1024)])
 def test_vi_matches_oracle(sgp, cfg, n, m):
     _check_vi(sgp, _problem(cfg, n, m))
 
