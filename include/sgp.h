@@ -24,6 +24,8 @@
  *                      (R/laplace_gradient_ascent.R:1568-1593)
  *   sgp_vi_phase1/2, sgp_vi_finish: the same VI evaluation split at its two
  *                      row-sum reductions so a caller can all-reduce across GPUs.
+ *   sgp_eval_laplace <- newtrap_sparseGP (R/newtrap_sparseGP.R:6-186) + dlogq_dcov_par
+ *                      (R/laplace_approx_gradient.R:25-553), Poisson likelihood
  *
  * Hyperparameters are passed as `theta` laid out [sigma, l_1..l_L, tau] with
  * L = 1 (sqexp, exp) or L = d (ard).  Gradients are d/d log(theta) in that order
@@ -136,6 +138,38 @@ int sgp_fitc_phase1(sgp_ctx* ctx, int kernel, const double* theta, const double*
 int sgp_fitc_phase2(sgp_ctx* ctx, const double* red1, int64_t n_global, unsigned flags,
                     double* red2);
 int sgp_fitc_finish(sgp_ctx* ctx, const double* red2, double* obj, double* grad);
+
+/* Poisson sparse Laplace (config 5): one evaluation = newtrap_sparseGP warm-started from the
+ * context's latent vector f (R/newtrap_sparseGP.R:6-186, obj_fun_pois
+ * R/laplace_approx_obj_funs.R:108-174) followed by dlogq_dcov_par at the mode
+ * (R/laplace_approx_gradient.R:25-553), exactly as one iteration of laplace_grad_ascent
+ * (R/laplace_gradient_ascent.R:510-541).  K22 = Kuu + (tau^2 + delta) I (quirk Q1).
+ * expo = the Poisson exposure `m` of the reference's likelihood helpers
+ * (R/derivative_functions_of_data_likelihoods.R:7-61); tol/maxit = tol_nr/maxit_nr.
+ * The mode f stays resident in the context and warm-starts the next evaluation; its value
+ * at context creation is 0, the reference starts at log(mean(y)) - log(expo)
+ * (R/optimize_gp.R:480): set it with sgp_lap_set_f.  obj = the last NR objective value
+ * (log q(y | theta, xu, f_hat)); nr_iters = length(objective_function_values).
+ * maxit = 0 skips the NR loop: objective and dlogq_dcov_par at the resident f as given. */
+int sgp_lap_set_f(sgp_ctx* ctx, const double* f /* n host values, or NULL */, double fill);
+int sgp_lap_get_f(sgp_ctx* ctx, double* f /* n host values */);
+/* objective_function_values of the last NR run (first min(count, max_n) copied; *count = all) */
+int sgp_lap_objective_values(sgp_ctx* ctx, double* out, int max_n, int* count);
+int sgp_eval_laplace(sgp_ctx* ctx, int kernel, const double* theta, const double* U, int64_t m,
+                     int64_t ldu, double delta, double expo, double tol, int maxit,
+                     double* obj, double* grad, int* nr_iters);
+
+/* Multi-GPU Laplace as a reduction state machine.  sgp_lap_begin writes this rank's partial
+ * sums (count doubles) to the DEVICE buffer red_out; the caller sums them over ranks in place,
+ * then calls sgp_lap_step(red_in = the summed buffer, red_out = a different buffer) until
+ * *done; each step reports the next count.  Every rank takes identical decisions (they
+ * are functions of the summed buffers only).  Buffers hold sgp_lap_red_count doubles. */
+int64_t sgp_lap_red_count(int kernel, int d, int64_t m);
+int sgp_lap_begin(sgp_ctx* ctx, int kernel, const double* theta, const double* U, int64_t m,
+                  int64_t ldu, double delta, double expo, double tol, int maxit, double* red_out,
+                  int64_t* count);
+int sgp_lap_step(sgp_ctx* ctx, const double* red_in, double* red_out, int64_t* count,
+                 int* done, double* obj, double* grad, int* nr_iters);
 
 /* Per-kernel timing of the last evaluation (HIP events on the launch stream).
  * names: '\n'-separated kernel-phase names; ms: their durations (max n entries). */

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libsgp.so")
-SOURCES = ["capi.hip", "k_cov.hip", "k_mfma.hip", "k_dense.hip"]
+SOURCES = ["capi.hip", "k_cov.hip", "k_mfma.hip", "k_dense.hip", "k_lap.hip"]
 HEADERS = ["sgp_internal.h", os.path.join("..", "..", "include", "sgp.h")]
 ARCH = os.environ.get("SGP_OFFLOAD_ARCH", "gfx950")
 

@@ -58,6 +58,18 @@ PROTOTYPES = {
                                   C.c_double, C.c_void_p]),
     "sgp_fitc_phase2": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_uint, C.c_void_p]),
     "sgp_fitc_finish": (C.c_int, [C.c_void_p, C.c_void_p, c_double_p, c_double_p]),
+    "sgp_lap_set_f": (C.c_int, [C.c_void_p, c_double_p, C.c_double]),
+    "sgp_lap_get_f": (C.c_int, [C.c_void_p, c_double_p]),
+    "sgp_lap_objective_values": (C.c_int, [C.c_void_p, c_double_p, C.c_int, c_int_p]),
+    "sgp_eval_laplace": (C.c_int, [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_int64,
+                                   C.c_int64, C.c_double, C.c_double, C.c_double, C.c_int,
+                                   c_double_p, c_double_p, c_int_p]),
+    "sgp_lap_red_count": (C.c_int64, [C.c_int, C.c_int, C.c_int64]),
+    "sgp_lap_begin": (C.c_int, [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_int64, C.c_int64,
+                                C.c_double, C.c_double, C.c_double, C.c_int, C.c_void_p,
+                                C.POINTER(C.c_int64)]),
+    "sgp_lap_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_int64), c_int_p,
+                               c_double_p, c_double_p, c_int_p]),
     "sgp_ctx_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "sgp_ctx_timings": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64, c_double_p, C.c_int, c_int_p]),
 }

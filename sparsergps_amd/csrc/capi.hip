@@ -137,6 +137,16 @@ struct sgp_ctx {
   const double* g_bm_S = nullptr;
   double g_bm_sscale = 0.0;
   bool use_graphs = false;  // opt-in (SGP_GRAPHS=1): replay faulted in one configuration
+  // Poisson-Laplace state (row/knot vectors allocated on first use)
+  double *y = nullptr, *mu = nullptr;     // per-row data (n_pad), kept for the Laplace path
+  double* lv = nullptr;                   // LV_N x n_pad row vectors
+  double* lm = nullptr;                   // LM_N x mp_max knot vectors
+  double* lslab = nullptr;                // K^T V row-chunk partials
+  int64_t lslab_cap = 0;
+  double* lred[2] = {nullptr, nullptr};   // ping-pong reduction buffers of sgp_eval_laplace
+  int lap_state = 0, lap_it = 0, lap_maxit = 0;
+  double lap_obj = 0.0, lap_obj_prev = 0.0, lap_cnt = 0.0, lap_tol = 0.0, lap_expo = 1.0;
+  std::vector<double> lap_objs;           // objective_function_values of the last NR run
   // timing
   bool timing = false;
   std::vector<Timer> timers;
@@ -147,7 +157,7 @@ struct sgp_ctx {
 namespace {
 
 constexpr int SC_LD22 = 0, SC_LDB = 1, SC_TU = 2, SC_TRKS = 3, SC_TRBS = 4, SC_RR = 5,
-              SC_G22 = 8;  // SC_G22 .. SC_G22 + P - 2
+              SC_G22 = 16;  // SC_G22 .. SC_G22 + P - 1 (contract_kmm records)
 constexpr int SC_N = 64;
 // per-block partials of the small reductions: k_contract_kmm writes up to 1024 blocks x (P-1)
 // records (P <= SGP_MAXD + 2), the dot/colsum helpers at most 1024 x 1
@@ -206,7 +216,8 @@ void ctx_free(sgp_ctx* c) {
                   c->K22inv, c->Bm,    c->Binv,   c->Pm,      c->Xt,    c->T1,   c->M3,
                   c->dinv,   c->logd22, c->logdB, c->uvec,    c->cdiag, c->status, c->red1,
                   c->red2,   c->slab_syrk, c->slab_con, c->slab_small, c->sc,
-                  c->Xt22,   c->T22,    c->dinv22, c->omega, c->pvec, c->rowq, c->red2f};
+                  c->Xt22,   c->T22,    c->dinv22, c->omega, c->pvec, c->rowq, c->red2f,
+                  c->y,      c->mu,     c->lv,     c->lm,    c->lslab, c->lred[0], c->lred[1]};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->g_bm) hipGraphExecDestroy(c->g_bm);
@@ -218,6 +229,13 @@ void ctx_free(sgp_ctx* c) {
   if (c->aux) hipStreamDestroy(c->aux);
   for (hipEvent_t e : c->pool) hipEventDestroy(e);
   if (c->own) hipStreamDestroy(c->own);
+}
+
+// n host values -> device vector of n_pad (zero padded), synchronous
+hipError_t upload_rows(double* dst, const double* src, int64_t n, int64_t n_pad) {
+  std::vector<double> h((size_t)n_pad, 0.0);
+  for (int64_t i = 0; i < n; ++i) h[(size_t)i] = src[i];
+  return hipMemcpy(dst, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice);
 }
 
 int upload_knots(sgp_ctx* c, const double* U, int64_t m, int64_t ldu) {
@@ -451,6 +469,8 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->slab_con, c->slab_con_cap);
   st = st ? st : dalloc(&c->slab_small, SLAB_SMALL);
   st = st ? st : dalloc(&c->sc, SC_N);
+  st = st ? st : dalloc(&c->y, np_);
+  st = st ? st : dalloc(&c->mu, np_);
   if (st) {
     ctx_free(c);
     delete c;
@@ -465,6 +485,8 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   hipError_t e = hipMemcpy(c->X, hx.data(), sizeof(double) * hx.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->r, hr.data(), sizeof(double) * hr.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemset(c->K, 0, sizeof(double) * np_ * mp);
+  if (e == hipSuccess) e = upload_rows(c->y, y, n, np_);
+  if (e == hipSuccess) e = upload_rows(c->mu, mu, n, np_);
   if (e != hipSuccess) {
     set_err("HIP error '%s' uploading data", hipGetErrorString(e));
     ctx_free(c);
@@ -499,6 +521,8 @@ int sgp_ctx_set_data(sgp_ctx* c, const double* y, const double* mu) {
   HIPCHK(hipMemcpyAsync(c->r, hr.data(), sizeof(double) * hr.size(), hipMemcpyHostToDevice,
                         c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(upload_rows(c->y, y, c->n, c->n_pad));
+  HIPCHK(upload_rows(c->mu, mu, c->n, c->n_pad));
   return SGP_OK;
 }
 
@@ -694,9 +718,10 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
     Scope tm(c, "contract_kmm");
     int nb = 0;
     HIPCHK(launch_contract_kmm(kp, c->U, c->mp, c->m, mp, c->uvec, c->K22inv, c->Binv, c->M3,
-                               -0.5, 0.5, -1.0 / (2.0 * kp.tau2), c->slab_small, SLAB_SMALL, &nb,
+                               -0.5, 0.5, -1.0 / (2.0 * kp.tau2), nullptr, nullptr, 0.0,
+                               c->slab_small, SLAB_SMALL, &nb,
                                c->stream));
-    HIPCHK(launch_colsum(c->slab_small, nb, kp.P - 1, c->sc + SC_G22, c->stream));
+    HIPCHK(launch_colsum(c->slab_small, nb, kp.P, c->sc + SC_G22, c->stream));
   }
   int64_t nrec = 0, nwg = 0;
   {
@@ -736,7 +761,7 @@ int sgp_vi_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
   if (getenv("SGP_DEBUG_SC")) {
     fprintf(stderr, "[sgp sc] ld22 %.17g ldB %.17g tu %.17g trKS %.17g trBS %.17g rr %.17g g22",
             sc[SC_LD22], sc[SC_LDB], sc[SC_TU], sc[SC_TRKS], sc[SC_TRBS], sc[SC_RR]);
-    for (int q = 0; q < kp.P - 1; ++q) fprintf(stderr, " %.17g", sc[SC_G22 + q]);
+    for (int q = 0; q < kp.P; ++q) fprintf(stderr, " %.17g", sc[SC_G22 + q]);
     fprintf(stderr, "\n");
   }
   const double n = (double)c->n_global;
@@ -907,8 +932,9 @@ int sgp_fitc_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
                          c->M3, mp, c->stream));
     int nb = 0;
     HIPCHK(launch_contract_kmm(kp, c->U, c->mp, c->m, mp, c->uvec, c->K22inv, c->Binv, c->M3,
-                               -0.5, 0.5, 0.5, c->slab_small, SLAB_SMALL, &nb, c->stream));
-    HIPCHK(launch_colsum(c->slab_small, nb, kp.P - 1, c->sc + SC_G22, c->stream));
+                               -0.5, 0.5, 0.5, nullptr, nullptr, 0.0, c->slab_small,
+                               SLAB_SMALL, &nb, c->stream));
+    HIPCHK(launch_colsum(c->slab_small, nb, kp.P, c->sc + SC_G22, c->stream));
   }
   double sc[SC_N], r2[2 * (SGP_MAXD + 5) + 2];
   int status[4];
@@ -950,6 +976,375 @@ int sgp_eval_fitc(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   st = sgp_fitc_phase2(c, c->red1, c->n, flags, c->red2f);
   if (st) return st;
   return sgp_fitc_finish(c, c->red2f, obj, grad);
+}
+
+
+// ------------------------------------------------------------------------- Poisson Laplace
+// State machine over the reduction points of newtrap_sparseGP + dlogq_dcov_par (adjoint form,
+// DESIGN.md sec. 3.4; numpy twin: tests/adjoint_ref.py NumpyLaplaceRank).
+//   begin   : K12, K22 = Kuu + (tau^2+delta) I, Z, S_Z;  obj partials at f0
+//   OBJ(0)  : C = (K22+S_B)^-1, x1 = (K22+S_Z)^-1 t_Z, objective; NR part a -> [K^T v, cnt]
+//             or, once the stop rule holds, gradient part a -> [K^T c2, K^T g, K^T (B sv)]
+//   NRB     : f += ...; obj partials at the new f
+//   GRADB   : h, a;  [S_a, sum a, contraction records]
+//   FIN     : G22 contraction, gradient
+enum { LS_NONE = 0, LS_OBJ0, LS_NRB, LS_OBJ, LS_GRADB, LS_FIN };
+enum { LV_F = 0, LV_Z, LV_ZI, LV_B, LV_RF, LV_TV, LV_OMZW, LV_Y1, LV_Y2, LV_DMT, LV_SV, LV_H,
+       LV_A, LV_V, LV_P, LV_C2, LV_G, LV_BSV, LV_N };   // C2, G, BSV adjacent (one K^T pass)
+enum { LM_X1 = 0, LM_X2, LM_S, LM_GG, LM_NGG, LM_CW, LM_N };
+
+static double* lvec(sgp_ctx* c, int k) { return c->lv + (int64_t)k * c->n_pad; }
+static double* lmv(sgp_ctx* c, int k) { return c->lm + (int64_t)k * c->mp_max; }
+static int64_t lap_obj_off(int64_t mp) { return mp * mp + mp + 8; }
+static int64_t lap_rec_off(int64_t mp) { return mp * mp + mp + 8; }
+
+int64_t sgp_lap_red_count(int kernel, int d, int64_t m) {
+  const int64_t mp = round_up(m, SGP_TILE);
+  return 2 * (mp * mp + mp + 8) + 2 * (num_ls(kernel, d) + 5) + 8;
+}
+
+static int lap_ensure(sgp_ctx* c) {
+  if (c->lv) return SGP_OK;
+  const int64_t np_ = c->n_pad, mp = c->mp_max;
+  int st = dalloc(&c->lv, LV_N * np_);
+  st = st ? st : dalloc(&c->lm, LM_N * mp);
+  c->lslab_cap = 4 * 128 * 4096;
+  if (c->lslab_cap < 4 * mp) c->lslab_cap = 4 * mp;
+  st = st ? st : dalloc(&c->lslab, c->lslab_cap);
+  const int64_t rc = sgp_lap_red_count(SGP_KERNEL_ARD, SGP_MAXD, c->m_max);
+  st = st ? st : dalloc(&c->lred[0], rc);
+  st = st ? st : dalloc(&c->lred[1], rc);
+  if (st) return st;
+  HIPCHK(hipMemset(c->lv, 0, sizeof(double) * LV_N * np_));
+  HIPCHK(hipMemset(c->lm, 0, sizeof(double) * LM_N * mp));
+  return SGP_OK;
+}
+
+int sgp_lap_set_f(sgp_ctx* c, const double* f, double fill) {
+  if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
+  HIPCHK(hipSetDevice(c->device));
+  int st = lap_ensure(c);
+  if (st) return st;
+  std::vector<double> h((size_t)c->n_pad, 0.0);
+  for (int64_t i = 0; i < c->n; ++i) h[(size_t)i] = f ? f[i] : fill;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(lvec(c, LV_F), h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice));
+  return SGP_OK;
+}
+
+int sgp_lap_get_f(sgp_ctx* c, double* f) {
+  if (!c || !f) { set_err("invalid arguments"); return SGP_EINVAL; }
+  HIPCHK(hipSetDevice(c->device));
+  int st = lap_ensure(c);
+  if (st) return st;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(f, lvec(c, LV_F), sizeof(double) * c->n, hipMemcpyDeviceToHost));
+  return SGP_OK;
+}
+
+// objective partials at the current f into red[o ..]: [S_B, t_Z, r'Z^-1 r, log p(y|f), log Z2]
+static int lap_obj_partials(sgp_ctx* c, double* red, int64_t o) {
+  const int64_t mp = c->mp, mm = mp * mp;
+  Scope t(c, "lap_obj");
+  int nb = 0;
+  HIPCHK(launch_lap_obj(c->n, c->n_pad, lvec(c, LV_F), c->y, c->mu, lvec(c, LV_Z),
+                        lvec(c, LV_ZI), c->lap_expo, lvec(c, LV_B), lvec(c, LV_RF),
+                        lvec(c, LV_TV), c->slab_small, &nb, c->stream));
+  HIPCHK(launch_syrk_aug(c->K, c->n_pad, mp, lvec(c, LV_RF), lvec(c, LV_B), c->slab_syrk,
+                         c->slab_syrk_cap, red + o, c->stream, 3, lvec(c, LV_TV)));
+  HIPCHK(launch_colsum(c->slab_small, nb, 2, red + o + mm + mp + 1, c->stream));
+  return SGP_OK;
+}
+
+int sgp_lap_begin(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
+                  int64_t ldu, double delta, double expo, double tol, int maxit, double* red_out,
+                  int64_t* count) {
+  KernParams kp;
+  int st = check_eval_args(c, kernel, theta, U, m, ldu, delta, &kp);
+  if (st) return st;
+  if (!red_out || !count) { set_err("red_out/count is NULL"); return SGP_EINVAL; }
+  if (!(expo > 0.0) || !(tol >= 0.0) || maxit < 0) {
+    set_err("invalid Laplace controls (expo=%g, tol=%g, maxit=%d)", expo, tol, maxit);
+    return SGP_EINVAL;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  st = lap_ensure(c);
+  if (st) return st;
+  timers_reset(c);
+  c->kp = kp;
+  c->m = m;
+  c->mp = round_up(m, SGP_TILE);
+  c->delta = delta;
+  c->phase = 0;
+  c->lap_expo = expo;
+  c->lap_tol = tol;
+  c->lap_maxit = maxit;
+  c->lap_it = 0;
+  c->lap_cnt = 0.0;
+  c->lap_objs.clear();
+  const int64_t mp = c->mp;
+  st = upload_knots(c, U, m, ldu);
+  if (st) return st;
+  HIPCHK(hipMemsetAsync(c->status, 0, sizeof(int) * 4, c->stream));
+  HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->stream));
+  st = k22_stage(c, 0.0);   // K22 = Kuu + (tau^2 + delta) I (newtrap_sparseGP.R:51-59)
+  if (st) return st;
+  {
+    Scope t(c, "build_knm");
+    HIPCHK(launch_build_knm(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp, m, mp, c->K,
+                            c->stream));
+  }
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
+  {
+    Scope t(c, "rowquad_q");
+    HIPCHK(launch_rowquad_knm(kp, c->K, c->K22inv, c->n, c->n_pad, m, mp, c->r, 0.0, nullptr,
+                              nullptr, nullptr, c->rowq, lvec(c, LV_P), c->stream));
+    HIPCHK(launch_lap_z(lvec(c, LV_P), c->n, c->n_pad, kp.sig2 + kp.tau2 + delta, lvec(c, LV_Z),
+                        lvec(c, LV_ZI), c->stream));
+  }
+  {
+    Scope t(c, "syrk_z");
+    HIPCHK(launch_syrk_aug(c->K, c->n_pad, mp, c->r, lvec(c, LV_ZI), c->slab_syrk,
+                           c->slab_syrk_cap, red_out, c->stream, 3));
+  }
+  st = lap_obj_partials(c, red_out, lap_obj_off(mp));
+  if (st) return st;
+  *count = lap_obj_off(mp) + mp * mp + mp + 3;
+  c->lap_state = LS_OBJ0;
+  return SGP_OK;
+}
+
+// consume objective sums: factor, solve, evaluate obj_fun_pois; returns the objective
+static int lap_consume_obj(sgp_ctx* c, const double* red, int64_t o, bool first, double* obj) {
+  const int64_t mp = c->mp, mm = mp * mp;
+  {
+    Scope t(c, "lap_dense");
+    if (first) {   // (K22 + S_Z)^-1 is fixed for the whole NR run (Z depends on theta only)
+      HIPCHK(dense_axpby(1.0, c->K22, 1.0, red, c->Bm, mm, c->stream));
+      HIPCHK(dense_spd_inverse(c->Bm, mp, c->Xt, c->T1, c->dinv, c->logdB, c->status + 1,
+                               c->stream));
+    }
+    HIPCHK(dense_axpby(1.0, c->K22, 1.0, red + o, c->Binv, mm, c->stream));
+    HIPCHK(dense_spd_inverse(c->Binv, mp, c->Xt, c->T1, c->dinv, c->logdB, c->status + 2,
+                             c->stream));
+    HIPCHK(launch_sum_small(c->logdB, mp / SGP_DB, c->sc + SC_LDB, c->stream));
+    HIPCHK(dense_gemv(c->Bm, mp, red + o + mm, 1.0, lmv(c, LM_X1), c->stream));
+    HIPCHK(launch_dot(red + o + mm, lmv(c, LM_X1), mp, c->slab_small, c->sc + SC_TU, c->stream));
+    HIPCHK(hipMemcpyAsync(c->sc + SC_RR, red + o + mm + mp, 3 * sizeof(double),
+                          hipMemcpyDeviceToDevice, c->stream));
+  }
+  double sc[SC_N];
+  int status[4];
+  HIPCHK(hipMemcpyAsync(sc, c->sc, sizeof(sc), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(status, c->status, sizeof(status), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (status[0] || status[1] || status[2]) {
+    c->lap_state = LS_NONE;
+    set_err("chol(): the leading minor of order %d of %s is not positive definite",
+            status[0] ? status[0] : (status[1] ? status[1] : status[2]),
+            status[0] ? "Sigma22" : (status[1] ? "Sigma22 + t(Sigma12) %*% ZSig12"
+                                               : "Sigma22 + t(Sigma12) %*% (B * Sigma12)"));
+    return SGP_ENOTPD;
+  }
+  const double ld22 = 2.0 * sc[SC_LD22], ldB = 2.0 * sc[SC_LDB];
+  const double rr = sc[SC_RR], logpy = sc[SC_RR + 1], logz2 = sc[SC_RR + 2], tu = sc[SC_TU];
+  // laplace_approx_obj_funs.R:158-172: quad + log p(y|f) + det_part_1 + det_part_2
+  *obj = (-0.5 * rr + 0.5 * tu) + logpy + (-0.5 * (-ld22 + ldB)) + (-0.5 * logz2);
+  return SGP_OK;
+}
+
+int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* count, int* done,
+                 double* obj, double* grad, int* nr_iters) {
+  if (!c || !red_in || !red_out || !count || !done || red_in == red_out) {
+    set_err("invalid arguments (red_in and red_out must be distinct device buffers)");
+    return SGP_EINVAL;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  *done = 0;
+  const KernParams& kp = c->kp;
+  const int64_t n = c->n, n_pad = c->n_pad, mp = c->mp, mm = mp * mp;
+  const int st_in = c->lap_state;
+  if (st_in == LS_OBJ0 || st_in == LS_OBJ) {
+    double o = 0.0;
+    int st = lap_consume_obj(c, red_in, st_in == LS_OBJ0 ? lap_obj_off(mp) : 0, st_in == LS_OBJ0,
+                             &o);
+    if (st) return st;
+    c->lap_obj_prev = c->lap_obj;
+    c->lap_obj = o;
+    c->lap_it += 1;
+    c->lap_objs.push_back(o);
+    const bool go = (st_in == LS_OBJ0 && c->lap_maxit > 0) ||
+                    (c->lap_it < c->lap_maxit &&
+                     (fabs(c->lap_obj - c->lap_obj_prev) > c->lap_tol || c->lap_cnt > 0.0));
+    if (go) {   // NR part a: grad_psi and K^T (grad_psi / omzw)
+      Scope t(c, "lap_nr_a");
+      HIPCHK(launch_gemv_rows(c->K, n_pad, mp, lmv(c, LM_X1), nullptr, lvec(c, LV_Y1), nullptr,
+                              c->stream));
+      int nb = 0;
+      HIPCHK(launch_lap_nr_a(n, n_pad, lvec(c, LV_F), c->y, c->mu, lvec(c, LV_Z), lvec(c, LV_ZI),
+                             c->lap_expo, lvec(c, LV_Y1), c->lap_tol, lvec(c, LV_G),
+                             lvec(c, LV_OMZW), lvec(c, LV_V), c->slab_small, &nb, c->stream));
+      HIPCHK(launch_gemv_cols(c->K, n_pad, mp, lvec(c, LV_V), n_pad, 1, c->lslab, c->lslab_cap,
+                              red_out, c->stream));
+      HIPCHK(launch_colsum(c->slab_small, nb, 1, red_out + mp, c->stream));
+      *count = mp + 1;
+      c->lap_state = LS_NRB;
+      return SGP_OK;
+    }
+    // gradient part a (dlogq_dcov_par at the final f)
+    Scope t(c, "lap_grad_a");
+    HIPCHK(launch_gemv_rows(c->K, n_pad, mp, lmv(c, LM_X1), nullptr, lvec(c, LV_Y1), nullptr,
+                            c->stream));
+    HIPCHK(launch_rowquad_knm(kp, c->K, c->Binv, n, n_pad, c->m, mp, c->r, 0.0, nullptr, nullptr,
+                              nullptr, c->rowq, lvec(c, LV_P), c->stream));
+    HIPCHK(launch_lap_grad_a(n, n_pad, lvec(c, LV_F), c->y, c->mu, lvec(c, LV_Z), lvec(c, LV_ZI),
+                             c->lap_expo, lvec(c, LV_Y1), lvec(c, LV_P), lvec(c, LV_C2),
+                             lvec(c, LV_G), lvec(c, LV_B), lvec(c, LV_DMT), lvec(c, LV_SV),
+                             lvec(c, LV_BSV), c->stream));
+    HIPCHK(launch_gemv_cols(c->K, n_pad, mp, lvec(c, LV_C2), n_pad, 3, c->lslab, c->lslab_cap,
+                            red_out, c->stream));
+    *count = 3 * mp;
+    c->lap_state = LS_GRADB;
+    return SGP_OK;
+  }
+  if (st_in == LS_NRB) {
+    {
+      Scope t(c, "lap_nr_b");
+      HIPCHK(hipMemcpyAsync(c->sc + SC_RR + 3, red_in + mp, sizeof(double),
+                            hipMemcpyDeviceToDevice, c->stream));
+      double cnt = 0.0;
+      HIPCHK(hipMemcpyAsync(&cnt, red_in + mp, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(dense_gemv(c->Binv, mp, red_in, 1.0, lmv(c, LM_X2), c->stream));
+      HIPCHK(launch_gemv_rows(c->K, n_pad, mp, lmv(c, LM_X2), nullptr, lvec(c, LV_Y2), nullptr,
+                              c->stream));
+      HIPCHK(launch_lap_nr_b(n, n_pad, lvec(c, LV_F), c->mu, lvec(c, LV_Z), lvec(c, LV_G),
+                             lvec(c, LV_OMZW), lvec(c, LV_Y1), lvec(c, LV_Y2), c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+      c->lap_cnt = cnt;
+    }
+    int st = lap_obj_partials(c, red_out, 0);
+    if (st) return st;
+    *count = mm + mp + 3;
+    c->lap_state = LS_OBJ;
+    return SGP_OK;
+  }
+  if (st_in == LS_GRADB) {
+    Scope t(c, "lap_grad_b");
+    const double* sr = red_in;
+    const double* ggr = red_in + mp;
+    const double* w = red_in + 2 * mp;
+    HIPCHK(dense_gemv(c->K22inv, mp, sr, 1.0, lmv(c, LM_S), c->stream));
+    HIPCHK(dense_gemv(c->K22inv, mp, ggr, 1.0, lmv(c, LM_GG), c->stream));
+    HIPCHK(dense_gemv(c->K22inv, mp, ggr, -1.0, lmv(c, LM_NGG), c->stream));
+    HIPCHK(dense_gemv(c->Binv, mp, w, 1.0, lmv(c, LM_CW), c->stream));
+    HIPCHK(launch_gemv_rows(c->K, n_pad, mp, lmv(c, LM_CW), nullptr, lvec(c, LV_Y2), nullptr,
+                            c->stream));
+    int nb = 0;
+    HIPCHK(launch_lap_grad_b(n, n_pad, lvec(c, LV_B), lvec(c, LV_SV), lvec(c, LV_Y2),
+                             lvec(c, LV_DMT), lvec(c, LV_C2), lvec(c, LV_G), lvec(c, LV_H),
+                             lvec(c, LV_A), c->slab_small, &nb, c->stream));
+    const int64_t off = lap_rec_off(mp);
+    HIPCHK(hipMemsetAsync(red_out, 0, sizeof(double) * (off + 2 * (kp.L + 5)), c->stream));
+    HIPCHK(launch_syrk_aug(c->K, n_pad, mp, c->r, lvec(c, LV_A), c->slab_syrk, c->slab_syrk_cap,
+                           red_out, c->stream, 3));
+    HIPCHK(launch_colsum(c->slab_small, nb, 1, red_out + mm + mp + 1, c->stream));
+    int64_t nrec = 0, nwg = 0;
+    // G1 = c2 s^T - h GG^T - diag(B) K C
+    ConArgs a1;
+    a1.alpha_in = lvec(c, LV_C2);
+    a1.uvec = lmv(c, LM_S);
+    a1.beta_in = lvec(c, LV_H);
+    a1.vvec = lmv(c, LM_NGG);
+    a1.rs_vec = lvec(c, LV_B);
+    a1.rs = -1.0;
+    HIPCHK(launch_contract_args(kp, c->K, c->Binv, c->X, n_pad, n, n_pad, c->U, c->mp, c->m, mp,
+                                a1, c->slab_con, &nrec, &nwg, c->stream));
+    HIPCHK(launch_colsum(c->slab_con, nwg, nrec, red_out + off, c->stream));
+    // G2 = -diag(2a) K K22^-1
+    ConArgs a2;
+    a2.rs_vec = lvec(c, LV_A);
+    a2.rs = -2.0;
+    HIPCHK(launch_contract_args(kp, c->K, c->K22inv, c->X, n_pad, n, n_pad, c->U, c->mp, c->m,
+                                mp, a2, c->slab_con, &nrec, &nwg, c->stream));
+    HIPCHK(launch_colsum(c->slab_con, nwg, nrec, red_out + off + nrec, c->stream));
+    *count = off + 2 * nrec;
+    c->lap_state = LS_FIN;
+    return SGP_OK;
+  }
+  if (st_in == LS_FIN) {
+    const int L = kp.L;
+    {
+      Scope t(c, "contract_kmm");
+      // G22 = (K22^-1 - C)/2 - s s^T/2 + (Cw GG^T + GG Cw^T)/4 + K22^-1 S_a K22^-1
+      HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->K22inv, mp, red_in, mp, 0.0,
+                           c->T1, mp, c->stream));
+      HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->T1, mp, c->K22inv, mp, 0.0,
+                           c->M3, mp, c->stream));
+      int nb = 0;
+      HIPCHK(launch_contract_kmm(kp, c->U, c->mp, c->m, mp, lmv(c, LM_S), c->K22inv, c->Binv,
+                                 c->M3, -0.5, 0.5, 1.0, lmv(c, LM_CW), lmv(c, LM_GG), 0.25,
+                                 c->slab_small, SLAB_SMALL, &nb, c->stream));
+      HIPCHK(launch_colsum(c->slab_small, nb, kp.P, c->sc + SC_G22, c->stream));
+    }
+    const int64_t off = lap_rec_off(mp);
+    const int nrec = L + 5;
+    double sc[SC_N], r2[2 * (SGP_MAXD + 5) + 2];
+    HIPCHK(hipMemcpyAsync(sc, c->sc, sizeof(sc), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(r2, red_in + mm + mp + 1, sizeof(double), hipMemcpyDeviceToHost,
+                          c->stream));
+    HIPCHK(hipMemcpyAsync(r2 + 1, red_in + off, sizeof(double) * 2 * nrec, hipMemcpyDeviceToHost,
+                          c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const double suma = r2[0];
+    const double* a = r2 + 1;
+    const double* b = r2 + 1 + nrec;
+    const double* g22 = sc + SC_G22;
+    if (grad) {
+      grad[0] = 2.0 * (a[0] + b[0]) + g22[0] + 2.0 * kp.sig2 * suma;
+      for (int q = 0; q < L; ++q) grad[1 + q] = a[1 + q] + b[1 + q] + g22[1 + q];
+      grad[L + 1] = 2.0 * kp.tau2 * (a[1 + L] + b[1 + L]) + 2.0 * kp.tau2 * g22[kp.P - 1] +
+                    2.0 * kp.tau2 * suma;
+    }
+    if (obj) *obj = c->lap_obj;
+    if (nr_iters) *nr_iters = c->lap_it;
+    *count = 0;
+    *done = 1;
+    c->lap_state = LS_NONE;
+    return SGP_OK;
+  }
+  set_err("sgp_lap_step called without sgp_lap_begin");
+  return SGP_EINVAL;
+}
+
+int sgp_lap_objective_values(sgp_ctx* c, double* out, int max_n, int* count) {
+  if (!c || !count) { set_err("invalid arguments"); return SGP_EINVAL; }
+  int k = 0;
+  for (double v : c->lap_objs) {
+    if (k >= max_n) break;
+    if (out) out[k] = v;
+    ++k;
+  }
+  *count = (int)c->lap_objs.size();
+  return SGP_OK;
+}
+
+int sgp_eval_laplace(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
+                     int64_t ldu, double delta, double expo, double tol, int maxit, double* obj,
+                     double* grad, int* nr_iters) {
+  if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
+  HIPCHK(hipSetDevice(c->device));
+  int st = lap_ensure(c);
+  if (st) return st;
+  int64_t count = 0;
+  st = sgp_lap_begin(c, kernel, theta, U, m, ldu, delta, expo, tol, maxit, c->lred[0], &count);
+  if (st) return st;
+  int cur = 0, done = 0;
+  while (!done) {
+    st = sgp_lap_step(c, c->lred[cur], c->lred[cur ^ 1], &count, &done, obj, grad, nr_iters);
+    if (st) return st;
+    cur ^= 1;
+  }
+  return SGP_OK;
 }
 
 }  // extern "C"

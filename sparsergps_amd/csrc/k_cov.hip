@@ -161,9 +161,11 @@ __global__ void __launch_bounds__(256) k_build_kmm(KernParams kp, const double* 
   K22[j * mp + k] = v;
 }
 
-// sum_{j,k<m} G22_jk dK22^p_jk, G22 = a u_j u_k + b (Ainv - Binv)_jk + c M3_jk.
-// Per block partial sums of P-1 entries (all parameters except tau, whose dK22 is 0 on the
-// Gaussian paths, vi_functions.R:313-316).
+// sum_{j,k<m} G22_jk dK22^p_jk with
+//   G22 = a u_j u_k + b (Ainv - Binv)_jk + c M3_jk + e (v_j w_k + w_j v_k)   (v, w optional).
+// Per block partial sums of P records: sigma, the length scales, and the tau-coincidence sum
+// sum_{u_j == u_k} G22_jk (dK22/dlog tau = 2 tau^2 there; used by the Laplace path, whose
+// K22 keeps tau^2 -- the Gaussian paths zero dK22/dtau, vi_functions.R:313-316).
 __global__ void __launch_bounds__(256) k_contract_kmm(KernParams kp, const double* __restrict__ U,
                                                       int64_t ldu, int64_t m, int64_t mp,
                                                       const double* __restrict__ uvec,
@@ -171,19 +173,27 @@ __global__ void __launch_bounds__(256) k_contract_kmm(KernParams kp, const doubl
                                                       const double* __restrict__ Binv,
                                                       const double* __restrict__ M3, double a,
                                                       double b, double c,
+                                                      const double* __restrict__ vvec,
+                                                      const double* __restrict__ wvec, double e2,
                                                       double* __restrict__ slab) {
   __shared__ double red[4][SGP_MAXD + 2];
-  const int np = kp.P - 1;
-  double acc[SGP_MAXD + 1];
+  const int np = kp.P;
+  double acc[SGP_MAXD + 2];
   for (int p = 0; p < np; ++p) acc[p] = 0.0;
   const int64_t total = m * m;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * 256) {
     const int64_t j = e / m, k = e % m;
     double uj[SGP_MAXD], uk[SGP_MAXD];
-    for (int q = 0; q < kp.d; ++q) { uj[q] = U[j + q * ldu]; uk[q] = U[k + q * ldu]; }
+    bool same = true;
+    for (int q = 0; q < kp.d; ++q) {
+      uj[q] = U[j + q * ldu];
+      uk[q] = U[k + q * ldu];
+      same = same && (uj[q] == uk[q]);
+    }
     const int64_t o = j * mp + k;
-    const double g = a * uvec[j] * uvec[k] + b * (Ainv[o] - Binv[o]) + c * M3[o];
+    double g = a * uvec[j] * uvec[k] + b * (Ainv[o] - Binv[o]) + c * M3[o];
+    if (vvec) g += e2 * (vvec[j] * wvec[k] + wvec[j] * vvec[k]);
     const double kv = kvalue(kp, uj, uk);
     const double gk = g * kv;
     acc[0] += 2.0 * gk;                                   // sigma: dK/dlog sigma = 2K
@@ -197,6 +207,7 @@ __global__ void __launch_bounds__(256) k_contract_kmm(KernParams kp, const doubl
         acc[1 + q] += gk * t * t;
       }
     }
+    if (same) acc[np - 1] += g;
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int p = 0; p < np; ++p) {
@@ -259,14 +270,15 @@ hipError_t launch_build_kmm(const KernParams& kp, const double* U, int64_t ldu, 
 hipError_t launch_contract_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,
                                int64_t mp, const double* uvec, const double* Ainv,
                                const double* Binv, const double* M3, double a, double b,
-                               double c, double* slab, int64_t slab_cap, int* nblocks, hipStream_t s) {
+                               double c, const double* vvec, const double* wvec, double e2,
+                               double* slab, int64_t slab_cap, int* nblocks, hipStream_t s) {
   int64_t total = m * m;
   int nb = (int)((total + 255) / 256);
   if (nb > 1024) nb = 1024;
   if (nb < 1) nb = 1;
   *nblocks = nb;
-  if ((int64_t)nb * (kp.P - 1) > slab_cap) return hipErrorInvalidValue;
+  if ((int64_t)nb * kp.P > slab_cap) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_contract_kmm, dim3(nb), dim3(256), 0, s, kp, U, ldu, m, mp, uvec, Ainv,
-                     Binv, M3, a, b, c, slab);
+                     Binv, M3, a, b, c, vvec, wvec, e2, slab);
   return hipGetLastError();
 }

@@ -1,0 +1,389 @@
+// Per-row kernels of the Poisson sparse-Laplace path (newtrap_sparseGP + dlogq_dcov_par in
+// adjoint form) and the two HBM-bound K12 matrix-vector passes it needs.
+//
+// Every kernel here is a single streaming pass: the n-vectors are ~8 B/row each, the GEMVs
+// read K12 (n_pad x mp, row-major) once.  Per-block partial sums go to a slab reduced by
+// launch_colsum (deterministic, no atomics), so all ranks / reruns see identical bits.
+//
+// Row semantics follow the reference (R/derivative_functions_of_data_likelihoods.R:7-61,
+// R/newtrap_sparseGP.R:234-325, R/laplace_approx_obj_funs.R:108-174,
+// R/laplace_approx_gradient.R:133-336) with a = exposure (`m` in the reference's Poisson
+// helpers): W = d2 = d3 = -a e^f, d1 = y - a e^f.
+#include "sgp_internal.h"
+
+namespace {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// block-wide sums of NV values into slab[blockIdx.x * NV + k]
+template <int NV>
+__device__ __forceinline__ void block_store_sums(const double (&v)[NV], double* slab) {
+  __shared__ double sh[4][NV];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const double s = wave_sum(v[k]);
+    if (lane == 0) sh[w][k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < NV)
+    slab[(int64_t)blockIdx.x * NV + threadIdx.x] =
+        sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
+}
+
+#define ROW_LOOP(i) \
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * 256)
+
+// Z_i = c0 - q_i (newtrap_sparseGP.R:63-66), zinv = 1/Z; padded rows Z = 1, zinv = 0.
+__global__ void __launch_bounds__(256) k_lap_z(const double* __restrict__ q, int64_t n,
+                                               int64_t n_pad, double c0, double* __restrict__ Z,
+                                               double* __restrict__ zinv) {
+  ROW_LOOP(i) {
+    const bool v = i < n;
+    const double z = v ? c0 - q[i] : 1.0;
+    Z[i] = z;
+    zinv[i] = v ? 1.0 / z : 0.0;
+  }
+}
+
+// Objective row terms at f (laplace_approx_obj_funs.R:108-174): SYRK weights
+// B = 1/(Z - 1/W) (the R2/R3 weight: -W/Z2 = B), rf = f - mu, tv = rf/Z,
+// slab = [sum log p(y_i|f_i), sum log Z2_i],  Z2 = 1 + sqrt(-W) Z sqrt(-W).
+__global__ void __launch_bounds__(256) k_lap_obj(int64_t n, int64_t n_pad,
+                                                 const double* __restrict__ f,
+                                                 const double* __restrict__ y,
+                                                 const double* __restrict__ mu,
+                                                 const double* __restrict__ Z,
+                                                 const double* __restrict__ zinv, double expo,
+                                                 double logexpo, double* __restrict__ B,
+                                                 double* __restrict__ rf, double* __restrict__ tv,
+                                                 double* __restrict__ slab) {
+  double acc[2] = {0.0, 0.0};
+  ROW_LOOP(i) {
+    if (i < n) {
+      const double fi = f[i], yi = y[i], zi = Z[i];
+      const double e = exp(fi);
+      const double W = -expo * e;
+      B[i] = 1.0 / (zi - 1.0 / W);
+      const double r = fi - mu[i];
+      rf[i] = r;
+      tv[i] = zinv[i] * r;
+      acc[0] += yi * logexpo - lgamma(yi + 1.0) - expo * e + yi * fi;
+      const double sw = sqrt(-W);
+      acc[1] += log(1.0 + sw * zi * sw);
+    } else {
+      B[i] = 0.0;
+      rf[i] = 0.0;
+      tv[i] = 0.0;
+    }
+  }
+  block_store_sums<2>(acc, slab);
+}
+
+// NR step, part a (grad_loglik_fn_pois + the first half of newtrap_sparseGP_update):
+//   g = y - a e^f, omzw = 1 - Z W, gpsi = g - (rf - y1)/Z   (y1 = K Bm_Z^-1 t_Z),
+//   v = gpsi / omzw (input of the K^T pass), slab = [#{|gpsi_i| > tol}].
+__global__ void __launch_bounds__(256) k_lap_nr_a(int64_t n, int64_t n_pad,
+                                                  const double* __restrict__ f,
+                                                  const double* __restrict__ y,
+                                                  const double* __restrict__ mu,
+                                                  const double* __restrict__ Z,
+                                                  const double* __restrict__ zinv, double expo,
+                                                  const double* __restrict__ y1, double tol,
+                                                  double* __restrict__ g, double* __restrict__ omzw,
+                                                  double* __restrict__ v,
+                                                  double* __restrict__ slab) {
+  double acc[1] = {0.0};
+  ROW_LOOP(i) {
+    if (i < n) {
+      const double e = exp(f[i]);
+      const double W = -expo * e;
+      const double gi = -expo * e + y[i];
+      const double zi = Z[i], iz = zinv[i];
+      const double om = 1.0 - zi * W;
+      const double gp = gi + (-iz * (f[i] - mu[i]) + iz * y1[i]);
+      g[i] = gi;
+      omzw[i] = om;
+      v[i] = (1.0 / om) * gp;
+      if (fabs(gp) > tol) acc[0] += 1.0;
+    } else {
+      g[i] = 0.0;
+      omzw[i] = 1.0;
+      v[i] = 0.0;
+    }
+  }
+  block_store_sums<1>(acc, slab);
+}
+
+// NR step, part b: f += (Z/omzw) g - rf/omzw + y1/omzw + y2/omzw  (y2 = K C K^T v)
+// (newtrap_sparseGP.R:252-289: A11 - A12 + A13 + A2).
+__global__ void __launch_bounds__(256) k_lap_nr_b(int64_t n, int64_t n_pad,
+                                                  double* __restrict__ f,
+                                                  const double* __restrict__ mu,
+                                                  const double* __restrict__ Z,
+                                                  const double* __restrict__ g,
+                                                  const double* __restrict__ omzw,
+                                                  const double* __restrict__ y1,
+                                                  const double* __restrict__ y2) {
+  ROW_LOOP(i) {
+    if (i < n) {
+      const double om = omzw[i], fi = f[i];
+      const double a11 = (Z[i] / om) * g[i];
+      const double a12 = (1.0 / om) * (fi - mu[i]);
+      const double a13 = y1[i] / om;
+      const double a2 = y2[i] / om;
+      f[i] = fi + (a11 - a12 + a13 + a2);
+    }
+  }
+}
+
+// Gradient rows, part a (laplace_approx_gradient.R:133-178): with p_i = k_i^T C k_i,
+//   c2 = rf/Z - y1/Z, B = 1/(Z - 1/W), dMt = B - B^2 p  (diag of Sigma~^-1),
+//   comp4 = -1/D + (1/(Z D))^2 p  (D = W - 1/Z),  sv = comp4 (-W3)(-1/W),  bsv = B sv.
+__global__ void __launch_bounds__(256) k_lap_grad_a(int64_t n, int64_t n_pad,
+                                                    const double* __restrict__ f,
+                                                    const double* __restrict__ y,
+                                                    const double* __restrict__ mu,
+                                                    const double* __restrict__ Z,
+                                                    const double* __restrict__ zinv, double expo,
+                                                    const double* __restrict__ y1,
+                                                    const double* __restrict__ p,
+                                                    double* __restrict__ c2,
+                                                    double* __restrict__ g,
+                                                    double* __restrict__ B,
+                                                    double* __restrict__ dMt,
+                                                    double* __restrict__ sv,
+                                                    double* __restrict__ bsv) {
+  ROW_LOOP(i) {
+    if (i < n) {
+      const double e = exp(f[i]);
+      const double W = -expo * e, W3 = W;
+      const double zi = Z[i], iz = zinv[i];
+      const double bi = 1.0 / (zi - 1.0 / W);
+      const double pi = p[i];
+      c2[i] = iz * (f[i] - mu[i]) - iz * y1[i];
+      g[i] = -expo * e + y[i];
+      B[i] = bi;
+      dMt[i] = bi - bi * bi * pi;
+      const double D = W - 1.0 / zi;
+      const double coef = iz * (1.0 / D);
+      const double comp4 = -(1.0 / D) + coef * coef * pi;
+      const double s = comp4 * (-W3) * (-1.0 / W);
+      sv[i] = s;
+      bsv[i] = bi * s;
+    } else {
+      c2[i] = 0.0;
+      g[i] = 0.0;
+      B[i] = 0.0;
+      dMt[i] = 0.0;
+      sv[i] = 0.0;
+      bsv[i] = 0.0;
+    }
+  }
+}
+
+// Gradient rows, part b: h = B sv - B (K C w)  (= Sigma~^-1 sv),
+//   a = -dMt/2 + c2^2/2 - h g/2 (the coefficient of A = d diag Sigma~), slab = [sum a].
+__global__ void __launch_bounds__(256) k_lap_grad_b(int64_t n, int64_t n_pad,
+                                                    const double* __restrict__ B,
+                                                    const double* __restrict__ sv,
+                                                    const double* __restrict__ y3,
+                                                    const double* __restrict__ dMt,
+                                                    const double* __restrict__ c2,
+                                                    const double* __restrict__ g,
+                                                    double* __restrict__ h,
+                                                    double* __restrict__ a,
+                                                    double* __restrict__ slab) {
+  double acc[1] = {0.0};
+  ROW_LOOP(i) {
+    if (i < n) {
+      const double bi = B[i];
+      const double hi = bi * sv[i] - bi * y3[i];
+      const double ci = c2[i];
+      const double ai = -0.5 * dMt[i] + 0.5 * ci * ci - 0.5 * hi * g[i];
+      h[i] = hi;
+      a[i] = ai;
+      acc[0] += ai;
+    } else {
+      h[i] = 0.0;
+      a[i] = 0.0;
+    }
+  }
+  block_store_sums<1>(acc, slab);
+}
+
+#undef ROW_LOOP
+
+// y1 = K x1 (and y2 = K x2 when x2 != nullptr): one wave per row, double2 loads.
+__global__ void __launch_bounds__(256) k_gemv_rows(const double* __restrict__ K, int64_t n_pad,
+                                                   int64_t mp, const double* __restrict__ x1,
+                                                   const double* __restrict__ x2,
+                                                   double* __restrict__ y1,
+                                                   double* __restrict__ y2) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t h = mp / 2;
+  const double2* X1 = reinterpret_cast<const double2*>(x1);
+  const double2* X2 = reinterpret_cast<const double2*>(x2);
+  for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n_pad; i += nw) {
+    const double2* row = reinterpret_cast<const double2*>(K + i * mp);
+    double s1 = 0.0, s2 = 0.0;
+    for (int64_t c = lane; c < h; c += 64) {
+      const double2 k = row[c];
+      const double2 a = X1[c];
+      s1 = fma(k.x, a.x, s1);
+      s1 = fma(k.y, a.y, s1);
+      if (x2) {
+        const double2 b = X2[c];
+        s2 = fma(k.x, b.x, s2);
+        s2 = fma(k.y, b.y, s2);
+      }
+    }
+    s1 = wave_sum(s1);
+    if (x2) s2 = wave_sum(s2);
+    if (lane == 0) {
+      y1[i] = s1;
+      if (x2) y2[i] = s2;
+    }
+  }
+}
+
+// part[ch][v][j] = sum_{i in chunk ch} K_ij V_v[i]  for v < NV (V_v = V + v * ldv)
+template <int NV>
+__global__ void __launch_bounds__(128) k_gemv_cols(const double* __restrict__ K, int64_t n_pad,
+                                                   int64_t mp, const double* __restrict__ V,
+                                                   int64_t ldv, int64_t chunk,
+                                                   double* __restrict__ part) {
+  const int64_t j = (int64_t)blockIdx.x * 128 + threadIdx.x;
+  const int64_t ch = blockIdx.y;
+  const int64_t i0 = ch * chunk;
+  const int64_t i1 = (i0 + chunk < n_pad) ? i0 + chunk : n_pad;
+  double acc[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+  int64_t i = i0;
+  for (; i + 4 <= i1; i += 4) {
+    double k[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) k[u] = K[(i + u) * mp + j];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) acc[v] = fma(k[u], V[v * ldv + i + u], acc[v]);
+  }
+  for (; i < i1; ++i) {
+    const double k = K[i * mp + j];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] = fma(k, V[v * ldv + i], acc[v]);
+  }
+  double* o = part + (ch * NV) * mp + j;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) o[v * mp] = acc[v];
+}
+
+constexpr int LAP_NB = 1024;   // blocks of the per-row kernels (slab rows)
+
+int row_blocks(int64_t n_pad) {
+  int64_t nb = (n_pad + 255) / 256;
+  return (int)(nb > LAP_NB ? LAP_NB : (nb < 1 ? 1 : nb));
+}
+
+}  // namespace
+
+int64_t lap_gemv_cols_chunks(int64_t n_pad, int64_t mp) {
+  int64_t target = 4096 / (mp / 128);
+  if (target < 1) target = 1;
+  int64_t maxch = (n_pad + 15) / 16;
+  return target < maxch ? target : maxch;
+}
+
+int64_t lap_gemv_cols_slab(int64_t n_pad, int64_t mp, int nv) {
+  return lap_gemv_cols_chunks(n_pad, mp) * nv * mp;
+}
+
+hipError_t launch_gemv_rows(const double* K, int64_t n_pad, int64_t mp, const double* x1,
+                            const double* x2, double* y1, double* y2, hipStream_t s) {
+  int64_t nb = (n_pad + 3) / 4;
+  if (nb > 4096) nb = 4096;
+  hipLaunchKernelGGL(k_gemv_rows, dim3((unsigned)nb), dim3(256), 0, s, K, n_pad, mp, x1, x2, y1,
+                     y2);
+  return hipGetLastError();
+}
+
+hipError_t launch_gemv_cols(const double* K, int64_t n_pad, int64_t mp, const double* V,
+                            int64_t ldv, int nv, double* part, int64_t part_cap, double* out,
+                            hipStream_t s) {
+  const int64_t nch = lap_gemv_cols_chunks(n_pad, mp);
+  if (nch * nv * mp > part_cap || nv < 1 || nv > 4) return hipErrorInvalidValue;
+  const int64_t chunk = (n_pad + nch - 1) / nch;
+  dim3 grid((unsigned)(mp / 128), (unsigned)nch);
+  switch (nv) {
+    case 1: hipLaunchKernelGGL(k_gemv_cols<1>, grid, dim3(128), 0, s, K, n_pad, mp, V, ldv, chunk, part); break;
+    case 2: hipLaunchKernelGGL(k_gemv_cols<2>, grid, dim3(128), 0, s, K, n_pad, mp, V, ldv, chunk, part); break;
+    case 3: hipLaunchKernelGGL(k_gemv_cols<3>, grid, dim3(128), 0, s, K, n_pad, mp, V, ldv, chunk, part); break;
+    default: hipLaunchKernelGGL(k_gemv_cols<4>, grid, dim3(128), 0, s, K, n_pad, mp, V, ldv, chunk, part); break;
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_colsum(part, nch, nv * mp, out, s);
+}
+
+hipError_t launch_lap_z(const double* q, int64_t n, int64_t n_pad, double c0, double* Z,
+                        double* zinv, hipStream_t s) {
+  hipLaunchKernelGGL(k_lap_z, dim3(row_blocks(n_pad)), dim3(256), 0, s, q, n, n_pad, c0, Z, zinv);
+  return hipGetLastError();
+}
+
+hipError_t launch_lap_obj(int64_t n, int64_t n_pad, const double* f, const double* y,
+                          const double* mu, const double* Z, const double* zinv, double expo,
+                          double* B, double* rf, double* tv, double* slab, int* nblocks,
+                          hipStream_t s) {
+  const int nb = row_blocks(n_pad);
+  *nblocks = nb;
+  hipLaunchKernelGGL(k_lap_obj, dim3(nb), dim3(256), 0, s, n, n_pad, f, y, mu, Z, zinv, expo,
+                     log(expo), B, rf, tv, slab);
+  return hipGetLastError();
+}
+
+hipError_t launch_lap_nr_a(int64_t n, int64_t n_pad, const double* f, const double* y,
+                           const double* mu, const double* Z, const double* zinv, double expo,
+                           const double* y1, double tol, double* g, double* omzw, double* v,
+                           double* slab, int* nblocks, hipStream_t s) {
+  const int nb = row_blocks(n_pad);
+  *nblocks = nb;
+  hipLaunchKernelGGL(k_lap_nr_a, dim3(nb), dim3(256), 0, s, n, n_pad, f, y, mu, Z, zinv, expo, y1,
+                     tol, g, omzw, v, slab);
+  return hipGetLastError();
+}
+
+hipError_t launch_lap_nr_b(int64_t n, int64_t n_pad, double* f, const double* mu, const double* Z,
+                           const double* g, const double* omzw, const double* y1,
+                           const double* y2, hipStream_t s) {
+  hipLaunchKernelGGL(k_lap_nr_b, dim3(row_blocks(n_pad)), dim3(256), 0, s, n, n_pad, f, mu, Z, g,
+                     omzw, y1, y2);
+  return hipGetLastError();
+}
+
+hipError_t launch_lap_grad_a(int64_t n, int64_t n_pad, const double* f, const double* y,
+                             const double* mu, const double* Z, const double* zinv, double expo,
+                             const double* y1, const double* p, double* c2, double* g, double* B,
+                             double* dMt, double* sv, double* bsv, hipStream_t s) {
+  hipLaunchKernelGGL(k_lap_grad_a, dim3(row_blocks(n_pad)), dim3(256), 0, s, n, n_pad, f, y, mu,
+                     Z, zinv, expo, y1, p, c2, g, B, dMt, sv, bsv);
+  return hipGetLastError();
+}
+
+hipError_t launch_lap_grad_b(int64_t n, int64_t n_pad, const double* B, const double* sv,
+                             const double* y3, const double* dMt, const double* c2,
+                             const double* g, double* h, double* a, double* slab, int* nblocks,
+                             hipStream_t s) {
+  const int nb = row_blocks(n_pad);
+  *nblocks = nb;
+  hipLaunchKernelGGL(k_lap_grad_b, dim3(nb), dim3(256), 0, s, n, n_pad, B, sv, y3, dMt, c2, g, h,
+                     a, slab);
+  return hipGetLastError();
+}

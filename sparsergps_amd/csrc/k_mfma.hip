@@ -50,7 +50,7 @@ __device__ __forceinline__ void store8(double* s, const double2 (&v)[4]) {
 // grid = splits * T (T = lower 128-tiles); block 256 = 4 waves as 2x2 of 64x64.
 __global__ void __launch_bounds__(256, 2)
 k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __restrict__ r,
-       const double* __restrict__ w, int64_t chunk, int T, int nb,
+       const double* __restrict__ w, const double* __restrict__ tv, int64_t chunk, int T, int nb,
        double* __restrict__ slab_s, double* __restrict__ slab_t, double* __restrict__ slab_rr) {
   __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
   __shared__ __attribute__((aligned(16))) double Kb[2][BK * SB];
@@ -99,7 +99,7 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
     if (tid < BK) {                                                             \
       const int64_t rr_ = rbeg + (int64_t)(step) * BK + tid;                    \
       const double rv_ = r[rr_];                                                \
-      vr = (w != nullptr) ? w[rr_] * rv_ : rv_;                                 \
+      vr = (tv != nullptr) ? tv[rr_] : ((w != nullptr) ? w[rr_] * rv_ : rv_);   \
     }                                                                           \
   }
 #define SYRK_SSTORE(buf)                                                        \
@@ -220,15 +220,15 @@ k_syrk_reduce_t(const double* __restrict__ slab_t, const double* __restrict__ sl
 // staged K values (iz_i = invz_vec ? invz_vec[i] : invz), optionally written to alpha_out.
 enum { EPI_GRAD = 0, EPI_ROWQUAD = 1 };
 
-template <int DT, int EPI>
+template <int DT, int EPI, bool V2 = false>
 __global__ void __launch_bounds__(256, 2)
 k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict__ M,
            const double* __restrict__ X, int64_t ldx, int64_t n, int64_t n_pad,
-           const double* __restrict__ U, int64_t ldu, int64_t m, int64_t mp,
-           const double* __restrict__ r, double invz, const double* __restrict__ invz_vec,
-           const double* __restrict__ uvec, const double* __restrict__ rs_vec, double rs,
-           const double* __restrict__ cdiag, double* __restrict__ slab, int nrec,
-           int count_a2, double* __restrict__ alpha_out, double* __restrict__ rowq) {
+           const double* __restrict__ U, int64_t ldu, int64_t m, int64_t mp, ConArgs ca,
+           double* __restrict__ slab, int nrec, double* __restrict__ rowq) {
+  const double* __restrict__ r = ca.r;
+  const double* __restrict__ uvec = ca.uvec;
+  const double* __restrict__ cdiag = ca.cdiag;
   constexpr int A_SZ = T128 * SA;   // 2304
   constexpr int B_SZ = BK * SB;     // 2304
   __shared__ __attribute__((aligned(16))) double lds[2 * (A_SZ + B_SZ)];
@@ -242,7 +242,8 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wr = wv >> 1, wc = wv & 1;
-  const bool with_u = (uvec != nullptr);
+  const bool with_u = (uvec != nullptr) && (ca.alpha_in == nullptr);   // fuse K u into the loop
+  constexpr bool with_v = V2;   // second rank-1 term (Laplace), compiled in only where used
 
   d4 acc[4][4];
 #pragma unroll
@@ -326,19 +327,23 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   double* s_rs = s_alpha + T128;            // 128
   double* s_u = s_rs + T128;                // 128
   double* s_cd = s_u + T128;                // 128
-  double* s_xs = s_cd + T128;               // 128 x d   ([row][c], scaled)
+  double* s_beta = s_cd + T128;             // 128
+  double* s_v = s_beta + T128;              // 128
+  double* s_xs = s_v + T128;                // 128 x d   ([row][c], scaled)
   double* s_us = s_xs + T128 * kp.d;        // 128 x d   ([col][c], scaled)
   ku += __shfl_xor(ku, 1, 64);                       // the two halves of row `arow`
   double a2 = 0.0;                                    // alpha^2, counted once (tj == 0)
   if ((tid & 1) == 0) {
     const int64_t i = i0 + arow;
-    const double iz = invz_vec ? invz_vec[i] : invz;
-    const double al = with_u ? (r[i] - ku) * iz : 0.0;   // padded rows: r = 0, K = 0 -> 0
+    const double iz = ca.invz_vec ? ca.invz_vec[i] : ca.invz;
+    const double al = ca.alpha_in ? ca.alpha_in[i]
+                                  : (with_u ? (r[i] - ku) * iz : 0.0);   // padded rows -> 0
     s_alpha[arow] = al;
-    s_rs[arow] = rs_vec ? rs * rs_vec[i] : rs;
+    s_rs[arow] = ca.rs_vec ? ca.rs * ca.rs_vec[i] : ca.rs;
+    s_beta[arow] = with_v ? ca.beta_in[i] : 0.0;
     if (tj == 0) {
-      if (count_a2 && i < n) a2 = al * al;
-      if (alpha_out) alpha_out[i] = al;
+      if (ca.count_a2 && i < n) a2 = al * al;
+      if (ca.alpha_out) ca.alpha_out[i] = al;
     }
   }
   const double* Kt = K + i0 * mp + j0;
@@ -374,7 +379,8 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     const double rl2s = kp.rl2[0];
     for (int e = tid; e < T128; e += 256) {
       const int64_t j = j0 + e;
-      s_u[e] = (with_u && j < m) ? uvec[j] : 0.0;
+      s_u[e] = (uvec && j < m) ? uvec[j] : 0.0;
+      s_v[e] = (with_v && j < m) ? ca.vvec[j] : 0.0;
       s_cd[e] = (cdiag && j < m) ? cdiag[j] : 0.0;
     }
     for (int e = tid; e < T128 * d; e += 256) {
@@ -400,13 +406,16 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
 #pragma unroll
       for (int c = 0; c < DT; ++c) uj[c] = (c < d) ? s_us[col * d + c] : 0.0;
       const double ucol = s_u[col];
+      const double vcol = with_v ? s_v[col] : 0.0;
 #pragma unroll
       for (int fm = 0; fm < 4; ++fm) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
           const bool valid = cvalid && ((i0 + row) < n);
-          const double G = fma(s_alpha[row], ucol, s_rs[row] * acc[fm][fn][q]);
+          double G = s_rs[row] * acc[fm][fn][q];
+          if constexpr (V2) G = fma(s_beta[row], vcol, G);
+          G = fma(s_alpha[row], ucol, G);
           const double gk = valid ? G * Kt[(int64_t)row * mp + col] : 0.0;
           e_sig += gk;
           const double* xr = &s_xs[row * d];
@@ -577,7 +586,7 @@ int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp) {
 
 hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const double* r,
                            const double* w, double* slab, int64_t slab_cap, double* red,
-                           hipStream_t s, int part) {
+                           hipStream_t s, int part, const double* tv) {
   SyrkPlan p = syrk_plan(n_pad, mp);
   double* slab_s = slab;
   double* slab_t = slab_s + (int64_t)p.splits * p.T * T128 * T128;
@@ -585,12 +594,35 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
   if (slab_rr + p.splits > slab + slab_cap) return hipErrorInvalidValue;
   if (part & 1)
     hipLaunchKernelGGL(k_syrk, dim3((unsigned)(p.splits * p.T)), dim3(256), 0, s, K, n_pad, mp,
-                       r, w, p.chunk, p.T, p.nb, slab_s, slab_t, slab_rr);
+                       r, w, tv, p.chunk, p.T, p.nb, slab_s, slab_t, slab_rr);
   if (part & 2) {
     hipLaunchKernelGGL(k_syrk_reduce, dim3(T128 * T128 / 256, p.T), dim3(256), 0, s, slab_s,
                        p.splits, p.T, mp, red);
     hipLaunchKernelGGL(k_syrk_reduce_t, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s,
                        slab_t, slab_rr, p.splits, p.nb, mp, red);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_contract_args(const KernParams& kp, const double* K, const double* M,
+                                const double* X, int64_t ldx, int64_t n, int64_t n_pad,
+                                const double* U, int64_t ldu, int64_t m, int64_t mp,
+                                const ConArgs& ca, double* slab, int64_t* nrec_out,
+                                int64_t* nwg_out, hipStream_t s) {
+  const int64_t nwg = (n_pad / T128) * (mp / T128);
+  const int nrec = kp.L + 5;
+  *nrec_out = nrec;
+  *nwg_out = nwg;
+  if (ca.beta_in != nullptr) {
+    if (kp.d > 8) return hipErrorInvalidValue;   // two-term epilogue is instantiated for d <= 8
+    hipLaunchKernelGGL((k_contract<8, EPI_GRAD, true>), dim3((unsigned)nwg), dim3(256), 0, s, kp,
+                       K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
+  } else if (kp.d <= 8) {
+    hipLaunchKernelGGL((k_contract<8, EPI_GRAD>), dim3((unsigned)nwg), dim3(256), 0, s, kp, K, M,
+                       X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
+  } else {
+    hipLaunchKernelGGL((k_contract<SGP_MAXD, EPI_GRAD>), dim3((unsigned)nwg), dim3(256), 0, s, kp,
+                       K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
   }
   return hipGetLastError();
 }
@@ -602,20 +634,17 @@ hipError_t launch_contract_knm(const KernParams& kp, const double* K, const doub
                                const double* uvec, const double* rs_vec, double rs,
                                const double* coinc_diag, int count_a2, double* slab,
                                int64_t* nrec_out, int64_t* nwg_out, hipStream_t s) {
-  const int64_t nwg = (n_pad / T128) * (mp / T128);
-  const int nrec = kp.L + 5;
-  *nrec_out = nrec;
-  *nwg_out = nwg;
-  if (kp.d <= 8) {
-    hipLaunchKernelGGL((k_contract<8, EPI_GRAD>), dim3((unsigned)nwg), dim3(256), 0, s, kp, K, M,
-                       X, ldx, n, n_pad, U, ldu, m, mp, r, invz, invz_vec, uvec, rs_vec, rs,
-                       coinc_diag, slab, nrec, count_a2, (double*)nullptr, (double*)nullptr);
-  } else {
-    hipLaunchKernelGGL((k_contract<SGP_MAXD, EPI_GRAD>), dim3((unsigned)nwg), dim3(256), 0, s, kp,
-                       K, M, X, ldx, n, n_pad, U, ldu, m, mp, r, invz, invz_vec, uvec, rs_vec,
-                       rs, coinc_diag, slab, nrec, count_a2, (double*)nullptr, (double*)nullptr);
-  }
-  return hipGetLastError();
+  ConArgs ca;
+  ca.r = r;
+  ca.invz = invz;
+  ca.invz_vec = invz_vec;
+  ca.uvec = uvec;
+  ca.rs_vec = rs_vec;
+  ca.rs = rs;
+  ca.cdiag = coinc_diag;
+  ca.count_a2 = count_a2;
+  return launch_contract_args(kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec_out,
+                              nwg_out, s);
 }
 
 hipError_t launch_rowquad_knm(const KernParams& kp, const double* K, const double* M, int64_t n,
@@ -624,10 +653,15 @@ hipError_t launch_rowquad_knm(const KernParams& kp, const double* K, const doubl
                               double* alpha_out, double* rowq_slab, double* out,
                               hipStream_t s) {
   const int64_t nwg = (n_pad / T128) * (mp / T128);
+  ConArgs ca;
+  ca.r = r;
+  ca.invz = invz;
+  ca.invz_vec = invz_vec;
+  ca.uvec = uvec;
+  ca.alpha_out = alpha_out;
   hipLaunchKernelGGL((k_contract<8, EPI_ROWQUAD>), dim3((unsigned)nwg), dim3(256), 0, s, kp, K, M,
                      (const double*)nullptr, (int64_t)0, n, n_pad, (const double*)nullptr,
-                     (int64_t)0, m, mp, r, invz, invz_vec, uvec, (const double*)nullptr, 1.0,
-                     (const double*)nullptr, (double*)nullptr, 0, 0, alpha_out, rowq_slab);
+                     (int64_t)0, m, mp, ca, (double*)nullptr, 0, rowq_slab);
   hipLaunchKernelGGL(k_rowq_reduce, dim3((unsigned)((n_pad + 255) / 256)), dim3(256), 0, s,
                      rowq_slab, mp / T128, n_pad, out);
   return hipGetLastError();

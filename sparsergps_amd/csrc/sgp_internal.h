@@ -73,18 +73,22 @@ hipError_t launch_build_kmm(const KernParams& kp, const double* U, int64_t ldu, 
                             int64_t mp, double diag_sub, double* K22, hipStream_t s);
 // sum_{j,k<m} G22_jk * dK22^p_jk for every parameter p != tau, where
 // G22 = a*u u^T + b*(Ainv - Binv) + c*M3.  Writes P partial sums per block into slab.
+// records per block: P (sigma, length scales, tau-coincidence sum of G22)
 hipError_t launch_contract_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,
                                int64_t mp, const double* uvec, const double* Ainv,
                                const double* Binv, const double* M3, double a, double b,
-                               double c, double* slab, int64_t slab_cap, int* nblocks, hipStream_t s);
+                               double c, const double* vvec, const double* wvec, double e2,
+                               double* slab, int64_t slab_cap, int* nblocks, hipStream_t s);
 
 // ---------------------------------------------------------------- k_mfma.hip
 // S_aug partials: S = K^T diag(w) K (lower 128-tiles), t = K^T diag(w) r, rr = r^T diag(w) r.
 // w == nullptr means w = 1.  Writes per-(split,tile) slabs, then reduces into
 // red = [S (mp x mp, full symmetric), t (mp), rr, n_local].
+// With tv set, t = K^T tv and rr = tv^T r instead (w still weights S).
 hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const double* r,
                            const double* w, double* slab, int64_t slab_cap, double* red,
-                           hipStream_t s, int part = 3);  // part: 1 = main kernel, 2 = reduce
+                           hipStream_t s, int part = 3,  // part: 1 = main kernel, 2 = reduce
+                           const double* tv = nullptr);
 int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp);
 // Gradient contraction on T = K M (K: n_pad x mp, M: mp x mp):
 //   G_ij = alpha_i u_j + rs_i T_ij,  alpha_i = (r_i - K_i u) * iz_i computed in the same pass
@@ -92,6 +96,29 @@ int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp);
 //   rs_i = rs_vec ? rs * rs_vec[i] : rs).  Per 128x128 tile record (L + 5 doubles):
 //   [sum G*K, sum G*K*w_c (c < L), tau-coincidence sum G, count, sum diag_j, alpha^T alpha
 //   (only if count_a2)].  coinc_diag may be nullptr.
+// Epilogue operands of the K12 contraction (k_mfma.hip k_contract):
+//   G_ij = alpha_i u_j + beta_i v_j + rs_i T_ij,  T = K M,  rs_i = rs * (rs_vec ? rs_vec[i] : 1)
+//   alpha_i = alpha_in[i] when alpha_in is set, else (r_i - K_i u) * iz_i fused into the k-loop
+//   when u is set (iz_i = invz_vec ? invz_vec[i] : invz), else 0.
+struct ConArgs {
+  const double* r = nullptr;
+  double invz = 0.0;
+  const double* invz_vec = nullptr;
+  const double* uvec = nullptr;
+  const double* alpha_in = nullptr;
+  const double* beta_in = nullptr;
+  const double* vvec = nullptr;
+  const double* rs_vec = nullptr;
+  double rs = 1.0;
+  const double* cdiag = nullptr;
+  int count_a2 = 0;
+  double* alpha_out = nullptr;
+};
+hipError_t launch_contract_args(const KernParams& kp, const double* K, const double* M,
+                                const double* X, int64_t ldx, int64_t n, int64_t n_pad,
+                                const double* U, int64_t ldu, int64_t m, int64_t mp,
+                                const ConArgs& ca, double* slab, int64_t* nrec_out,
+                                int64_t* nwg_out, hipStream_t s);
 hipError_t launch_contract_knm(const KernParams& kp, const double* K, const double* M,
                                const double* X, int64_t ldx, int64_t n, int64_t n_pad,
                                const double* U, int64_t ldu, int64_t m, int64_t mp,
@@ -157,4 +184,38 @@ hipError_t launch_fitc_z(const double* q, int64_t n, int64_t n_pad, double c0, d
 // omega_i = alpha_i^2 - (w_i - w_i^2 p_i) for i < n (0 otherwise); per-block sums -> slab.
 hipError_t launch_fitc_omega(const double* alpha, const double* w, const double* p, int64_t n,
                              int64_t n_pad, double* omega, double* slab, int* nblocks,
+                             hipStream_t s);
+
+// ---------------------------------------------------------------- k_lap.hip
+// K12 matrix-vector passes (HBM-bound, one read of K each).
+// y1 = K x1 (and y2 = K x2 if x2 != nullptr), n_pad rows.
+hipError_t launch_gemv_rows(const double* K, int64_t n_pad, int64_t mp, const double* x1,
+                            const double* x2, double* y1, double* y2, hipStream_t s);
+// out[v*mp + j] = sum_i K_ij V[v*ldv + i] for v < nv (<= 4); part = slab of
+// lap_gemv_cols_slab(n_pad, mp, nv) doubles (row-chunk partials, deterministic reduce).
+hipError_t launch_gemv_cols(const double* K, int64_t n_pad, int64_t mp, const double* V,
+                            int64_t ldv, int nv, double* part, int64_t part_cap, double* out,
+                            hipStream_t s);
+int64_t lap_gemv_cols_slab(int64_t n_pad, int64_t mp, int nv);
+// Poisson-Laplace per-row steps (see k_lap.hip for the formulas and reference lines).
+hipError_t launch_lap_z(const double* q, int64_t n, int64_t n_pad, double c0, double* Z,
+                        double* zinv, hipStream_t s);
+hipError_t launch_lap_obj(int64_t n, int64_t n_pad, const double* f, const double* y,
+                          const double* mu, const double* Z, const double* zinv, double expo,
+                          double* B, double* rf, double* tv, double* slab, int* nblocks,
+                          hipStream_t s);
+hipError_t launch_lap_nr_a(int64_t n, int64_t n_pad, const double* f, const double* y,
+                           const double* mu, const double* Z, const double* zinv, double expo,
+                           const double* y1, double tol, double* g, double* omzw, double* v,
+                           double* slab, int* nblocks, hipStream_t s);
+hipError_t launch_lap_nr_b(int64_t n, int64_t n_pad, double* f, const double* mu, const double* Z,
+                           const double* g, const double* omzw, const double* y1,
+                           const double* y2, hipStream_t s);
+hipError_t launch_lap_grad_a(int64_t n, int64_t n_pad, const double* f, const double* y,
+                             const double* mu, const double* Z, const double* zinv, double expo,
+                             const double* y1, const double* p, double* c2, double* g, double* B,
+                             double* dMt, double* sv, double* bsv, hipStream_t s);
+hipError_t launch_lap_grad_b(int64_t n, int64_t n_pad, const double* B, const double* sv,
+                             const double* y3, const double* dMt, const double* c2,
+                             const double* g, double* h, double* a, double* slab, int* nblocks,
                              hipStream_t s);

@@ -30,7 +30,7 @@ def shard_rows(n, world, rank):
 class HipRowBackend:
     """libsgp.so context over this rank's rows; reduction buffers are torch device tensors.
     mode "vi" (sgp_vi_*) or "fitc" (sgp_fitc_*): both are phase1 -> sum -> phase2 -> sum ->
-    finish."""
+    finish; mode "laplace" (sgp_lap_*): begin -> sum -> step -> sum -> ... -> done."""
 
     def __init__(self, X_local, y_local, mu_local, m_max, device_index, cov_fun, mode="vi"):
         import torch
@@ -47,6 +47,8 @@ class HipRowBackend:
             n1, n2 = self.ctx.vi_red1_count(m_max), self.ctx.vi_red2_count(cov_fun)
         elif mode == "fitc":
             n1, n2 = self.ctx.fitc_red1_count(m_max), self.ctx.fitc_red2_count(cov_fun, m_max)
+        elif mode == "laplace":
+            n1 = n2 = self.ctx.lap_red_count(cov_fun, m_max)
         else:
             raise ValueError(mode)
         self.red1 = torch.zeros(n1, dtype=torch.float64, device=self.dev)
@@ -84,6 +86,22 @@ class HipRowBackend:
             return self.ctx.vi_finish(red2.data_ptr(), self.nparams)
         return self.ctx.fitc_finish(red2.data_ptr(), self.nparams)
 
+    # ---- Laplace state machine (ping-pong between red1 and red2)
+    def lap_begin(self, theta, U, delta, expo, tol, maxit):
+        cnt = self.ctx.lap_begin(theta, self.cov_fun, U, delta, expo, tol, maxit,
+                                 self.red1.data_ptr())
+        self._cur = 0
+        return self.red1[:cnt]
+
+    def lap_step(self, red):
+        bufs = (self.red1, self.red2)
+        src, dst = bufs[self._cur], bufs[self._cur ^ 1]
+        cnt, done, obj, grad, it = self.ctx.lap_step(src.data_ptr(), dst.data_ptr(), self.nparams)
+        self._cur ^= 1
+        if done:
+            return None, True, (obj, grad, it)
+        return dst[:cnt], False, None
+
     def close(self):
         self.ctx.close()
 
@@ -109,3 +127,32 @@ class RowShardedVI:
             if self.world > 1:
                 self.dist.all_reduce(red2, group=self.group)
             return b.finish(red2)
+
+
+class RowShardedLaplace:
+    """Poisson sparse-Laplace evaluation (NR to the mode + gradient) over row blocks.
+
+    The NR loop is the reference's (R/newtrap_sparseGP.R:76-131); each iteration has two
+    exchange steps -- K^T (grad_psi / (1 - Z W)) with the stop-rule count (m + 1 doubles) and
+    the objective partials S_B, t_Z, scalars (m^2 + m + 3) -- and the gradient two more.  Every
+    decision is a function of summed buffers, so all ranks iterate identically.
+    """
+
+    def __init__(self, backend, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.backend = backend
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+
+    def eval(self, theta, U, delta=1e-6, expo=1.0, tol=1e-5, maxit=1000):
+        """-> (objective, gradient d/dlog theta, NR iteration count)"""
+        b = self.backend
+        with (b.stream_context() if hasattr(b, "stream_context") else contextlib.nullcontext()):
+            red = b.lap_begin(theta, U, delta, expo, tol, maxit)
+            while True:
+                if self.world > 1:
+                    self.dist.all_reduce(red, group=self.group)
+                red, done, res = b.lap_step(red)
+                if done:
+                    return res

@@ -1,0 +1,85 @@
+"""Poisson sparse-Laplace evaluation on the MI355X (config 5 of SURVEY.md sec. 8).
+
+Host-side mirror of the reference's Laplace hot path (luisdamiano/sparseRGPs):
+  newtrap_sparseGP        R/newtrap_sparseGP.R:6-186 (+ _update 234-325)
+  obj_fun_pois            R/laplace_approx_obj_funs.R:108-174
+  dlogq_dcov_par          R/laplace_approx_gradient.R:25-553   (knots fixed)
+  d{1,2,3}log_py_dff_pois R/derivative_functions_of_data_likelihoods.R:7-61
+with K22 = k(xu, xu) + (tau^2 + delta) I (quirk Q1) and Z the FITC diagonal.  One call of
+``laplace_eval`` is one iteration body of laplace_grad_ascent
+(R/laplace_gradient_ascent.R:510-541): NR warm-started from the previous mode, then the
+gradient at the new mode.  All work runs in libsgp.so (no CPU fallback); the mode f stays
+resident on the device between calls.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import numpy as np
+
+from .covariance import theta_vector
+from .vi import _context_for, param_names
+
+
+def _prep(cov_par, cov_fun, xu, xy):
+    xy_m = np.asarray(xy, dtype=np.float64)
+    d = 1 if xy_m.ndim == 1 else xy_m.shape[1]
+    lnames = [f"l{c + 1}" for c in range(d)] if cov_fun == "ard" else None
+    theta = theta_vector(cov_par, cov_fun, d, lnames)
+    names = param_names(cov_fun, d, lnames)
+    xu_m = np.asarray(xu, dtype=np.float64).reshape(-1, d)
+    return theta, names, xu_m
+
+
+def _mu_vec(mu, y):
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    if mu is None:
+        mu = np.log(np.mean(y))          # poisson-regression-vignette.Rmd:92
+    return np.ascontiguousarray(np.broadcast_to(np.asarray(mu, dtype=np.float64), y.shape))
+
+
+def laplace_eval(cov_par, cov_fun, xu, xy, y, mu, ff=None, m=1.0, delta=1e-6, tol=1e-5,
+                 maxit=1000, ctx=None):
+    """NR to the Laplace mode from `ff` (or the context's resident mode when ff is None), then
+    dlogq_dcov_par there.  Returns dict(objective, gradient (names(cov_par) order), gp,
+    objective_function_values, nr_iter)."""
+    theta, names, xu_m = _prep(cov_par, cov_fun, xu, xy)
+    muv = _mu_vec(mu, y)
+    if ctx is None:
+        ctx = _context_for(xy, y, mu, xu_m.shape[0])
+        ctx.set_data(y, muv)
+    if ff is not None:
+        ctx.lap_set_f(ff)
+    obj, g, it = ctx.eval_laplace(theta, cov_fun, xu_m, delta, m, tol, maxit)
+    byname = dict(zip(names, g))
+    return {"objective": obj,
+            "gradient": OrderedDict((k, float(byname[k])) for k in cov_par.keys()),
+            "gp": ctx.lap_get_f(),
+            "objective_function_values": ctx.lap_objective_values(),
+            "nr_iter": it}
+
+
+def newtrap_sparseGP(start_vals, cov_par, cov_fun, xy, xu, y, mu, m=1.0, delta=1e-6,
+                     maxit=1000, tol=1e-6, ctx=None):
+    """R/newtrap_sparseGP.R:6-186 for the Poisson likelihood: {"gp",
+    "objective_function_values"} (the fused evaluation also forms the gradient at the mode)."""
+    r = laplace_eval(cov_par, cov_fun, xu, xy, y, mu, start_vals, m, delta, tol, maxit, ctx)
+    return {"gp": r["gp"], "objective_function_values": r["objective_function_values"]}
+
+
+def dlogq_dcov_par(cov_par, cov_fun, dcov_fun_dtheta=True, dcov_fun_dknot=None, knot_opt=None,
+                   xu=None, xy=None, y=None, ff=None, mu=None, m=1.0, delta=1e-6,
+                   transform=True, ctx=None):
+    """R/laplace_approx_gradient.R:25-553 at the given ff (no NR step): {"gradient",
+    "trans_par"}."""
+    if dcov_fun_dknot is not None and dcov_fun_dknot is not False:
+        raise NotImplementedError("knot gradients (xu_opt='simultaneous') are not in this build")
+    r = laplace_eval(cov_par, cov_fun, xu, xy, y, mu, ff, m, delta, 0.0, 0, ctx)
+    grad = r["gradient"] if dcov_fun_dtheta else 0
+    trans_par = OrderedDict((k, float(np.log(v))) for k, v in cov_par.items())
+    return {"gradient": grad, "trans_par": trans_par}
+
+
+def obj_fun_pois(ff, cov_par, cov_fun, xu, xy, y, mu, m=1.0, delta=1e-6, ctx=None):
+    """R/laplace_approx_obj_funs.R:108-174 at ff (log q(y | theta, xu, ff))."""
+    return laplace_eval(cov_par, cov_fun, xu, xy, y, mu, ff, m, delta, 0.0, 0, ctx)["objective"]

@@ -76,10 +76,10 @@ class SparseGPContext:
 
     def timings(self):
         """[(phase name, ms)] of the last evaluation (HIP events on the launch stream)."""
-        names = C.create_string_buffer(4096)
-        ms = (C.c_double * 64)()
+        names = C.create_string_buffer(65536)
+        ms = (C.c_double * 2048)()
         cnt = C.c_int(0)
-        _lib.check(self._lib.sgp_ctx_timings(self.handle, names, 4096, ms, 64, C.byref(cnt)))
+        _lib.check(self._lib.sgp_ctx_timings(self.handle, names, 65536, ms, 2048, C.byref(cnt)))
         nm = names.value.decode().split("\n")
         return [(nm[i], ms[i]) for i in range(cnt.value)]
 
@@ -130,6 +130,67 @@ class SparseGPContext:
                                      _lib.dptr(grad))
         _lib.check(st)
         return obj.value, grad
+
+    # ------------------------------------------------------------------ Poisson Laplace
+    def lap_set_f(self, f=None, fill=0.0):
+        """Set the resident latent vector f (NR warm start); f=None fills with `fill`."""
+        if f is None:
+            _lib.check(self._lib.sgp_lap_set_f(self.handle, None, float(fill)))
+        else:
+            f = np.ascontiguousarray(np.broadcast_to(np.asarray(f, dtype=np.float64), (self.n,)))
+            _lib.check(self._lib.sgp_lap_set_f(self.handle, _lib.dptr(f), 0.0))
+
+    def lap_get_f(self):
+        f = np.zeros(self.n, dtype=np.float64)
+        _lib.check(self._lib.sgp_lap_get_f(self.handle, _lib.dptr(f)))
+        return f
+
+    def lap_objective_values(self):
+        cnt = C.c_int(0)
+        _lib.check(self._lib.sgp_lap_objective_values(self.handle, None, 0, C.byref(cnt)))
+        out = np.zeros(max(cnt.value, 1), dtype=np.float64)
+        _lib.check(self._lib.sgp_lap_objective_values(self.handle, _lib.dptr(out), cnt.value,
+                                                      C.byref(cnt)))
+        return out[:cnt.value]
+
+    def eval_laplace(self, theta, cov_fun, xu, delta=1e-6, expo=1.0, tol=1e-5, maxit=1000):
+        """newtrap_sparseGP from the resident f, then dlogq_dcov_par at the mode:
+        (log q(y | theta, xu, f_hat), d/d log(theta), NR iteration count)."""
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        U, m = self._knots(xu)
+        obj = C.c_double(0.0)
+        it = C.c_int(0)
+        grad = np.zeros(theta.size, dtype=np.float64)
+        _lib.check(self._lib.sgp_eval_laplace(self.handle, _lib.KERNELS[cov_fun], _lib.dptr(theta),
+                                              _lib.dptr(U), m, m, float(delta), float(expo),
+                                              float(tol), int(maxit), C.byref(obj),
+                                              _lib.dptr(grad), C.byref(it)))
+        return obj.value, grad, it.value
+
+    def lap_red_count(self, cov_fun, m):
+        return int(self._lib.sgp_lap_red_count(_lib.KERNELS[cov_fun], self.d, int(m)))
+
+    def lap_begin(self, theta, cov_fun, xu, delta, expo, tol, maxit, red_ptr):
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        U, m = self._knots(xu)
+        cnt = C.c_int64(0)
+        _lib.check(self._lib.sgp_lap_begin(self.handle, _lib.KERNELS[cov_fun], _lib.dptr(theta),
+                                           _lib.dptr(U), m, m, float(delta), float(expo),
+                                           float(tol), int(maxit), C.c_void_p(red_ptr),
+                                           C.byref(cnt)))
+        return cnt.value
+
+    def lap_step(self, red_in_ptr, red_out_ptr, nparams):
+        """-> (count, done, obj, grad, nr_iters)"""
+        cnt = C.c_int64(0)
+        done = C.c_int(0)
+        obj = C.c_double(0.0)
+        it = C.c_int(0)
+        grad = np.zeros(nparams, dtype=np.float64)
+        _lib.check(self._lib.sgp_lap_step(self.handle, C.c_void_p(red_in_ptr),
+                                          C.c_void_p(red_out_ptr), C.byref(cnt), C.byref(done),
+                                          C.byref(obj), _lib.dptr(grad), C.byref(it)))
+        return cnt.value, bool(done.value), obj.value, grad, it.value
 
     # multi-GPU phases (device buffers passed as integer pointers, e.g. tensor.data_ptr())
     def vi_red1_count(self, m):

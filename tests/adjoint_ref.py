@@ -242,3 +242,191 @@ class NumpyFITCRank:
                 grad[1 + c] = rec[1 + c] + np.sum(G22 * self.Kuu * (self.dU[:, :, c] / self.ls[c]) ** 2)
         grad[L + 1] = 2 * tau2 * rec[1 + L] + tau2 * sum_om
         return obj, grad
+
+
+# ------------------------------------------------------------------------------ Laplace model
+def _lgamma1(y):
+    from scipy.special import gammaln
+    return gammaln(np.asarray(y, dtype=np.float64) + 1.0)
+
+
+class NumpyLaplaceRank:
+    """Poisson sparse-Laplace evaluation (newtrap_sparseGP + dlogq_dcov_par) in adjoint form,
+    as the same reduction state machine as sgp_lap_begin / sgp_lap_step (capi.hip).
+
+    Per-rank partials are summed between steps; everything m x m is replicated.
+    Algebra: with Z = s^2+t^2+d-q, W = -a e^f, B = W/(ZW-1),
+    S_w = K^T diag(w) K, Bm_Z = K22 + S_{1/Z}, C = (K22 + S_B)^-1:
+      obj   = -r'(r/Z)/2 + t_Z' Bm_Z^-1 t_Z/2 + log p(y|f) - (logdet Bm_B - logdet K22)/2
+              - sum log(1 - W Z)/2
+      NR    f += [Z g - r + K (Bm_Z^-1 t_Z) + K C K^T (gpsi/omzw)] / omzw
+      grad  <G, dK12> + <G22, dK22> + A1 sum(a) with
+            G = c2 s^T - h GG^T - diag(B) K C - diag(2a) K K22^-1,
+            G22 = (K22^-1 - C)/2 - s s^T/2 + sym(Cw GG^T)/2 + K22^-1 S_a K22^-1.
+    """
+
+    def __init__(self, X, y, mu):
+        self.X = np.asarray(X, dtype=np.float64)
+        self.y = np.asarray(y, dtype=np.float64)
+        self.mu = np.asarray(mu, dtype=np.float64)
+        self.f = None
+
+    def set_f(self, f):
+        self.f = np.array(f, dtype=np.float64)
+
+    # -- local row-block partials
+    def _obj_partials(self):
+        f, Z = self.f, self.Z
+        a = self.expo
+        W = -a * np.exp(f)
+        B = W / (Z * W - 1.0)
+        r = f - self.mu
+        K = self.K
+        logpy = np.sum(self.y * math.log(a) - _lgamma1(self.y) - a * np.exp(f) + self.y * f)
+        return [(K.T @ (B[:, None] * K)).reshape(-1), K.T @ (r / Z),
+                np.array([r @ (r / Z), logpy, np.sum(np.log(1.0 - W * Z))])]
+
+    def begin(self, kernel, theta, U, delta, expo, tol=1e-5, maxit=1000):
+        d = self.X.shape[1]
+        self.kernel, self.U, self.delta, self.expo = kernel, np.asarray(U), delta, expo
+        self.tol, self.maxit = tol, maxit
+        L, sigma, tau, ls = _params(kernel, theta, d)
+        self.L, self.sigma, self.tau, self.ls = L, sigma, tau, ls
+        m = self.U.shape[0]
+        self.K, self.diff = _kmat(kernel, self.X, self.U, sigma, ls)
+        Kuu, self.dU = _kmat(kernel, self.U, self.U, sigma, ls)
+        self.Kuu = Kuu
+        K22 = Kuu.copy()
+        K22[np.diag_indices(m)] = np.diag(Kuu) + tau ** 2 + delta          # quirk Q1
+        self.K22, self.K22inv = K22, np.linalg.inv(K22)
+        q = np.sum(self.K * (self.K @ self.K22inv), axis=1)
+        self.Z = sigma ** 2 + tau ** 2 + delta - q
+        self.SZ_local = (self.K.T @ ((1 / self.Z)[:, None] * self.K)).reshape(-1)
+        self.objs = []
+        self.state = "obj0"
+        return np.concatenate([self.SZ_local] + self._obj_partials())
+
+    def _consume_obj(self, red):
+        m = self.U.shape[0]
+        mm = m * m
+        off = 0
+        if self.state == "obj0":
+            SZ = red[:mm].reshape(m, m)
+            self.BmZinv = np.linalg.inv(self.K22 + SZ)
+            self.ld22 = np.linalg.slogdet(self.K22)[1]
+            off = mm
+        SB = red[off:off + mm].reshape(m, m)
+        tZ = red[off + mm:off + mm + m]
+        rr, logpy, logz2 = red[off + mm + m:off + mm + m + 3]
+        BmB = self.K22 + SB
+        self.C = np.linalg.inv(BmB)
+        self.x1 = self.BmZinv @ tZ
+        obj = -0.5 * rr + 0.5 * tZ @ self.x1 + logpy - 0.5 * (-self.ld22 + np.linalg.slogdet(BmB)[1]) \
+            - 0.5 * logz2
+        self.objs.append(obj)
+
+    def _nr_a(self):
+        f, Z = self.f, self.Z
+        W = -self.expo * np.exp(f)
+        self.omzw = 1.0 - Z * W
+        self.g = self.y - self.expo * np.exp(f)
+        self.r = f - self.mu
+        self.y1 = self.K @ self.x1
+        c2 = (self.r - self.y1) / Z
+        self.gpsi = self.g - c2
+        return np.concatenate([self.K.T @ (self.gpsi / self.omzw),
+                               [float(np.sum(np.abs(self.gpsi) > self.tol))]])
+
+    def _grad_a(self):
+        f, Z, K = self.f, self.Z, self.K
+        W = -self.expo * np.exp(f)
+        W3 = W
+        B = W / (Z * W - 1.0)
+        self.B = B
+        self.g = self.y - self.expo * np.exp(f)
+        r = f - self.mu
+        self.c2 = (r - K @ self.x1) / Z
+        p = np.sum(K * (K @ self.C), axis=1)
+        self.dMt = B - B * B * p
+        D = W - 1.0 / Z
+        coef = 1.0 / (Z * D)
+        comp4 = -1.0 / D + coef * coef * p
+        self.sv = comp4 * W3 / W
+        return np.concatenate([K.T @ self.c2, K.T @ self.g, K.T @ (B * self.sv)])
+
+    def _grad_b(self, red):
+        m = self.U.shape[0]
+        K, B = self.K, self.B
+        self.s = self.K22inv @ red[:m]
+        self.GG = self.K22inv @ red[m:2 * m]
+        self.Cw = self.C @ red[2 * m:3 * m]
+        h = B * self.sv - B * (K @ self.Cw)
+        a = -0.5 * self.dMt + 0.5 * self.c2 ** 2 - 0.5 * h * self.g
+        G = np.outer(self.c2, self.s) - np.outer(h, self.GG) - B[:, None] * (K @ self.C) \
+            - (2 * a)[:, None] * (K @ self.K22inv)
+        GK = G * K
+        rec = [np.sum(GK)]
+        if self.kernel == "sqexp":
+            rec.append(np.sum(GK * np.sum(self.diff ** 2, axis=2)) / self.ls[0] ** 2)
+        else:
+            rec += [np.sum(GK * (self.diff[:, :, c] / self.ls[c]) ** 2) for c in range(self.L)]
+        rec.append(np.sum(G[np.all(self.diff == 0.0, axis=2)]))
+        return np.concatenate([(K.T @ (a[:, None] * K)).reshape(-1), [np.sum(a)], rec])
+
+    def _finish(self, red):
+        m, L = self.U.shape[0], self.L
+        mm = m * m
+        Sa, suma, rec = red[:mm].reshape(m, m), red[mm], red[mm + 1:]
+        K22inv = self.K22inv
+        X = np.outer(self.Cw, self.GG)
+        G22 = 0.5 * (K22inv - self.C) - 0.5 * np.outer(self.s, self.s) + 0.25 * (X + X.T) + \
+            K22inv @ Sa @ K22inv
+        tau2, sig2 = self.tau ** 2, self.sigma ** 2
+        grad = np.zeros(L + 2)
+        grad[0] = 2 * rec[0] + np.sum(G22 * 2 * self.Kuu) + 2 * sig2 * suma
+        if self.kernel == "sqexp":
+            grad[1] = rec[1] + np.sum(G22 * self.Kuu * np.sum(self.dU ** 2, axis=2)) / self.ls[0] ** 2
+        else:
+            for c in range(L):
+                grad[1 + c] = rec[1 + c] + np.sum(G22 * self.Kuu * (self.dU[:, :, c] / self.ls[c]) ** 2)
+        coinc22 = np.all(self.dU == 0.0, axis=2)
+        grad[L + 1] = 2 * tau2 * rec[1 + L] + 2 * tau2 * np.sum(G22[coinc22]) + 2 * tau2 * suma
+        return self.objs[-1], grad
+
+    def step(self, red):
+        """Consume the summed partials of the previous step; return (next partials or None,
+        done, result)."""
+        if self.state in ("obj0", "obj"):
+            first = self.state == "obj0"
+            self._consume_obj(red)
+            it = len(self.objs)
+            if first or (it < self.maxit and (abs(self.objs[-1] - self.objs[-2]) > self.tol
+                                              or self.cnt > 0)):
+                self.state = "nr_b"
+                return self._nr_a(), False, None
+            self.state = "grad_b"
+            return self._grad_a(), False, None
+        if self.state == "nr_b":
+            m = self.U.shape[0]
+            v2, self.cnt = red[:m], red[m]
+            x2 = self.C @ v2
+            self.f = self.f + (self.Z * self.g - self.r + self.y1 + self.K @ x2) / self.omzw
+            self.state = "obj"
+            return np.concatenate(self._obj_partials()), False, None
+        if self.state == "grad_b":
+            self.state = "finish"
+            return self._grad_b(red), False, None
+        if self.state == "finish":
+            self.state = "done"
+            return None, True, self._finish(red)
+        raise RuntimeError(self.state)
+
+
+def eval_laplace(kernel, theta, X, y, mu, U, f0, expo=1.0, delta=1e-6, tol=1e-5, maxit=1000):
+    rk = NumpyLaplaceRank(X, y, mu)
+    rk.set_f(f0)
+    red = rk.begin(kernel, theta, U, delta, expo, tol, maxit)
+    while True:
+        red, done, res = rk.step(red)
+        if done:
+            return res[0], res[1], rk.f, len(rk.objs)

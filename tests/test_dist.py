@@ -14,7 +14,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from sparsergps_amd.dist import RowShardedVI, shard_rows
+from sparsergps_amd.dist import RowShardedLaplace, RowShardedVI, shard_rows
 
 
 def _free_port():
@@ -97,3 +97,63 @@ def test_shard_rows_partition():
             sizes = [b - a for a, b in blocks]
             assert max(sizes) - min(sizes) <= 1
     assert shard_rows(1_000_000, 8, 3) == (375_000, 500_000)    # C4: 8 blocks of 125 000
+
+
+class NumpyLaplaceBackend:
+    def __init__(self, X, y, mu, f0, cov_fun):
+        import adjoint_ref
+        self.rk = adjoint_ref.NumpyLaplaceRank(X, y, mu)
+        self.rk.set_f(f0)
+        self.cov_fun = cov_fun
+
+    def lap_begin(self, theta, U, delta, expo, tol, maxit):
+        return torch.from_numpy(self.rk.begin(self.cov_fun, theta, U, delta, expo, tol, maxit))
+
+    def lap_step(self, red):
+        nxt, done, res = self.rk.step(red.numpy())
+        if done:
+            return None, True, (res[0], res[1], len(self.rk.objs))
+        return torch.from_numpy(nxt), False, None
+
+
+def _lap_worker(rank, world, port, n, m, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import sgp_oracle as O
+        P = O.make_poisson_problem(n=n, m=m)
+        U = P["U"].copy()
+        U[:2] = P["X"][[1, n - 2]]                      # coincident knots on both shards
+        s0, s1 = shard_rows(n, world, rank)
+        be = NumpyLaplaceBackend(P["X"][s0:s1], P["y"][s0:s1], P["mu"][s0:s1], P["f0"][s0:s1],
+                                 "sqexp")
+        theta = np.array(list(P["cov_par"].values()))
+        obj, grad, it = RowShardedLaplace(be).eval(theta, U, P["delta"], P["a"], 1e-5, 1000)
+        if rank == 0:
+            nr = O.newtrap_sparseGP(P["f0"], P["cov_par"], "sqexp", P["X"], U, P["y"], P["mu"],
+                                    P["a"], P["delta"], tol=1e-5)
+            g = O.dlogq_dcov_par(P["cov_par"], "sqexp", U, P["X"], P["y"], nr["gp"], P["mu"],
+                                 P["a"], P["delta"])["gradient"]
+            gv = np.array(list(g.values()))
+            o = nr["objective_function_values"][-1]
+            q.put((abs(obj - o) / abs(o), float(np.max(np.abs(grad - gv) / np.maximum(1, np.abs(gv)))),
+                   it, len(nr["objective_function_values"])))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_row_sharded_laplace_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lap_worker, args=(r, world, port, 301, 19, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    rel_obj, rel_grad, it, it_ref = q.get(timeout=5)
+    assert it == it_ref
+    assert rel_obj < 1e-12 and rel_grad < 1e-10

@@ -59,3 +59,48 @@ def test_two_ranks_one_gpu_gloo(mode):
         assert p.exitcode == 0
     rel_obj, rel_grad = q.get(timeout=5)
     assert rel_obj < 1e-9 and rel_grad < 1e-7
+
+
+def _lap_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import sgp_oracle as O
+        from sparsergps_amd.dist import HipRowBackend, RowShardedLaplace, shard_rows
+        n, m = 2501, 150
+        P = O.make_poisson_problem(n=n, m=m)
+        U = P["U"].copy()
+        U[:2] = P["X"][[5, n - 3]]
+        s0, s1 = shard_rows(n, world, rank)
+        be = HipRowBackend(P["X"][s0:s1], P["y"][s0:s1], P["mu"][s0:s1], m, 0, "sqexp", "laplace")
+        be.ctx.lap_set_f(P["f0"][s0:s1])
+        theta = np.array(list(P["cov_par"].values()))
+        obj, grad, it = RowShardedLaplace(be).eval(theta, U, P["delta"], P["a"], 1e-5, 1000)
+        be.close()
+        if rank == 0:
+            nr = O.newtrap_sparseGP(P["f0"], P["cov_par"], "sqexp", P["X"], U, P["y"], P["mu"],
+                                    P["a"], P["delta"], tol=1e-5)
+            g = np.array(list(O.dlogq_dcov_par(P["cov_par"], "sqexp", U, P["X"], P["y"], nr["gp"],
+                                               P["mu"], P["a"], P["delta"])["gradient"].values()))
+            o = nr["objective_function_values"][-1]
+            q.put((abs(obj - o) / abs(o), float(np.max(np.abs(grad - g) / np.maximum(1, np.abs(g)))),
+                   it, len(nr["objective_function_values"])))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_laplace_two_ranks_one_gpu_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lap_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    rel_obj, rel_grad, it, it_ref = q.get(timeout=5)
+    assert it == it_ref
+    assert rel_obj < 1e-9 and rel_grad < 1e-7

@@ -212,3 +212,28 @@ def test_golden_fills():
     cp = {"sigma": 1.3, "l": 1.7, "tau": 0.4}
     assert np.allclose(O.make_cov_matC(z["x"], z["xp"], cp, "sqexp", 1e-6), z["cov_sqexp_cross"], rtol=1e-14)
     assert np.allclose(O.dsig_dthetaC(z["x"], None, cp, "exp", "l"), z["d_exp_l_sym"], rtol=1e-14)
+
+
+@pytest.mark.parametrize("cov_fun,coinc", [("sqexp", False), ("ard", True)])
+def test_laplace_adjoint_model_matches_oracle(cov_fun, coinc):
+    """The adjoint-form Laplace algebra the GPU implements (tests/adjoint_ref.py) reproduces the
+    literal newtrap_sparseGP + dlogq_dcov_par, including the reference's comp3 form."""
+    import adjoint_ref as A
+    P = O.make_poisson_problem(n=260, m=18)
+    U = P["U"].copy()
+    if coinc:
+        U[:2] = P["X"][[4, 9]]
+    cp = P["cov_par"]
+    if cov_fun == "ard":
+        cp = OrderedDict([("sigma", 1.1)] + [(f"l{c + 1}", 1.5 + 0.3 * c) for c in range(5)]
+                         + [("tau", 0.2)])
+    th = np.array(list(cp.values()))
+    nr = O.newtrap_sparseGP(P["f0"], cp, cov_fun, P["X"], U, P["y"], P["mu"], P["a"], P["delta"],
+                            tol=1e-5)
+    g = np.array(list(O.dlogq_dcov_par(cp, cov_fun, U, P["X"], P["y"], nr["gp"], P["mu"], P["a"],
+                                       P["delta"])["gradient"].values()))
+    o, grad, f, it = A.eval_laplace(cov_fun, th, P["X"], P["y"], P["mu"], U, P["f0"], P["a"],
+                                    P["delta"], tol=1e-5)
+    assert it == len(nr["objective_function_values"])
+    assert abs(o - nr["objective_function_values"][-1]) < 1e-10 * abs(o)
+    assert np.max(np.abs(grad - g) / np.maximum(1, np.abs(g))) < 1e-10
