@@ -31,7 +31,9 @@ HBM_PEAK_GBS = 8000.0
 
 def make_problem(config, n=None, m=None):
     """Synthetic inputs of SURVEY.md 8(d) (numpy PCG64 streams); no reference files read."""
-    from oracle.sgp_oracle import make_gaussian_problem  # generator only (data, not the checker)
+    from oracle.sgp_oracle import make_gaussian_problem, make_poisson_problem  # generators only
+    if config == "C5":
+        return make_poisson_problem(n=n, m=m)
     return make_gaussian_problem(config, n=n, m=m)
 
 
@@ -71,11 +73,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="C3", choices=["C2", "C3"])
+    ap.add_argument("--mode", default="vi", choices=["vi", "fitc", "laplace"],
+                    help="vi = the headline metric; fitc / laplace = secondary modes (SURVEY 8(d))")
+    ap.add_argument("--config", default=None, choices=["C2", "C3", "C5"])
+    ap.add_argument("--tol-nr", type=float, default=1e-5)
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--m", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    if args.config is None:
+        args.config = "C5" if args.mode == "laplace" else "C3"
+    if (args.mode == "laplace") != (args.config == "C5"):
+        ap.error("--mode laplace goes with --config C5 (Poisson data); vi/fitc with C2/C3")
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -85,7 +94,7 @@ def main():
     import torch.distributed as dist
 
     import sparsergps_amd as S
-    from sparsergps_amd.dist import HipRowBackend, RowShardedVI, shard_rows
+    from sparsergps_amd.dist import HipRowBackend, RowShardedLaplace, RowShardedVI, shard_rows
 
     if world > 1:
         torch.cuda.set_device(local_rank)
@@ -100,9 +109,22 @@ def main():
     s0, s1 = shard_rows(n, world, rank)
     n_loc = s1 - s0
 
-    backend = HipRowBackend(P["X"][s0:s1], P["y"][s0:s1], P["mu"][s0:s1], m, local_rank, cov_fun)
-    runner = RowShardedVI(backend, n, None)
+    backend = HipRowBackend(P["X"][s0:s1], P["y"][s0:s1], P["mu"][s0:s1], m, local_rank, cov_fun,
+                            args.mode)
     ctx = backend.ctx
+    nr_iters = []
+    if args.mode == "laplace":
+        ctx.lap_set_f(P["f0"][s0:s1])      # optimize_gp.R:480 start, then warm starts
+        lap = RowShardedLaplace(backend, None)
+
+        class _Runner:
+            def eval(self, theta, U, delta):
+                o, g, it = lap.eval(theta, U, delta, P["a"], args.tol_nr, 1000)
+                nr_iters.append(it)
+                return o, g
+        runner = _Runner()
+    else:
+        runner = RowShardedVI(backend, n, None)
     del P["X"]
 
     # an optimizer-like trajectory: theta moves every step (no result can be reused)
@@ -134,10 +156,13 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     phase_avg = {k: v / args.steps for k, v in phase_ms.items()}
+    timed_iters = nr_iters[args.warmup:]
 
-    # roofline of the dominant kernel: fused GEMM + gradient contraction (2 n_loc m^2 MFMA flops)
-    t_con = phase_avg.get("contract_knm", float("nan")) * 1e-3
-    flops = 2.0 * n_loc * m * m
+    # roofline of the dominant kernel: fused GEMM + gradient contraction (2 n_loc m^2 MFMA flops
+    # per pass; FITC and Laplace run two passes inside the "contract_knm"/"lap_grad_b" scope)
+    con_key = {"vi": "contract_knm", "fitc": "contract_knm", "laplace": "lap_grad_b"}[args.mode]
+    t_con = phase_avg.get(con_key, float("nan")) * 1e-3
+    flops = 2.0 * n_loc * m * m * (1 if args.mode == "vi" else 2)
     achieved = flops / t_con / 1e12 if t_con > 0 else float("nan")
     traffic = None
     tp = os.path.join(ROOT, "profiles", "pmc_traffic_contract_knm.json")
@@ -150,8 +175,14 @@ def main():
             traffic = None
 
     if rank == 0:
+        metric = {"vi": "sparse-GP objective+gradient evals/sec at n=1e6, m=1024, d=8",
+                  "fitc": "FITC objective+gradient evals/sec (secondary mode)",
+                  "laplace": "Poisson sparse-Laplace NR+objective+gradient evals/sec (C5, secondary)"}
+        workload = {"vi": "Titsias VI ELBO + gradient", "fitc": "FITC log-likelihood + gradient",
+                    "laplace": "Poisson Laplace: NR (warm start, tol_nr=%g) + obj_fun_pois + "
+                               "dlogq_dcov_par" % args.tol_nr}[args.mode]
         out = {
-            "metric": "sparse-GP objective+gradient evals/sec at n=1e6, m=1024, d=8",
+            "metric": metric[args.mode],
             "value": args.steps / elapsed,
             "unit": "evals/s",
             "n_gpus": world,
@@ -162,19 +193,21 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (SURVEY.md 8(d) C3 generator: X,U~U(0,10)^8, y=sum sin(x)/sqrt(8)+N(0,.25))",
-            "config": {"workload": f"{args.config}: Titsias VI ELBO + gradient, n={n}, m={m}, d={d}, "
+            "data": f"synthetic (SURVEY.md 8(d) {args.config} generator, numpy PCG64)",
+            "config": {"workload": f"{args.config}: {workload}, n={n}, m={m}, d={d}, "
                                    f"{cov_fun}, P={len(names)}, knots fixed",
                        "n": n, "m": m, "d": d, "kernel": cov_fun,
                        "parallelism": f"rows{world}" if world > 1 else "single"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
-                         "traffic": traffic, "kernel": "contract_knm (k_contract<8>)",
+                         "traffic": traffic, "kernel": con_key + " (k_contract<8>)",
                          "flops_per_launch": flops},
             "phases_ms": {k: round(v, 4) for k, v in phase_avg.items()},
             "objective": obj,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if args.mode == "laplace":
+            out["nr_iters_per_eval"] = timed_iters
+        if world == 1 and not args.no_cpu_baseline and args.mode == "vi":
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
     backend.close()
