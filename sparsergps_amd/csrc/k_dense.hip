@@ -136,30 +136,35 @@ __device__ __forceinline__ double rsqrt_nr(double p) {
   return y;
 }
 
-// Pivot step k of the SPD Gauss-Jordan inverse: P = inv(A_kk) for the current 64x64 pivot
-// block (a Schur complement, SPD).  Register-blocked Cholesky + triangular inverse with one
-// barrier per column (branch-free rank-1 updates), then P = X^T X through LDS.
-// logd[k] = sum log L_ii of the pivot block; a bad pivot sets status = global index + 1.
-__global__ void __launch_bounds__(256) k_gj_pivot(const double* __restrict__ A, int64_t lda,
-                                                  int k, double* __restrict__ P,
-                                                  double* __restrict__ logd,
-                                                  int* __restrict__ status) {
-  __shared__ double colv[2][64];
-  __shared__ double xrow[2][64];
-  __shared__ double piv_s[64];
-  __shared__ double Xs[64][65];
+// Pivot of the SPD Gauss-Jordan inverse: P = inv(B) for a 64x64 SPD block B (a Schur
+// complement) read from B[i * ldb + j] (global or LDS), by the symmetric sweep operator:
+// 64 in-place sweeps, each one barrier and a 4x4 register-blocked rank-1 update per thread
+// (no square roots, no separate triangular inverse).  The sweep pivots d_k are the Schur
+// complements L_kk^2 of the Cholesky factor, so *logd_slot = sum log L_kk = 1/2 sum log d_k;
+// a non-positive pivot sets status = gofs + k + 1 (R's chol() leading-minor order).
+// lds: GJ_PIVOT_LDS doubles.  Called by all 256 threads of the block.
+constexpr int GJ_PIVOT_LDS = 2 * 64 + 64;
+
+__device__ __forceinline__ double rcp_nr(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = r * fma(-d, r, 2.0);
+  r = r * fma(-d, r, 2.0);
+  return r;
+}
+
+__device__ __forceinline__ void gj_pivot_body(const double* B, int64_t ldb, int64_t gofs,
+                                              double* __restrict__ P,
+                                              double* __restrict__ logd_slot,
+                                              int* __restrict__ status, double* lds) {
+  double (*colv)[64] = reinterpret_cast<double (*)[64]>(lds);
+  double* piv_s = lds + 128;
   const int tid = threadIdx.x;
   const int bi = tid >> 4, bj = tid & 15;
-  const int64_t o = (int64_t)k * 64;
-  double a[4][4], x[4][4];
+  double a[4][4];
 #pragma unroll
   for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int i = 4 * bi + ii, j = 4 * bj + jj;
-      a[ii][jj] = A[(o + i) * lda + o + j];
-      x[ii][jj] = (i == j) ? 1.0 : 0.0;
-    }
+    for (int jj = 0; jj < 4; ++jj) a[ii][jj] = B[(4 * bi + ii) * ldb + 4 * bj + jj];
   for (int kb4 = 0; kb4 < 16; ++kb4) {
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
@@ -169,141 +174,71 @@ __global__ void __launch_bounds__(256) k_gj_pivot(const double* __restrict__ A, 
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii) colv[b][4 * bi + ii] = a[ii][kk];
       }
-      if (bi == kb4) {
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) xrow[b][4 * bj + jj] = x[kk][jj];
-      }
       __syncthreads();
-      const double p2 = colv[b][kc];
-      const double rp = rsqrt_nr(p2);
+      const double d = colv[b][kc];
+      const double r = rcp_nr(d);
       if (tid == 0) {
-        piv_s[kc] = p2 * rp;
-        if (!(p2 > 0.0) || !isfinite(p2)) atomicCAS(status, 0, (int)(o + kc + 1));
+        piv_s[kc] = d;
+        if (!(d > 0.0) || !isfinite(d)) atomicCAS(status, 0, (int)(gofs + kc + 1));
       }
-      double li[4], lj[4], xk[4];
+      // sweep: a_ij <- a_ij - v_i v_j / d with v = column kc and v_kc = -1, row/col kc
+      // zeroed first (gives a_ik = a_ik / d, a_kk = -1/d); the result is -inv(B)
+      double vi[4], vj[4];
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
         const int i = 4 * bi + ii;
-        li[ii] = (i > kc) ? colv[b][i] * rp : 0.0;
+        vi[ii] = (i == kc) ? -r : colv[b][i] * r;
       }
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int j = 4 * bj + jj;
-        lj[jj] = (j > kc) ? colv[b][j] * rp : 0.0;
-        xk[jj] = xrow[b][j] * rp;          // X[kc][j] = 0 for j > kc
+        vj[jj] = (j == kc) ? -1.0 : colv[b][j];
       }
-      // trailing update of A (only j > kc, i > kc change) and of the rows i > kc of X
+      if (bi == kb4) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) a[kk][jj] = 0.0;
+      }
+      if (bj == kb4) {
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) a[ii][kk] = 0.0;
+      }
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          a[ii][jj] = fma(-li[ii], lj[jj], a[ii][jj]);
-          x[ii][jj] = fma(-li[ii], xk[jj], x[ii][jj]);
-        }
-      if (bi == kb4) {                    // row kc of X is final
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) x[kk][jj] = xk[jj];
-      }
+        for (int jj = 0; jj < 4; ++jj) a[ii][jj] = fma(-vi[ii], vj[jj], a[ii][jj]);
     }
   }
-  // P = X^T X  (X = L^{-1} lower triangular)
 #pragma unroll
   for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int i = 4 * bi + ii, j = 4 * bj + jj;
-      Xs[i][j] = (j <= i) ? x[ii][jj] : 0.0;
-    }
+    for (int jj = 0; jj < 4; ++jj) P[(4 * bi + ii) * 64 + 4 * bj + jj] = -a[ii][jj];
   __syncthreads();
-  double pacc[4][4];
-#pragma unroll
-  for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) pacc[ii][jj] = 0.0;
-  for (int kr = 0; kr < 64; ++kr) {
-    double xa[4], xb[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) { xa[q] = Xs[kr][4 * bi + q]; xb[q] = Xs[kr][4 * bj + q]; }
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) pacc[ii][jj] = fma(xa[ii], xb[jj], pacc[ii][jj]);
-  }
-#pragma unroll
-  for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) P[(4 * bi + ii) * 64 + 4 * bj + jj] = pacc[ii][jj];
   double lg = (tid < 64) ? log(piv_s[tid]) : 0.0;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) lg += __shfl_xor(lg, off, 64);
-  if (tid == 0) logd[k] = lg;
+  if (tid == 0) *logd_slot = 0.5 * lg;
 }
 
-// R = P * A[k-block rows, all columns] (64 x mp) and C = A[all rows, k-block cols] (mp x 64).
-// One workgroup per 64-column block j.
-__global__ void __launch_bounds__(256) k_gj_panel(const double* __restrict__ A, int64_t lda,
-                                                  int k, const double* __restrict__ P,
-                                                  double* __restrict__ R, double* __restrict__ Cb) {
-  __shared__ double Ps[64][65];
-  __shared__ double Bs[64][65];
-  const int tid = threadIdx.x;
-  const int j = blockIdx.x;
-  const int64_t o = (int64_t)k * 64, oj = (int64_t)j * 64;
-  for (int e = tid; e < 4096; e += 256) {
-    const int r = e >> 6, c = e & 63;
-    Ps[r][c] = P[e];
-    Bs[r][c] = A[(o + r) * lda + oj + c];
-    Cb[(oj + r) * 64 + c] = A[(oj + r) * lda + o + c];
-  }
-  __syncthreads();
-  const int bi = tid >> 4, bj = tid & 15;
-  double acc[4][4];
-#pragma unroll
-  for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) acc[ii][jj] = 0.0;
-  for (int q = 0; q < 64; ++q) {
-    double pa[4], bb[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) { pa[t] = Ps[4 * bi + t][q]; bb[t] = Bs[q][4 * bj + t]; }
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) acc[ii][jj] = fma(pa[ii], bb[jj], acc[ii][jj]);
-  }
-#pragma unroll
-  for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) R[(int64_t)(4 * bi + ii) * (lda) + oj + 4 * bj + jj] = acc[ii][jj];
+// Pivot step k as its own launch (the first pivot of dense_spd_inverse).
+__global__ void __launch_bounds__(256) k_gj_pivot(const double* __restrict__ A, int64_t lda,
+                                                  int k, double* __restrict__ P,
+                                                  double* __restrict__ logd,
+                                                  int* __restrict__ status) {
+  __shared__ double lds[GJ_PIVOT_LDS];
+  const int64_t o = (int64_t)k * 64;
+  gj_pivot_body(A + o * lda + o, lda, o, P, logd + k, status, lds);
 }
 
-// Gauss-Jordan update of every 64x64 tile (i, j) for pivot block k (f64 MFMA, K = 64):
-//   i == k: A_kj = R_j (A_kk = P);   j == k: A_ik = -C_i P;   else A_ij -= C_i R_j.
-__global__ void __launch_bounds__(256) k_gj_update(double* __restrict__ A, int64_t lda, int k,
-                                                   const double* __restrict__ P,
-                                                   const double* __restrict__ R,
-                                                   const double* __restrict__ Cb) {
-  __shared__ double As[64][66];   // C_i (64 x 64)
-  __shared__ double Bs[64][66];   // R_j or P
-  const int ti = blockIdx.y, tj = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t oi = (int64_t)ti * 64, oj = (int64_t)tj * 64;
-  if (ti == k) {
-    for (int e = tid; e < 4096; e += 256) {
-      const int r = e >> 6, c = e & 63;
-      A[(oi + r) * lda + oj + c] = (tj == k) ? P[e] : R[(int64_t)r * lda + oj + c];
-    }
-    return;
-  }
-  const bool colk = (tj == k);
-  for (int e = tid; e < 4096; e += 256) {
-    const int r = e >> 6, c = e & 63;
-    As[r][c] = Cb[(oi + r) * 64 + c];
-    Bs[r][c] = colk ? P[e] : R[(int64_t)r * lda + oj + c];
-  }
-  __syncthreads();
+// One Gauss-Jordan step k, out of place (Ao -> An), every 64x64 tile (i, j) in one launch:
+//   i == k: An_kj = P_k Ao_kj (An_kk = P_k);   j == k: An_ik = -Ao_ik P_k;
+//   else    An_ij = Ao_ij - (Ao_ik P_k) Ao_kj                       (two 64^3 f64-MFMA products)
+// Look-ahead: the workgroup owning tile (k+1, k+1) factors its fresh tile right away and writes
+// the next pivot inverse P_{k+1}, so a step costs one launch instead of pivot + panel + update.
+constexpr int GJ_LS = 70;   // LDS row stride (doubles): conflict-free f64 fragment reads
+
+__device__ __forceinline__ void gj_mm64(const double* As, const double* Bs, d4 (&acc)[2][2]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int wr = wv >> 1, wc = wv & 1;
-  d4 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -314,8 +249,8 @@ __global__ void __launch_bounds__(256) k_gj_update(double* __restrict__ A, int64
     double af[2], bf[2];
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
-      af[f] = As[wr * 32 + f * 16 + (lane & 15)][kx];
-      bf[f] = Bs[kx][wc * 32 + f * 16 + (lane & 15)];
+      af[f] = As[(wr * 32 + f * 16 + (lane & 15)) * GJ_LS + kx];
+      bf[f] = Bs[kx * GJ_LS + wc * 32 + f * 16 + (lane & 15)];
     }
 #pragma unroll
     for (int fm = 0; fm < 2; ++fm)
@@ -323,17 +258,101 @@ __global__ void __launch_bounds__(256) k_gj_update(double* __restrict__ A, int64
       for (int fn = 0; fn < 2; ++fn)
         acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
   }
+}
+
+__device__ __forceinline__ void gj_load_tile(double* S, const double* G, int64_t ldg) {
+  for (int e = threadIdx.x; e < 4096; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    S[r * GJ_LS + c] = G[r * ldg + c];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
+                                                 double* __restrict__ An, int64_t lda, int k,
+                                                 int nb, const double* __restrict__ Pk,
+                                                 double* __restrict__ Pn,
+                                                 double* __restrict__ logd,
+                                                 int* __restrict__ status) {
+  __shared__ double lds[2 * 64 * GJ_LS];
+  double* S0 = lds;
+  double* S1 = lds + 64 * GJ_LS;
+  const int i = blockIdx.y, j = blockIdx.x;
+  const int64_t oi = (int64_t)i * 64, oj = (int64_t)j * 64, ok = (int64_t)k * 64;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  d4 acc[2][2];
+  if (i == k) {
+    if (j == k) {
+      for (int e = threadIdx.x; e < 4096; e += 256)
+        An[(oi + (e >> 6)) * lda + oj + (e & 63)] = Pk[e];
+      return;
+    }
+    gj_load_tile(S0, Pk, 64);
+    gj_load_tile(S1, Ao + ok * lda + oj, lda);
+    __syncthreads();
+    gj_mm64(S0, S1, acc);
+#pragma unroll
+    for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
+          const int c = wc * 32 + fn * 16 + (lane & 15);
+          An[(oi + r) * lda + oj + c] = acc[fm][fn][q];
+        }
+    return;
+  }
+  gj_load_tile(S0, Ao + oi * lda + ok, lda);     // C_i = Ao_ik
+  gj_load_tile(S1, Pk, 64);
+  __syncthreads();
+  gj_mm64(S0, S1, acc);                          // C_i P_k
+  if (j == k) {
+#pragma unroll
+    for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
+          const int c = wc * 32 + fn * 16 + (lane & 15);
+          An[(oi + r) * lda + oj + c] = -acc[fm][fn][q];
+        }
+    return;
+  }
+  __syncthreads();                               // everyone is done reading S0 / S1
 #pragma unroll
   for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
     for (int fn = 0; fn < 2; ++fn)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int64_t row = oi + wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
-        const int64_t col = oj + wc * 32 + fn * 16 + (lane & 15);
-        double* dst = &A[row * lda + col];
-        *dst = colk ? -acc[fm][fn][q] : (*dst - acc[fm][fn][q]);
+        const int r = wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
+        const int c = wc * 32 + fn * 16 + (lane & 15);
+        S0[r * GJ_LS + c] = acc[fm][fn][q];
       }
+  gj_load_tile(S1, Ao + ok * lda + oj, lda);     // Ao_kj
+  __syncthreads();
+  gj_mm64(S0, S1, acc);                          // (C_i P_k) Ao_kj
+  const bool look_ahead = (i == k + 1) && (j == k + 1);
+  if (look_ahead) __syncthreads();               // S0 is reused for the fresh tile below
+#pragma unroll
+  for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
+        const int c = wc * 32 + fn * 16 + (lane & 15);
+        const int64_t g = (oi + r) * lda + oj + c;
+        const double v = Ao[g] - acc[fm][fn][q];
+        An[g] = v;
+        if (look_ahead) S0[r * GJ_LS + c] = v;
+      }
+  if (look_ahead) {
+    __syncthreads();
+    gj_pivot_body(S0, GJ_LS, (int64_t)(k + 1) * 64, Pn, logd + k + 1, status, S1);
+  }
 }
 
 __global__ void __launch_bounds__(256) k_copy_block(const double* __restrict__ src,
@@ -534,12 +553,22 @@ hipError_t dense_trtri(const double* L, int64_t mp, int64_t lda, const double* d
 
 hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* Cb, double* P,
                              double* logd, int* status, hipStream_t s) {
+  // R: mp x mp ping-pong buffer; P: nb 64x64 pivot inverses (mp * 64 doubles); Cb unused.
+  (void)Cb;
   const int nb = (int)(mp / SGP_DB);
+  hipLaunchKernelGGL(k_gj_pivot, dim3(1), dim3(256), 0, s, A, mp, 0, P, logd, status);
+  double* src = A;
+  double* dst = R;
   for (int k = 0; k < nb; ++k) {
-    hipLaunchKernelGGL(k_gj_pivot, dim3(1), dim3(256), 0, s, A, mp, k, P, logd, status);
-    hipLaunchKernelGGL(k_gj_panel, dim3(nb), dim3(256), 0, s, A, mp, k, P, R, Cb);
-    hipLaunchKernelGGL(k_gj_update, dim3(nb, nb), dim3(256), 0, s, A, mp, k, P, R, Cb);
+    double* Pn = (k + 1 < nb) ? P + (int64_t)(k + 1) * 4096 : P;
+    hipLaunchKernelGGL(k_gj_step, dim3(nb, nb), dim3(256), 0, s, src, dst, mp, k, nb,
+                       P + (int64_t)k * 4096, Pn, logd, status);
+    double* t = src;
+    src = dst;
+    dst = t;
   }
+  if (src != A)
+    return hipMemcpyAsync(A, src, sizeof(double) * mp * mp, hipMemcpyDeviceToDevice, s);
   return hipGetLastError();
 }
 
