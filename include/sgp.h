@@ -171,6 +171,26 @@ int sgp_lap_begin(sgp_ctx* ctx, int kernel, const double* theta, const double* U
 int sgp_lap_step(sgp_ctx* ctx, const double* red_in, double* red_out, int64_t* count,
                  int* done, double* obj, double* grad, int* nr_iters);
 
+/* Posterior of the knot values u at the end of a fit, from the context's last completed
+ * evaluation (VI: vi_functions.R:1161-1180; FITC: laplace_gradient_ascent.R:1635-1655;
+ * Laplace: newtrap_sparseGP.R:137-176).  muu, u_mean: m host values; u_var: m x m host,
+ * column-major (ld m). */
+int sgp_posterior_u(sgp_ctx* ctx, const double* muu, double* u_mean, double* u_var);
+
+/* Sparse prediction at x_pred (np x d, column-major, ld ldxp) from a knot posterior:
+ *   SGP_PRED_VI      predict_vi      (R/vi_functions.R:1222-1333; gaussian only)
+ *   SGP_PRED_LAPLACE predict_laplace (R/laplace_approx_prediction.R:3-123; FITC or Laplace fits,
+ *                    gaussian != 0 selects the family == "gaussian" Sigma22)
+ * as dispatched by predict_gp (R/laplace_approx_prediction.R:408-542).  u_var is m x m
+ * column-major (ld ldv).  pred_var: np values, or with full_cov the np x np matrix
+ * (column-major, ld ldpv).  Host buffers; device work space is allocated per call. */
+enum { SGP_PRED_VI = 0, SGP_PRED_LAPLACE = 1 };
+int sgp_predict(int device, int kernel, const double* theta, double delta, int method,
+                int gaussian, const double* U, int64_t m, int64_t ldu, const double* u_mean,
+                const double* muu, const double* u_var, int64_t ldv, const double* x_pred,
+                int64_t np, int64_t ldxp, int d, const double* mu_pred, int full_cov,
+                double* pred_mean, double* pred_var, int64_t ldpv);
+
 /* Per-kernel timing of the last evaluation (HIP events on the launch stream).
  * names: '\n'-separated kernel-phase names; ms: their durations (max n entries). */
 int sgp_ctx_enable_timing(sgp_ctx* ctx, int enable);

@@ -539,10 +539,11 @@ def laplace_mats(cov_par, cov_fun, xu, xy, delta):
 
 
 def newtrap_sparseGP(start_vals, cov_par, cov_fun, xy, xu, y, mu, m, delta=1e-6,
-                     maxit=1000, tol=1e-6):
+                     maxit=1000, tol=1e-6, muu=None):
     """newtrap_sparseGP.R:6-186 for the Poisson likelihood.
 
-    Returns dict(gp, objective_function_values, gradient, u_posterior_mean/variance needs muu -> omitted).
+    Returns dict(gp, objective_function_values, gradient[, u_posterior_mean,
+    u_posterior_variance] when muu is given (l.137-176, with the loop's last W)).
     """
     y = np.asarray(y, dtype=np.float64).reshape(-1)
     mu = np.asarray(mu, dtype=np.float64).reshape(-1)
@@ -561,7 +562,11 @@ def newtrap_sparseGP(start_vals, cov_par, cov_fun, xy, xu, y, mu, m, delta=1e-6,
         grad_psi = grad_loglik_fn_pois(ff, y, mu, Sigma12, Sigma22, Z, m)
         ff = newtrap_sparseGP_update(ff, W, Z, Sigma12, Sigma22, grad_psi, y, mu, m)
         obj.append(obj_fun_pois(ff, mu, Z, Sigma12, Sigma22, y, m))
-    return {"gp": ff, "objective_function_values": np.array(obj), "gradient": grad_psi}
+    out = {"gp": ff, "objective_function_values": np.array(obj), "gradient": grad_psi}
+    if muu is not None:
+        out["u_posterior_mean"], out["u_posterior_variance"] = laplace_posterior_u(
+            cov_par, cov_fun, xu, xy, y, mu, muu, ff, W, delta)
+    return out
 
 
 def dlogq_dcov_par(cov_par, cov_fun, xu, xy, y, ff, mu, m, delta=1e-6):
@@ -611,6 +616,93 @@ def dlogq_dcov_par(cov_par, cov_fun, xu, xy, y, ff, mu, m, delta=1e-6):
         comp3 = -(1 / W) * (B * comp3_1) + (1 / W) * (BS12 @ (C @ (Sigma12.T @ (B * comp3_1))))  # l.313-314
         grad[par_name] = float(0.5 * comp2 - 0.5 * comp1 - 0.5 * ((comp4 * (-W3)) @ comp3))  # l.334-336
     return {"gradient": grad, "trans_par": trans_par}
+
+
+# --------------------------------------------------------------------------------------
+# Knot posteriors at the end of the drivers, and sparse prediction
+# --------------------------------------------------------------------------------------
+
+
+def fitc_posterior_u(cov_par, cov_fun, xu, xy, y, mu, muu, delta=1e-6):
+    """Posterior of u at the end of norm_grad_ascent (laplace_gradient_ascent.R:1635-1655):
+    the VI formula with the FITC diagonal Z."""
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    mu = np.asarray(mu, dtype=np.float64).reshape(-1)
+    Sigma12, Sigma22, Z = fitc_mats(cov_par, cov_fun, xu, xy, delta)
+    ZSig12 = (1 / Z)[:, None] * Sigma12
+    R1 = r_chol(Sigma22 + Sigma12.T @ ZSig12)
+    v = ZSig12.T @ (y - mu)
+    u_mean = muu + v - Sigma12.T @ (ZSig12 @ r_solve(R1, r_solve(R1.T, v)))
+    Y = r_solve(R1.T, Sigma12.T)
+    u_var = Sigma22 - Sigma12.T @ ZSig12 + (ZSig12.T @ Y.T @ Y @ ZSig12)
+    return u_mean, u_var
+
+
+def laplace_posterior_u(cov_par, cov_fun, xu, xy, y, mu, muu, ff, W, delta=1e-6):
+    """Posterior of u at the end of newtrap_sparseGP (newtrap_sparseGP.R:137-176); W is the
+    d2 log p(y|f) of the last NR iteration's start (the loop leaves it one step stale)."""
+    ff = np.asarray(ff, dtype=np.float64).reshape(-1)
+    mu = np.asarray(mu, dtype=np.float64).reshape(-1)
+    Sigma12, Sigma22, Z = laplace_mats(cov_par, cov_fun, xu, xy, delta)
+    ZSig12 = (1 / Z)[:, None] * Sigma12
+    WmZ_inv = 1 / ((1 / W) - Z)
+    TT = Sigma12.T @ (WmZ_inv[:, None] * Sigma12)
+    R = r_chol(Sigma22 + Sigma12.T @ ZSig12)
+    v = ZSig12.T @ (ff - mu)
+    u_mean = muu + v - Sigma12.T @ (ZSig12 @ r_solve(R, r_solve(R.T, v)))
+    u_var = Sigma22 + TT + TT @ r_solve(Sigma22 - TT, TT)
+    return u_mean, u_var
+
+
+def _pred_mats(xu, x_pred, cov_fun, cov_par, delta, sub_tau):
+    d = _as_matrix(xu).shape[1]
+    lnames = lnames_for(cov_fun, d)
+    s12, s22 = _cov_mats(cov_par, cov_fun, xu, x_pred, delta, lnames)
+    if sub_tau:
+        s22 = s22 - float(cov_par["tau"]) ** 2 * np.eye(s22.shape[0])
+    return s12, s22, lnames
+
+
+def predict_vi(u_mean, u_var, xu, x_pred, cov_fun, cov_par, mu, muu, full_cov=False,
+               delta=1e-6):
+    """vi_functions.R:1222-1333 (gaussian family)."""
+    x_pred = _as_matrix(x_pred)
+    s12, s22, lnames = _pred_mats(xu, x_pred, cov_fun, cov_par, delta, True)
+    s22_inv = r_solve(s22)
+    pred_mean = mu + s12 @ r_solve(s22, np.asarray(u_mean) - np.asarray(muu))
+    T = -s22_inv + s22_inv @ u_var @ s22_inv
+    if full_cov:
+        if cov_fun == "ard":
+            s11 = make_cov_mat_ardC(x_pred, None, cov_par, cov_fun, delta, lnames)
+        else:
+            s11 = make_cov_matC(x_pred, None, cov_par, cov_fun, delta)
+        pred_var = s11 + s12 @ T @ s12.T
+    else:
+        s11 = float(cov_par["tau"]) ** 2 + float(cov_par["sigma"]) ** 2 + delta
+        pred_var = s11 + np.sum(s12 * (T @ s12.T).T, axis=1)
+    return {"pred_mean": pred_mean, "pred_var": pred_var}
+
+
+def predict_laplace(u_mean, u_var, xu, x_pred, cov_fun, cov_par, mu, muu, full_cov=False,
+                    family="gaussian", delta=1e-6):
+    """laplace_approx_prediction.R:3-123 (FITC / Laplace sparse prediction)."""
+    x_pred = _as_matrix(x_pred)
+    s12, s22, lnames = _pred_mats(xu, x_pred, cov_fun, cov_par, delta, family == "gaussian")
+    s22_inv = r_solve(s22)
+    pred_mean = mu + s12 @ r_solve(s22, np.asarray(u_mean) - np.asarray(muu))
+    T = -s22_inv + s22_inv @ u_var @ s22_inv
+    if full_cov:
+        if cov_fun == "ard":
+            s11 = make_cov_mat_ardC(x_pred, None, cov_par, cov_fun, delta, lnames)
+        else:
+            s11 = make_cov_matC(x_pred, None, cov_par, cov_fun, delta)
+        Q = s12 @ r_solve(s22, s12.T)
+        s11 = np.diag(np.diag(s11 - Q)) + Q
+        pred_var = s11 + s12 @ T @ s12.T
+    else:
+        c0 = float(cov_par["sigma"]) ** 2 + float(cov_par["tau"]) ** 2
+        pred_var = np.array([c0 + s12[i] @ T @ s12[i] for i in range(s12.shape[0])])
+    return {"pred_mean": pred_mean, "pred_var": pred_var}
 
 
 # --------------------------------------------------------------------------------------

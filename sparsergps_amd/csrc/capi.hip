@@ -127,6 +127,7 @@ struct sgp_ctx {
   double delta = 0.0;
   unsigned flags = 0;
   int phase = 0;
+  int last_mode = 0;   // 1 VI, 2 FITC, 3 Laplace: the evaluation sgp_posterior_u refers to
   // K22 stage runs on `aux` concurrently with phase 1 (it depends only on U and theta)
   hipStream_t aux = nullptr;
   hipEvent_t ev_knots = nullptr, ev_k22 = nullptr;
@@ -142,6 +143,7 @@ struct sgp_ctx {
   double* lv = nullptr;                   // LV_N x n_pad row vectors
   double* lm = nullptr;                   // LM_N x mp_max knot vectors
   double* lslab = nullptr;                // K^T V row-chunk partials
+  double* Cprev = nullptr;                // (K22 + S_B)^-1 of the previous NR iterate
   int64_t lslab_cap = 0;
   double* lred[2] = {nullptr, nullptr};   // ping-pong reduction buffers of sgp_eval_laplace
   int lap_state = 0, lap_it = 0, lap_maxit = 0;
@@ -217,7 +219,8 @@ void ctx_free(sgp_ctx* c) {
                   c->dinv,   c->logd22, c->logdB, c->uvec,    c->cdiag, c->status, c->red1,
                   c->red2,   c->slab_syrk, c->slab_con, c->slab_small, c->sc,
                   c->Xt22,   c->T22,    c->dinv22, c->omega, c->pvec, c->rowq, c->red2f,
-                  c->y,      c->mu,     c->lv,     c->lm,    c->lslab, c->lred[0], c->lred[1]};
+                  c->y,      c->mu,     c->lv,     c->lm,    c->lslab, c->lred[0], c->lred[1],
+                  c->Cprev};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->g_bm) hipGraphExecDestroy(c->g_bm);
@@ -758,6 +761,7 @@ int sgp_vi_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
             status[0] ? "Sigma22" : "Sigma22 + t(Sigma12) %*% ZSig12");
     return SGP_ENOTPD;
   }
+  c->last_mode = 1;
   if (getenv("SGP_DEBUG_SC")) {
     fprintf(stderr, "[sgp sc] ld22 %.17g ldB %.17g tu %.17g trKS %.17g trBS %.17g rr %.17g g22",
             sc[SC_LD22], sc[SC_LDB], sc[SC_TU], sc[SC_TRKS], sc[SC_TRBS], sc[SC_RR]);
@@ -954,6 +958,7 @@ int sgp_fitc_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
             status[0] ? "Sigma22" : "Sigma22 + t(Sigma12) %*% ZSig12");
     return SGP_ENOTPD;
   }
+  c->last_mode = 2;
   const double n = (double)c->n_global;
   const double ld22 = 2.0 * sc[SC_LD22], ldB = 2.0 * sc[SC_LDB];
   const double rr = sc[SC_RR], sumlogz = sc[SC_RR + 1], tu = sc[SC_TU];
@@ -1014,6 +1019,7 @@ static int lap_ensure(sgp_ctx* c) {
   const int64_t rc = sgp_lap_red_count(SGP_KERNEL_ARD, SGP_MAXD, c->m_max);
   st = st ? st : dalloc(&c->lred[0], rc);
   st = st ? st : dalloc(&c->lred[1], rc);
+  st = st ? st : dalloc(&c->Cprev, mp * mp);
   if (st) return st;
   HIPCHK(hipMemset(c->lv, 0, sizeof(double) * LV_N * np_));
   HIPCHK(hipMemset(c->lm, 0, sizeof(double) * LM_N * mp));
@@ -1124,6 +1130,9 @@ static int lap_consume_obj(sgp_ctx* c, const double* red, int64_t o, bool first,
       HIPCHK(dense_spd_inverse(c->Bm, mp, c->Xt, c->T1, c->dinv, c->logdB, c->status + 1,
                                c->stream));
     }
+    if (!first)   // newtrap_sparseGP's u posterior uses the W of the last update's start
+      HIPCHK(hipMemcpyAsync(c->Cprev, c->Binv, sizeof(double) * mm, hipMemcpyDeviceToDevice,
+                            c->stream));
     HIPCHK(dense_axpby(1.0, c->K22, 1.0, red + o, c->Binv, mm, c->stream));
     HIPCHK(dense_spd_inverse(c->Binv, mp, c->Xt, c->T1, c->dinv, c->logdB, c->status + 2,
                              c->stream));
@@ -1307,6 +1316,7 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
     }
     if (obj) *obj = c->lap_obj;
     if (nr_iters) *nr_iters = c->lap_it;
+    c->last_mode = 3;
     *count = 0;
     *done = 1;
     c->lap_state = LS_NONE;
@@ -1343,6 +1353,186 @@ int sgp_eval_laplace(sgp_ctx* c, int kernel, const double* theta, const double* 
     st = sgp_lap_step(c, c->lred[cur], c->lred[cur ^ 1], &count, &done, obj, grad, nr_iters);
     if (st) return st;
     cur ^= 1;
+  }
+  return SGP_OK;
+}
+
+
+// ------------------------------------------------------------------------- knot posterior
+// u | y at the end of the drivers, from the replicated state of the last evaluation:
+//   VI / FITC (vi_functions.R:1161-1180, laplace_gradient_ascent.R:1635-1655):
+//     u_mean = muu + K22 Bm^-1 t,  u_var = K22 Bm^-1 K22   (= Sigma22 - S + S Bm^-1 S)
+//   Laplace (newtrap_sparseGP.R:137-176): u_mean = muu + K22 (K22+S_Z)^-1 t_Z(f_hat),
+//     u_var = K22 (K22 + S_B(W_prev))^-1 K22   (= Sigma22 + TT + TT (Sigma22 - TT)^-1 TT)
+int sgp_posterior_u(sgp_ctx* c, const double* muu, double* u_mean, double* u_var) {
+  if (!c || !muu || !u_mean || !u_var) { set_err("invalid arguments"); return SGP_EINVAL; }
+  if (c->last_mode == 0) { set_err("no completed evaluation in this context"); return SGP_EINVAL; }
+  HIPCHK(hipSetDevice(c->device));
+  const int64_t mp = c->mp, m = c->m;
+  const double* vec = c->uvec;
+  const double* inv = c->Binv;
+  if (c->last_mode == 3) {
+    vec = lmv(c, LM_X1);
+    if (c->lap_it >= 2) inv = c->Cprev;
+  }
+  HIPCHK(dense_gemv(c->K22, mp, vec, 1.0, c->T22, c->stream));   // T22 row 0 as scratch
+  HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->K22, mp, inv, mp, 0.0, c->T1, mp,
+                       c->stream));
+  HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->T1, mp, c->K22, mp, 0.0, c->M3,
+                       mp, c->stream));
+  std::vector<double> hv((size_t)mp), hm((size_t)(mp * mp));
+  HIPCHK(hipMemcpyAsync(hv.data(), c->T22, sizeof(double) * mp, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(hm.data(), c->M3, sizeof(double) * mp * mp, hipMemcpyDeviceToHost,
+                        c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (int64_t j = 0; j < m; ++j) u_mean[j] = muu[j] + hv[(size_t)j];
+  for (int64_t j = 0; j < m; ++j)
+    for (int64_t i = 0; i < m; ++i) u_var[i + j * m] = hm[(size_t)(i * mp + j)];
+  return SGP_OK;
+}
+
+// ------------------------------------------------------------------------- prediction
+namespace {
+struct DevBuf {
+  double* p = nullptr;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+};
+struct StreamGuard {
+  hipStream_t s = nullptr;
+  ~StreamGuard() {
+    if (s) {
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+    }
+  }
+};
+struct IntBuf {
+  int* p = nullptr;
+  ~IntBuf() { if (p) (void)hipFree(p); }
+};
+}  // namespace
+
+int sgp_predict(int device, int kernel, const double* theta, double delta, int method,
+                int gaussian, const double* U, int64_t m, int64_t ldu, const double* u_mean,
+                const double* muu, const double* u_var, int64_t ldv, const double* x_pred,
+                int64_t np, int64_t ldxp, int d, const double* mu_pred, int full_cov,
+                double* pred_mean, double* pred_var, int64_t ldpv) {
+  KernParams kp;
+  int st = make_params(kernel, d, theta, delta, &kp);
+  if (st) return st;
+  if (!U || m < 1 || ldu < m || !u_mean || !muu || !u_var || ldv < m || !x_pred || np < 1 ||
+      ldxp < np || !mu_pred || !pred_mean || !pred_var || (full_cov && ldpv < np)) {
+    set_err("invalid sgp_predict arguments");
+    return SGP_EINVAL;
+  }
+  if (method != SGP_PRED_VI && method != SGP_PRED_LAPLACE) {
+    set_err("invalid prediction method %d", method);
+    return SGP_EINVAL;
+  }
+  if (method == SGP_PRED_VI && !gaussian) {
+    set_err("Error: VI not supported for non-gaussian data.");   // predict_gp, l.424-427
+    return SGP_EINVAL;
+  }
+  HIPCHK(hipSetDevice(device));
+  StreamGuard sg;
+  HIPCHK(hipStreamCreateWithFlags(&sg.s, hipStreamNonBlocking));
+  hipStream_t s = sg.s;
+  const int64_t mp = round_up(m, SGP_TILE), npp = round_up(np, SGP_TILE), mm = mp * mp;
+  DevBuf dU, K22, Kinv, R, Pb, logd, V, T1, T22, wv, Xp, Kp, yv, rowq, q, S, Y;
+  IntBuf status;
+  st = dalloc(&dU.p, mp * d);
+  st = st ? st : dalloc(&K22.p, mm);
+  st = st ? st : dalloc(&Kinv.p, mm);
+  st = st ? st : dalloc(&R.p, mm);
+  st = st ? st : dalloc(&Pb.p, mp * 64);
+  st = st ? st : dalloc(&logd.p, mp / SGP_DB);
+  st = st ? st : dalloc(&V.p, mm);
+  st = st ? st : dalloc(&T1.p, mm);
+  st = st ? st : dalloc(&T22.p, mm);
+  st = st ? st : dalloc(&wv.p, 2 * mp);
+  st = st ? st : dalloc(&Xp.p, npp * d);
+  st = st ? st : dalloc(&Kp.p, npp * mp);
+  st = st ? st : dalloc(&yv.p, npp);
+  st = st ? st : dalloc(&rowq.p, npp * (mp / SGP_TILE));
+  st = st ? st : dalloc(&q.p, npp);
+  st = st ? st : dalloc(&status.p, 4);
+  if (!st && full_cov) {
+    st = dalloc(&S.p, npp * npp);
+    st = st ? st : dalloc(&Y.p, npp * mp);
+  }
+  if (st) return st;
+  {
+    std::vector<double> hU((size_t)(mp * d), 0.0), hX((size_t)(npp * d), 0.0);
+    for (int c = 0; c < d; ++c) {
+      for (int64_t j = 0; j < m; ++j) hU[(size_t)(c * mp + j)] = U[j + c * ldu];
+      for (int64_t i = 0; i < np; ++i) hX[(size_t)(c * npp + i)] = x_pred[i + c * ldxp];
+    }
+    std::vector<double> hd((size_t)mp, 0.0), hV((size_t)mm, 0.0);
+    for (int64_t j = 0; j < m; ++j) hd[(size_t)j] = u_mean[j] - muu[j];
+    for (int64_t i = 0; i < m; ++i)
+      for (int64_t j = 0; j < m; ++j) hV[(size_t)(i * mp + j)] = u_var[i + j * ldv];
+    HIPCHK(hipMemcpy(dU.p, hU.data(), sizeof(double) * hU.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(Xp.p, hX.data(), sizeof(double) * hX.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(wv.p + mp, hd.data(), sizeof(double) * mp, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(V.p, hV.data(), sizeof(double) * mm, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(status.p, 0, sizeof(int) * 4));
+  }
+  // Sigma22: the gaussian family subtracts tau^2 I again (vi_functions.R:1246-1260,
+  // laplace_approx_prediction.R:25-43) -> diagonal sigma^2 + delta; otherwise Kuu+(tau^2+delta)I
+  const double diag_sub = gaussian ? kp.tau2 : 0.0;
+  HIPCHK(launch_build_kmm(kp, dU.p, mp, m, mp, diag_sub, K22.p, s));
+  HIPCHK(hipMemcpyAsync(Kinv.p, K22.p, sizeof(double) * mm, hipMemcpyDeviceToDevice, s));
+  HIPCHK(dense_spd_inverse(Kinv.p, mp, R.p, nullptr, Pb.p, logd.p, status.p, s));
+  HIPCHK(dense_gemv(Kinv.p, mp, wv.p + mp, 1.0, wv.p, s));          // Sigma22^-1 (u_mean - muu)
+  HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, Kinv.p, mp, V.p, mp, 0.0, T1.p, mp,
+                       s));
+  HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, T1.p, mp, Kinv.p, mp, 0.0, T22.p, mp,
+                       s));                                           // Sigma22^-1 u_var Sigma22^-1
+  const bool lap_full = (method == SGP_PRED_LAPLACE) && full_cov;
+  if (!lap_full) HIPCHK(dense_axpby(1.0, T22.p, -1.0, Kinv.p, T22.p, mm, s));   // temp22
+  HIPCHK(launch_build_knm(kp, Xp.p, npp, np, npp, dU.p, mp, m, mp, Kp.p, s));
+  HIPCHK(launch_gemv_rows(Kp.p, npp, mp, wv.p, nullptr, yv.p, nullptr, s));
+  std::vector<double> hy((size_t)npp), hq((size_t)npp, 0.0);
+  if (!full_cov) {
+    HIPCHK(launch_rowquad_knm(kp, Kp.p, T22.p, np, npp, m, mp, nullptr, 0.0, nullptr, nullptr,
+                              nullptr, rowq.p, q.p, s));
+  } else {
+    if (lap_full)
+      HIPCHK(launch_rowquad_knm(kp, Kp.p, Kinv.p, np, npp, m, mp, nullptr, 0.0, nullptr, nullptr,
+                                nullptr, rowq.p, q.p, s));
+    if (method == SGP_PRED_VI)
+      HIPCHK(launch_fill_cov(kp, Xp.p, np, npp, Xp.p, np, npp, true, S.p, npp, s));
+    else
+      HIPCHK(hipMemsetAsync(S.p, 0, sizeof(double) * npp * npp, s));
+    HIPCHK(launch_gemm64(false, false, false, npp, mp, mp, 1.0, Kp.p, mp, T22.p, mp, 0.0, Y.p, mp,
+                         s));
+    HIPCHK(launch_gemm64(false, true, false, npp, npp, mp, 1.0, Y.p, mp, Kp.p, mp, 1.0, S.p, npp,
+                         s));
+  }
+  int hst[4];
+  HIPCHK(hipMemcpyAsync(hy.data(), yv.p, sizeof(double) * npp, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hq.data(), q.p, sizeof(double) * npp, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hst, status.p, sizeof(hst), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (hst[0]) {
+    set_err("Sigma22 is not positive definite (leading minor of order %d)", hst[0]);
+    return SGP_ENOTPD;
+  }
+  for (int64_t i = 0; i < np; ++i) pred_mean[i] = mu_pred[i] + hy[(size_t)i];
+  if (!full_cov) {
+    // vi_functions.R:1321: tau^2 + sigma^2 + delta; laplace_approx_prediction.R:114: sigma^2 + tau^2
+    const double c0 = (method == SGP_PRED_VI) ? (kp.tau2 + kp.sig2) + delta : kp.sig2 + kp.tau2;
+    for (int64_t i = 0; i < np; ++i) pred_var[i] = c0 + hq[(size_t)i];
+    return SGP_OK;
+  }
+  std::vector<double> hS((size_t)(npp * npp));
+  HIPCHK(hipMemcpyAsync(hS.data(), S.p, sizeof(double) * hS.size(), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  for (int64_t j = 0; j < np; ++j)
+    for (int64_t i = 0; i < np; ++i) pred_var[i + j * ldpv] = hS[(size_t)(i * npp + j)];
+  if (lap_full) {   // diag(diag(Sigma11 - Q)) + Q with Sigma11_ii = sigma^2 + tau^2 + delta
+    const double c11 = (kp.sig2 + kp.tau2) + delta;
+    for (int64_t i = 0; i < np; ++i) pred_var[i + i * ldpv] += c11 - hq[(size_t)i];
   }
   return SGP_OK;
 }

@@ -131,6 +131,18 @@ class SparseGPContext:
         _lib.check(st)
         return obj.value, grad
 
+    def posterior_u(self, muu):
+        """Knot posterior (u_mean, u_var) of the last completed evaluation, as the drivers
+        return it at the end of a fit (vi_functions.R:1161-1180,
+        laplace_gradient_ascent.R:1635-1655, newtrap_sparseGP.R:137-176)."""
+        mu_u = np.ascontiguousarray(np.asarray(muu, dtype=np.float64).reshape(-1))
+        m = mu_u.size
+        um = np.zeros(m, dtype=np.float64)
+        uv = np.zeros((m, m), dtype=np.float64, order="F")
+        _lib.check(self._lib.sgp_posterior_u(self.handle, _lib.dptr(mu_u), _lib.dptr(um),
+                                             _lib.dptr(uv)))
+        return um, uv
+
     # ------------------------------------------------------------------ Poisson Laplace
     def lap_set_f(self, f=None, fill=0.0):
         """Set the resident latent vector f (NR warm start); f=None fills with `fill`."""
