@@ -191,6 +191,23 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
                 int64_t np, int64_t ldxp, int d, const double* mu_pred, int full_cov,
                 double* pred_mean, double* pred_var, int64_t ldpv);
 
+/* Knot gradients (xu_opt = "simultaneous"; the knot branches of delbo_dcov_par
+ * R/vi_functions.R:425-593, dlogp_dcov_par R/laplace_approx_gradient.R:973-1126 and
+ * dlogq_dcov_par 341-543, with dsqexp_dx2 / dsqexp_dx2_ard
+ * R/covariance_function_derivatives.R:178-302 as dcov_fun_dknot; d <= 8).  When enabled,
+ * every evaluation also contracts G against dK12/du in the same GEMM epilogue, and the
+ * multi-GPU second reduction buffers grow by sgp_knot_red_extra(d, m) doubles (VI, FITC;
+ * sgp_lap_red_count already has room).  sgp_knot_gradient then returns, row-major
+ * (knot-major, quirk Q16), d obj / d u_kc times the reference's factor
+ * (ub - lb) / ((u - lb)(ub - u) + 1e-4) (quirk Q8) with bounds = d x 2 column-major
+ * [lower | upper], or NULL for the reference's knot_bounds from this context's rows
+ * (vi_functions.R:175-178; multi-GPU callers pass the global bounds, see
+ * sgp_ctx_row_bounds). */
+int sgp_ctx_enable_knot_grad(sgp_ctx* ctx, int enable);
+int64_t sgp_knot_red_extra(int d, int64_t m);
+int sgp_knot_gradient(sgp_ctx* ctx, const double* bounds, double* grad_knot);
+int sgp_ctx_row_bounds(sgp_ctx* ctx, double* col_min, double* col_max);
+
 /* Per-kernel timing of the last evaluation (HIP events on the launch stream).
  * names: '\n'-separated kernel-phase names; ms: their durations (max n entries). */
 int sgp_ctx_enable_timing(sgp_ctx* ctx, int enable);

@@ -265,6 +265,71 @@ def lnames_for(cov_fun, d):
 
 
 # --------------------------------------------------------------------------------------
+# Knot derivatives (R/covariance_function_derivatives.R:178-306) and the dSigma/dknot
+# matrices of the gradient functions' knot branches (vi_functions.R:429-482)
+# --------------------------------------------------------------------------------------
+
+
+def knot_bounds_of(xy):
+    """vi_functions.R:175-178 / laplace_approx_gradient.R:769-772 (quirk Q9)."""
+    xy = _as_matrix(xy)
+    lo, hi = xy.min(axis=0), xy.max(axis=0)
+    diffs = hi - lo
+    return np.column_stack([lo - diffs / 10, hi + diffs / 10])
+
+
+def dsqexp_dx2(x1, x2, cov_par, bounds, ard=False):
+    """dsqexp_dx2 (l.178-233) / dsqexp_dx2_ard (l.237-302) with transform = TRUE: the
+    derivative vector over the d coordinates of x2, times dx2/dx2t (quirk Q8)."""
+    x1 = np.asarray(x1, dtype=np.float64)
+    x2 = np.asarray(x2, dtype=np.float64)
+    sigma = float(cov_par["sigma"])
+    dx2_dx2t = (bounds[:, 1] - bounds[:, 0]) / (((x2 - bounds[:, 0]) * (bounds[:, 1] - x2)) + 1e-4)
+    if ard:
+        ls = np.array([float(cov_par[f"l{c + 1}"]) for c in range(x1.size)])
+        k = sigma ** 2 * math.exp(-1 / 2 * np.sum((x1 - x2) ** 2 / ls ** 2))
+        return (1 / ls ** 2) * (x1 - x2) * k * dx2_dx2t
+    l = float(cov_par["l"])
+    k = sigma ** 2 * math.exp(-np.sum((x1 - x2) ** 2) / (2 * l ** 2))
+    return (1 / l ** 2) * (x1 - x2) * k * dx2_dx2t
+
+
+def knot_trans(xu, bounds):
+    """inv_trans_fun (l.196-200): the transformed knot coordinates (trans_knot)."""
+    xu = _as_matrix(xu)
+    return np.log((xu - bounds[:, 0]) + 1e-4) - np.log((bounds[:, 1] - xu) + 1e-4)
+
+
+def _dknot_mats(k, c, cov_par, xu, xy, bounds, ard):
+    """dsig12_dknot / dsig22_dknot (vi_functions.R:429-482): column k of dSigma12 and row and
+    column k of dSigma22 for coordinate c of knot k."""
+    n, m = xy.shape[0], xu.shape[0]
+    d12 = np.zeros((n, m))
+    d12[:, k] = [dsqexp_dx2(xy[i], xu[k], cov_par, bounds, ard)[c] for i in range(n)]
+    d22 = np.zeros((m, m))
+    col = np.array([dsqexp_dx2(xu[i], xu[k], cov_par, bounds, ard)[c] for i in range(m)])
+    d22[:, k] = col
+    d22[k, :] = col
+    return d12, d22
+
+
+def _knot_loop(xu, xy, cov_par, dcov_fun_dknot, knot_opt, one):
+    """Row-major knot gradient (quirk Q16): grad_knot[(k-1)*d + c] for k in knot_opt."""
+    xu, xy = _as_matrix(xu), _as_matrix(xy)
+    m, d = xu.shape
+    bounds = knot_bounds_of(xy)
+    ard = dcov_fun_dknot == "ard"
+    opt = set(range(1, m + 1)) if knot_opt is None else set(knot_opt)
+    g = np.zeros(m * d)
+    for k in range(m):
+        for c in range(d):
+            if (k + 1) in opt:
+                d12, d22 = _dknot_mats(k, c, cov_par, xu, xy, bounds, ard)
+                g[k * d + c] = one(d12, d22)
+    return g, knot_trans(xu, bounds)
+
+
+# --------------------------------------------------------------------------------------
 # L2: Titsias VI objective and gradient (R/vi_functions.R)
 # --------------------------------------------------------------------------------------
 
@@ -329,7 +394,8 @@ def _gaussian_comps(A, B, C, FF, Sigma12, Sigma22, dS12, dS22, comp2_1):
     return comp1, comp2
 
 
-def delbo_dcov_par(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6):
+def delbo_dcov_par(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6, dcov_fun_dknot=None,
+                   knot_opt=None):
     """vi_functions.R:126-602 with dcov_fun_dknot = NA (xu_opt = "fixed").
 
     Returns {"gradient": OrderedDict(name -> d ELBO / d log theta), "trans_par": OrderedDict}.
@@ -375,6 +441,15 @@ def delbo_dcov_par(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6):
         else:
             dtrace = -(1 / (2 * tau ** 2)) * np.sum(A_trace)               # l.54-60
         grad[par_name] = float(0.5 * comp2 - 0.5 * comp1 + dtrace)         # l.416-417
+    if dcov_fun_dknot is not None:                                         # l.425-593
+
+        def one(d12, d22):
+            A_trace = -np.sum((2 * d12 - FF.T @ d22) * FF.T, axis=1)
+            comp1, comp2 = _gaussian_comps(np.zeros(n), B, C, FF, Sigma12, Sigma22, d12, d22,
+                                           comp2_1)
+            return float(0.5 * comp2 - 0.5 * comp1 - (1 / (2 * tau ** 2)) * np.sum(A_trace))
+        gk, tk = _knot_loop(xu, xy, cov_par, dcov_fun_dknot, knot_opt, one)
+        return {"gradient": grad, "knot_gradient": gk, "trans_par": trans_par, "trans_knot": tk}
     return {"gradient": grad, "trans_par": trans_par}
 
 
@@ -428,7 +503,8 @@ def fitc_obj_eval(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6):
     return obj_fun_norm(mu, Z, s12, s22, y)
 
 
-def dlogp_dcov_par(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6):
+def dlogp_dcov_par(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6, dcov_fun_dknot=None,
+                   knot_opt=None):
     """laplace_approx_gradient.R:720-971 (FITC gradient, knots fixed)."""
     y = np.asarray(y, dtype=np.float64).reshape(-1)
     mu = np.asarray(mu, dtype=np.float64).reshape(-1)
@@ -461,6 +537,14 @@ def dlogp_dcov_par(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6):
         A = A1 - A2
         comp1, comp2 = _gaussian_comps(A, B, C, FF, Sigma12, Sigma22, dS12, dS22, comp2_1)
         grad[par_name] = float(0.5 * comp2 - 0.5 * comp1)                  # l.964-965
+    if dcov_fun_dknot is not None:                                         # l.973-1126
+
+        def one(d12, d22):
+            A = -np.sum((2 * d12 - FF.T @ d22) * FF.T, axis=1)
+            comp1, comp2 = _gaussian_comps(A, B, C, FF, Sigma12, Sigma22, d12, d22, comp2_1)
+            return float(0.5 * comp2 - 0.5 * comp1)
+        gk, tk = _knot_loop(xu, xy, cov_par, dcov_fun_dknot, knot_opt, one)
+        return {"gradient": grad, "knot_gradient": gk, "trans_par": trans_par, "trans_knot": tk}
     return {"gradient": grad, "trans_par": trans_par}
 
 
@@ -569,7 +653,8 @@ def newtrap_sparseGP(start_vals, cov_par, cov_fun, xy, xu, y, mu, m, delta=1e-6,
     return out
 
 
-def dlogq_dcov_par(cov_par, cov_fun, xu, xy, y, ff, mu, m, delta=1e-6):
+def dlogq_dcov_par(cov_par, cov_fun, xu, xy, y, ff, mu, m, delta=1e-6, dcov_fun_dknot=None,
+                   knot_opt=None):
     """laplace_approx_gradient.R:25-553 (Poisson sparse Laplace gradient, knots fixed)."""
     y = np.asarray(y, dtype=np.float64).reshape(-1)
     mu = np.asarray(mu, dtype=np.float64).reshape(-1)
@@ -615,6 +700,17 @@ def dlogq_dcov_par(cov_par, cov_fun, xu, xy, y, ff, mu, m, delta=1e-6):
         BS12 = B[:, None] * Sigma12
         comp3 = -(1 / W) * (B * comp3_1) + (1 / W) * (BS12 @ (C @ (Sigma12.T @ (B * comp3_1))))  # l.313-314
         grad[par_name] = float(0.5 * comp2 - 0.5 * comp1 - 0.5 * ((comp4 * (-W3)) @ comp3))  # l.334-336
+    if dcov_fun_dknot is not None:                                         # l.341-543
+
+        def one(d12, d22):
+            A = -np.sum((2 * d12 - FF.T @ d22) * FF.T, axis=1)
+            comp1, comp2 = _gaussian_comps(A, B, C, FF, Sigma12, Sigma22, d12, d22, comp2_1)
+            c31 = A * grad_log_py_ff + 2 * d12 @ GG - FF.T @ d22 @ GG
+            BS12 = B[:, None] * Sigma12
+            c3 = -(1 / W) * (B * c31) + (1 / W) * (BS12 @ (C @ (Sigma12.T @ (B * c31))))
+            return float(0.5 * comp2 - 0.5 * comp1 - 0.5 * ((comp4 * (-W3)) @ c3))
+        gk, tk = _knot_loop(xu, xy, cov_par, dcov_fun_dknot, knot_opt, one)
+        return {"gradient": grad, "knot_gradient": gk, "trans_par": trans_par, "trans_knot": tk}
     return {"gradient": grad, "trans_par": trans_par}
 
 

@@ -126,6 +126,12 @@ struct sgp_ctx {
   int64_t m = 0, mp = 0, n_global = 0;
   double delta = 0.0;
   unsigned flags = 0;
+  // knot gradients (opt-in, d <= 8)
+  bool knot_on = false;
+  double *knot_slab = nullptr, *knot_part = nullptr, *knot_kmm = nullptr;
+  std::vector<double> knot_raw;           // d F / d u (m x d, row-major), before the chain factor
+  std::vector<double> hU;                 // host copy of the knots (m x d, column-major)
+  std::vector<double> xmin, xmax;         // column ranges of this context's rows
   int phase = 0;
   int last_mode = 0;   // 1 VI, 2 FITC, 3 Laplace: the evaluation sgp_posterior_u refers to
   // K22 stage runs on `aux` concurrently with phase 1 (it depends only on U and theta)
@@ -220,7 +226,7 @@ void ctx_free(sgp_ctx* c) {
                   c->red2,   c->slab_syrk, c->slab_con, c->slab_small, c->sc,
                   c->Xt22,   c->T22,    c->dinv22, c->omega, c->pvec, c->rowq, c->red2f,
                   c->y,      c->mu,     c->lv,     c->lm,    c->lslab, c->lred[0], c->lred[1],
-                  c->Cprev};
+                  c->Cprev,  c->knot_slab, c->knot_part, c->knot_kmm};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->g_bm) hipGraphExecDestroy(c->g_bm);
@@ -242,6 +248,9 @@ hipError_t upload_rows(double* dst, const double* src, int64_t n, int64_t n_pad)
 }
 
 int upload_knots(sgp_ctx* c, const double* U, int64_t m, int64_t ldu) {
+  c->hU.assign((size_t)(m * c->d), 0.0);
+  for (int q = 0; q < c->d; ++q)
+    for (int64_t j = 0; j < m; ++j) c->hU[(size_t)(j + q * m)] = U[j + q * ldu];
   std::vector<double> h((size_t)(c->mp * c->d), 0.0);
   for (int q = 0; q < c->d; ++q)
     for (int64_t j = 0; j < m; ++j) h[(size_t)(q * c->mp + j)] = U[j + q * ldu];
@@ -466,8 +475,8 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->cdiag, mp);
   st = st ? st : dalloc(&c->status, 4);
   st = st ? st : dalloc(&c->red1, sgp_vi_red1_count(m_max));
-  st = st ? st : dalloc(&c->red2, 64);
-  st = st ? st : dalloc(&c->red2f, sgp_fitc_red2_count(SGP_KERNEL_ARD, SGP_MAXD, m_max));
+  st = st ? st : dalloc(&c->red2, 64 + mp * 8);
+  st = st ? st : dalloc(&c->red2f, sgp_fitc_red2_count(SGP_KERNEL_ARD, SGP_MAXD, m_max) + mp * 8);
   st = st ? st : dalloc(&c->slab_syrk, c->slab_syrk_cap);
   st = st ? st : dalloc(&c->slab_con, c->slab_con_cap);
   st = st ? st : dalloc(&c->slab_small, SLAB_SMALL);
@@ -478,6 +487,18 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
     ctx_free(c);
     delete c;
     return st;
+  }
+  c->xmin.assign((size_t)d, 0.0);
+  c->xmax.assign((size_t)d, 0.0);
+  for (int q = 0; q < d; ++q) {
+    double lo = X[q * ldx], hi = X[q * ldx];
+    for (int64_t i = 1; i < n; ++i) {
+      const double v = X[i + q * ldx];
+      lo = v < lo ? v : lo;
+      hi = v > hi ? v : hi;
+    }
+    c->xmin[(size_t)q] = lo;
+    c->xmax[(size_t)q] = hi;
   }
   // X: column-major with ld = n_pad, zero padded
   std::vector<double> hx((size_t)(np_ * d), 0.0);
@@ -569,6 +590,108 @@ int64_t sgp_vi_red1_count(int64_t m) {
 }
 
 int64_t sgp_vi_red2_count(int kernel, int d) { return num_ls(kernel, d) + 5; }
+
+int64_t sgp_knot_red_extra(int d, int64_t m) { return round_up(m, SGP_TILE) * d; }
+
+// One K12 contraction pass: per-tile records summed into rec_out (L + 5 doubles) and, with
+// knot gradients on, the per-knot column sums summed (or accumulated) into knot_out (mp x d).
+static int contract_pass(sgp_ctx* c, const double* M, ConArgs ca, double* rec_out,
+                         double* knot_out, bool knot_acc) {
+  int64_t nrec = 0, nwg = 0;
+  if (c->knot_on) ca.knot_slab = c->knot_slab;
+  HIPCHK(launch_contract_args(c->kp, c->K, M, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp, c->m,
+                              c->mp, ca, c->slab_con, &nrec, &nwg, c->stream));
+  HIPCHK(launch_colsum(c->slab_con, nwg, nrec, rec_out, c->stream));
+  if (c->knot_on)
+    HIPCHK(launch_knot_reduce(c->knot_slab, c->n_pad / SGP_TILE, c->mp, c->kp.d, c->knot_part,
+                              knot_out, knot_acc, c->stream));
+  return SGP_OK;
+}
+
+// d F / d u_kc = sum_i G_ik dK12_ik/du_kc + <G22, dK22/du_kc> (the knot branches of
+// delbo_dcov_par / dlogp_dcov_par / dlogq_dcov_par, vi_functions.R:425-593): combines the
+// reduced K12 part (knot_red, device) with the m x m part into c->knot_raw.
+static int knot_finish(sgp_ctx* c, const double* knot_red, const double* uvec, const double* Ainv,
+                       const double* Binv, const double* M3, double a, double b, double cc,
+                       const double* v, const double* w, double e2) {
+  if (!c->knot_on) return SGP_OK;
+  const KernParams& kp = c->kp;
+  const int64_t m = c->m, d = kp.d;
+  HIPCHK(launch_knot_kmm(kp, c->U, c->mp, m, c->mp, uvec, Ainv, Binv, M3, a, b, cc, v, w, e2,
+                         c->knot_kmm, c->stream));
+  std::vector<double> h12((size_t)(m * d)), h22((size_t)(m * d));
+  HIPCHK(hipMemcpyAsync(h12.data(), knot_red, sizeof(double) * m * d, hipMemcpyDeviceToHost,
+                        c->stream));
+  HIPCHK(hipMemcpyAsync(h22.data(), c->knot_kmm, sizeof(double) * m * d, hipMemcpyDeviceToHost,
+                        c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->knot_raw.assign((size_t)(m * d), 0.0);
+  const bool ard = kp.kernel == SGP_KERNEL_ARD;
+  for (int64_t k = 0; k < m; ++k)
+    for (int q = 0; q < d; ++q) {
+      // the K12 part carries (x - u)/l_c (ARD) or (x - u) (sqexp); the m x m part raw u - u
+      const double f12 = ard ? kp.rl[q] : kp.rl2[0];
+      c->knot_raw[(size_t)(k * d + q)] =
+          h12[(size_t)(k * d + q)] * f12 + h22[(size_t)(k * d + q)] * kp.rl2[q];
+    }
+  return SGP_OK;
+}
+
+int sgp_ctx_enable_knot_grad(sgp_ctx* c, int enable) {
+  if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
+  if (!enable) { c->knot_on = false; return SGP_OK; }
+  if (c->d > 8) {
+    set_err("knot gradients are implemented for d <= 8 (d = %d)", c->d);
+    return SGP_EINVAL;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  if (!c->knot_slab) {
+    int st = dalloc(&c->knot_slab, (c->n_pad / SGP_TILE) * c->mp_max * c->d);
+    st = st ? st : dalloc(&c->knot_part, 64 * c->mp_max * c->d);
+    st = st ? st : dalloc(&c->knot_kmm, c->mp_max * c->d);
+    if (st) return st;
+  }
+  c->knot_on = true;
+  return SGP_OK;
+}
+
+int sgp_ctx_row_bounds(sgp_ctx* c, double* lo, double* hi) {
+  if (!c || !lo || !hi) { set_err("invalid arguments"); return SGP_EINVAL; }
+  for (int q = 0; q < c->d; ++q) {
+    lo[q] = c->xmin[(size_t)q];
+    hi[q] = c->xmax[(size_t)q];
+  }
+  return SGP_OK;
+}
+
+int sgp_knot_gradient(sgp_ctx* c, const double* bounds, double* grad_knot) {
+  if (!c || !grad_knot) { set_err("invalid arguments"); return SGP_EINVAL; }
+  const int64_t m = c->m, d = c->d;
+  if (c->knot_raw.size() != (size_t)(m * d) || c->last_mode == 0) {
+    set_err("no knot gradient: enable it with sgp_ctx_enable_knot_grad before the evaluation");
+    return SGP_EINVAL;
+  }
+  std::vector<double> lb((size_t)d), ub((size_t)d);
+  for (int q = 0; q < d; ++q) {
+    if (bounds) {
+      lb[(size_t)q] = bounds[q];
+      ub[(size_t)q] = bounds[d + q];
+    } else {   // vi_functions.R:175-178: column range of xy widened by a tenth on each side
+      const double diff = c->xmax[(size_t)q] - c->xmin[(size_t)q];
+      lb[(size_t)q] = c->xmin[(size_t)q] - diff / 10;
+      ub[(size_t)q] = c->xmax[(size_t)q] + diff / 10;
+    }
+  }
+  // dsqexp_dx2(_ard) transform = TRUE factor dx2_dx2t (covariance_function_derivatives.R:186)
+  for (int64_t k = 0; k < m; ++k)
+    for (int q = 0; q < d; ++q) {
+      const double u = c->hU[(size_t)(k + q * m)];
+      const double chain = (ub[(size_t)q] - lb[(size_t)q]) /
+                           (((u - lb[(size_t)q]) * (ub[(size_t)q] - u)) + 1e-4);
+      grad_knot[k * d + q] = c->knot_raw[(size_t)(k * d + q)] * chain;
+    }
+  return SGP_OK;
+}
 
 static int k22_stage(sgp_ctx* c, double diag_sub);
 
@@ -726,16 +849,16 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
                                c->stream));
     HIPCHK(launch_colsum(c->slab_small, nb, kp.P, c->sc + SC_G22, c->stream));
   }
-  int64_t nrec = 0, nwg = 0;
   {
     Scope tm(c, "contract_knm");
-    HIPCHK(launch_contract_knm(kp, c->K, c->Pm, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp,
-                               c->m, mp, c->r, 1.0 / z, nullptr, c->uvec, nullptr, 1.0, c->cdiag,
-                               1, c->slab_con, &nrec, &nwg, c->stream));
-  }
-  {
-    Scope tm(c, "contract_reduce");
-    HIPCHK(launch_colsum(c->slab_con, nwg, nrec, red2, c->stream));
+    ConArgs ca;
+    ca.r = c->r;
+    ca.invz = 1.0 / z;
+    ca.uvec = c->uvec;
+    ca.cdiag = c->cdiag;
+    ca.count_a2 = 1;
+    int st2 = contract_pass(c, c->Pm, ca, red2, red2 + sgp_vi_red2_count(kp.kernel, kp.d), false);
+    if (st2) return st2;
   }
   c->phase = 2;
   return SGP_OK;
@@ -788,7 +911,8 @@ int sgp_vi_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
   for (int q = 0; q < L; ++q) grad[1 + q] = r2[1 + q] + sc[SC_G22 + 1 + q];
   grad[L + 1] = 2.0 * kp.tau2 * (c_sum - (c_cnt - c->delta * c_dg) / kp.tau2) +
                 2.0 * kp.tau2 * trW - 2.0 * trace_term;
-  return SGP_OK;
+  return knot_finish(c, red2 + n2, c->uvec, c->K22inv, c->Binv, c->M3, -0.5, 0.5,
+                     -1.0 / (2.0 * kp.tau2), nullptr, nullptr, 0.0);
 }
 
 int sgp_eval_vi(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
@@ -877,7 +1001,8 @@ int sgp_fitc_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned f
   c->flags = flags;
   int st = bm_stage(c, S, 1.0);
   if (st) return st;
-  HIPCHK(hipMemsetAsync(red2, 0, sizeof(double) * sgp_fitc_red2_count(kp.kernel, kp.d, c->m),
+  HIPCHK(hipMemsetAsync(red2, 0, sizeof(double) * (sgp_fitc_red2_count(kp.kernel, kp.d, c->m) +
+                                                    (c->knot_on ? mp * kp.d : 0)),
                         c->stream));
   {
     Scope tm(c, "mm_vectors");
@@ -905,16 +1030,23 @@ int sgp_fitc_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned f
   int64_t nrec = 0, nwg = 0;
   {
     Scope tm(c, "contract_knm");
+    nrec = kp.L + 5;
+    double* kout = red2 + off + 2 * nrec;
     // pass 1: G1 = alpha u^T - diag(1/Z) K Bm^-1
-    HIPCHK(launch_contract_knm(kp, c->K, c->Binv, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp,
-                               c->m, mp, c->r, 0.0, c->zinv, c->uvec, c->zinv, -1.0, nullptr, 0,
-                               c->slab_con, &nrec, &nwg, c->stream));
-    HIPCHK(launch_colsum(c->slab_con, nwg, nrec, red2 + off, c->stream));
+    ConArgs a1;
+    a1.r = c->r;
+    a1.invz_vec = c->zinv;
+    a1.uvec = c->uvec;
+    a1.rs_vec = c->zinv;
+    a1.rs = -1.0;
+    st = contract_pass(c, c->Binv, a1, red2 + off, kout, false);
+    if (st) return st;
     // pass 2: G2 = -diag(omega) K K22^-1
-    HIPCHK(launch_contract_knm(kp, c->K, c->K22inv, c->X, c->n_pad, c->n, c->n_pad, c->U,
-                               c->mp, c->m, mp, c->r, 0.0, nullptr, nullptr, c->omega, -1.0,
-                               nullptr, 0, c->slab_con, &nrec, &nwg, c->stream));
-    HIPCHK(launch_colsum(c->slab_con, nwg, nrec, red2 + off + nrec, c->stream));
+    ConArgs a2;
+    a2.rs_vec = c->omega;
+    a2.rs = -1.0;
+    st = contract_pass(c, c->K22inv, a2, red2 + off + nrec, kout, true);
+    if (st) return st;
   }
   c->phase = 12;
   return SGP_OK;
@@ -970,7 +1102,8 @@ int sgp_fitc_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
   grad[0] = 2.0 * (a[0] + b[0]) + sc[SC_G22] + kp.sig2 * sum_omega;
   for (int q = 0; q < L; ++q) grad[1 + q] = a[1 + q] + b[1 + q] + sc[SC_G22 + 1 + q];
   grad[L + 1] = 2.0 * kp.tau2 * (a[1 + L] + b[1 + L]) + kp.tau2 * sum_omega;
-  return SGP_OK;
+  return knot_finish(c, red2 + off + 2 * nrec, c->uvec, c->K22inv, c->Binv, c->M3, -0.5, 0.5, 0.5,
+                     nullptr, nullptr, 0.0);
 }
 
 int sgp_eval_fitc(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
@@ -1005,7 +1138,7 @@ static int64_t lap_rec_off(int64_t mp) { return mp * mp + mp + 8; }
 
 int64_t sgp_lap_red_count(int kernel, int d, int64_t m) {
   const int64_t mp = round_up(m, SGP_TILE);
-  return 2 * (mp * mp + mp + 8) + 2 * (num_ls(kernel, d) + 5) + 8;
+  return 2 * (mp * mp + mp + 8) + 2 * (num_ls(kernel, d) + 5) + 8 + mp * 8;
 }
 
 static int lap_ensure(sgp_ctx* c) {
@@ -1257,7 +1390,8 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
     HIPCHK(launch_syrk_aug(c->K, n_pad, mp, c->r, lvec(c, LV_A), c->slab_syrk, c->slab_syrk_cap,
                            red_out, c->stream, 3));
     HIPCHK(launch_colsum(c->slab_small, nb, 1, red_out + mm + mp + 1, c->stream));
-    int64_t nrec = 0, nwg = 0;
+    int64_t nrec = kp.L + 5;
+    double* kout = red_out + off + 2 * nrec;
     // G1 = c2 s^T - h GG^T - diag(B) K C
     ConArgs a1;
     a1.alpha_in = lvec(c, LV_C2);
@@ -1266,17 +1400,15 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
     a1.vvec = lmv(c, LM_NGG);
     a1.rs_vec = lvec(c, LV_B);
     a1.rs = -1.0;
-    HIPCHK(launch_contract_args(kp, c->K, c->Binv, c->X, n_pad, n, n_pad, c->U, c->mp, c->m, mp,
-                                a1, c->slab_con, &nrec, &nwg, c->stream));
-    HIPCHK(launch_colsum(c->slab_con, nwg, nrec, red_out + off, c->stream));
+    int st = contract_pass(c, c->Binv, a1, red_out + off, kout, false);
+    if (st) return st;
     // G2 = -diag(2a) K K22^-1
     ConArgs a2;
     a2.rs_vec = lvec(c, LV_A);
     a2.rs = -2.0;
-    HIPCHK(launch_contract_args(kp, c->K, c->K22inv, c->X, n_pad, n, n_pad, c->U, c->mp, c->m,
-                                mp, a2, c->slab_con, &nrec, &nwg, c->stream));
-    HIPCHK(launch_colsum(c->slab_con, nwg, nrec, red_out + off + nrec, c->stream));
-    *count = off + 2 * nrec;
+    st = contract_pass(c, c->K22inv, a2, red_out + off + nrec, kout, true);
+    if (st) return st;
+    *count = off + 2 * nrec + (c->knot_on ? mp * kp.d : 0);
     c->lap_state = LS_FIN;
     return SGP_OK;
   }
@@ -1317,6 +1449,9 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
     if (obj) *obj = c->lap_obj;
     if (nr_iters) *nr_iters = c->lap_it;
     c->last_mode = 3;
+    int st = knot_finish(c, red_in + off + 2 * nrec, lmv(c, LM_S), c->K22inv, c->Binv, c->M3,
+                         -0.5, 0.5, 1.0, lmv(c, LM_CW), lmv(c, LM_GG), 0.25);
+    if (st) return st;
     *count = 0;
     *done = 1;
     c->lap_state = LS_NONE;

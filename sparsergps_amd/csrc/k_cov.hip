@@ -220,7 +220,57 @@ __global__ void __launch_bounds__(256) k_contract_kmm(KernParams kp, const doubl
         red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
+// Knot part of the m x m contraction for d K22 / d u_kc = e_k v^T + v e_k^T,
+// v_l = K22_lk (u_lc - u_kc) / l_c^2: one block per knot k, out[k*d + c] =
+// 2 sum_l G22_kl K22_kl (u_lc - u_kc) (raw coordinates; the 1/l_c^2 is applied by the caller).
+__global__ void __launch_bounds__(256) k_knot_kmm(KernParams kp, const double* __restrict__ U,
+                                                  int64_t ldu, int64_t m, int64_t mp,
+                                                  const double* __restrict__ uvec,
+                                                  const double* __restrict__ Ainv,
+                                                  const double* __restrict__ Binv,
+                                                  const double* __restrict__ M3, double a,
+                                                  double b, double c,
+                                                  const double* __restrict__ vvec,
+                                                  const double* __restrict__ wvec, double e2,
+                                                  double* __restrict__ out) {
+  __shared__ double red[4][SGP_MAXD];
+  const int64_t k = blockIdx.x;
+  double uk[SGP_MAXD], acc[SGP_MAXD];
+  for (int q = 0; q < kp.d; ++q) {
+    uk[q] = U[k + q * ldu];
+    acc[q] = 0.0;
+  }
+  for (int64_t l = threadIdx.x; l < m; l += 256) {
+    double ul[SGP_MAXD];
+    for (int q = 0; q < kp.d; ++q) ul[q] = U[l + q * ldu];
+    const int64_t o = k * mp + l;
+    double g = a * uvec[k] * uvec[l] + b * (Ainv[o] - Binv[o]) + c * M3[o];
+    if (vvec) g += e2 * (vvec[k] * wvec[l] + wvec[k] * vvec[l]);
+    const double gk = 2.0 * g * kvalue(kp, ul, uk);
+    for (int q = 0; q < kp.d; ++q) acc[q] = fma(gk, ul[q] - uk[q], acc[q]);
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int q = 0; q < kp.d; ++q) {
+    double v = wave_sum(acc[q]);
+    if (lane == 0) red[w][q] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kp.d)
+    out[k * kp.d + threadIdx.x] =
+        red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
 }  // namespace
+
+hipError_t launch_knot_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,
+                           int64_t mp, const double* uvec, const double* Ainv,
+                           const double* Binv, const double* M3, double a, double b, double c,
+                           const double* vvec, const double* wvec, double e2, double* out,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_knot_kmm, dim3((unsigned)m), dim3(256), 0, s, kp, U, ldu, m, mp, uvec, Ainv,
+                     Binv, M3, a, b, c, vvec, wvec, e2, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_fill_cov(const KernParams& kp, const double* x, int64_t n, int64_t ldx,
                            const double* xp, int64_t np, int64_t ldxp, bool sym, double* out,

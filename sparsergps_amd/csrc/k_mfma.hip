@@ -220,7 +220,7 @@ k_syrk_reduce_t(const double* __restrict__ slab_t, const double* __restrict__ sl
 // staged K values (iz_i = invz_vec ? invz_vec[i] : invz), optionally written to alpha_out.
 enum { EPI_GRAD = 0, EPI_ROWQUAD = 1 };
 
-template <int DT, int EPI, bool V2 = false>
+template <int DT, int EPI, bool V2 = false, bool KNOT = false>
 __global__ void __launch_bounds__(256, 2)
 k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict__ M,
            const double* __restrict__ X, int64_t ldx, int64_t n, int64_t n_pad,
@@ -393,6 +393,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     __syncthreads();
 
     const int L = kp.L;
+    double* s_kn = s_us + T128 * d;           // KNOT: [2 (wr)][128 cols][d]
     double e_sig = 0.0, c_sum = 0.0, c_cnt = 0.0, c_dg = 0.0;
     double e_l[DT];
 #pragma unroll
@@ -407,6 +408,11 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
       for (int c = 0; c < DT; ++c) uj[c] = (c < d) ? s_us[col * d + c] : 0.0;
       const double ucol = s_u[col];
       const double vcol = with_v ? s_v[col] : 0.0;
+      double kn[DT];
+      if constexpr (KNOT) {
+#pragma unroll
+        for (int c = 0; c < DT; ++c) kn[c] = 0.0;
+      }
 #pragma unroll
       for (int fm = 0; fm < 4; ++fm) {
 #pragma unroll
@@ -427,6 +433,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
               const double tt = t * t;
               s += tt;
               if (ard) e_l[c] = fma(gk, tt, e_l[c]);
+              if constexpr (KNOT) kn[c] = fma(gk, t, kn[c]);
             }
           }
           if (!ard) e_l[0] = fma(gk, s * rl2s, e_l[0]);
@@ -443,7 +450,27 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
           }
         }
       }
+      if constexpr (KNOT) {
+        // column sums over this wave's 64 rows: the 4 lanes sharing (lane & 15)
+#pragma unroll
+        for (int c = 0; c < DT; ++c) {
+          if (c < d) {
+            double v2 = kn[c];
+            v2 += __shfl_xor(v2, 16, 64);
+            v2 += __shfl_xor(v2, 32, 64);
+            if ((lane >> 4) == 0) s_kn[(wr * T128 + col) * d + c] = v2;
+          }
+        }
+      }
       __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (KNOT) {
+      __syncthreads();
+      for (int e = tid; e < T128 * d; e += 256) {
+        const int col = e / d, c = e % d;
+        ca.knot_slab[(ti * mp + j0 + col) * d + c] =
+            s_kn[col * d + c] + s_kn[(T128 + col) * d + c];
+      }
     }
 
     // record = [e_sig, e_l[0..L-1], c_sum, c_cnt, c_dg, alpha^T alpha]
@@ -469,6 +496,28 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     if (tid < nrec)
       slab[wgid * nrec + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
   }
+}
+
+// knot partials: part[r][col] = sum_{ti = r, r+64, ...} slab[ti][col]   (grid: ncol/256 x 64)
+__global__ void __launch_bounds__(256)
+k_knot_reduce1(const double* __restrict__ slab, int64_t ntiles, int64_t ncol,
+               double* __restrict__ part) {
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r = blockIdx.y;
+  if (col >= ncol) return;
+  double s = 0.0;
+  for (int64_t t = r; t < ntiles; t += gridDim.y) s += slab[t * ncol + col];
+  part[r * ncol + col] = s;
+}
+
+__global__ void __launch_bounds__(256)
+k_knot_reduce2(const double* __restrict__ part, int rows, int64_t ncol, double* __restrict__ out,
+               int accumulate) {
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (col >= ncol) return;
+  double s = 0.0;
+  for (int r = 0; r < rows; ++r) s += part[(int64_t)r * ncol + col];
+  out[col] = accumulate ? out[col] + s : s;
 }
 
 // rowq[tj][i] summed over the column tiles -> out[i] (deterministic order)
@@ -604,6 +653,16 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
   return hipGetLastError();
 }
 
+hipError_t launch_knot_reduce(const double* knot_slab, int64_t ntiles, int64_t mp, int d,
+                              double* part, double* out, bool accumulate, hipStream_t s) {
+  const int64_t ncol = mp * d;
+  const unsigned gx = (unsigned)((ncol + 255) / 256);
+  hipLaunchKernelGGL(k_knot_reduce1, dim3(gx, 64), dim3(256), 0, s, knot_slab, ntiles, ncol, part);
+  hipLaunchKernelGGL(k_knot_reduce2, dim3(gx), dim3(256), 0, s, part, 64, ncol, out,
+                     accumulate ? 1 : 0);
+  return hipGetLastError();
+}
+
 hipError_t launch_contract_args(const KernParams& kp, const double* K, const double* M,
                                 const double* X, int64_t ldx, int64_t n, int64_t n_pad,
                                 const double* U, int64_t ldu, int64_t m, int64_t mp,
@@ -613,7 +672,17 @@ hipError_t launch_contract_args(const KernParams& kp, const double* K, const dou
   const int nrec = kp.L + 5;
   *nrec_out = nrec;
   *nwg_out = nwg;
-  if (ca.beta_in != nullptr) {
+  if (ca.knot_slab != nullptr) {
+    if (kp.d > 8) return hipErrorInvalidValue;   // knot epilogue is instantiated for d <= 8
+    if (ca.beta_in != nullptr)
+      hipLaunchKernelGGL((k_contract<8, EPI_GRAD, true, true>), dim3((unsigned)nwg), dim3(256), 0,
+                         s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec,
+                         (double*)nullptr);
+    else
+      hipLaunchKernelGGL((k_contract<8, EPI_GRAD, false, true>), dim3((unsigned)nwg), dim3(256),
+                         0, s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec,
+                         (double*)nullptr);
+  } else if (ca.beta_in != nullptr) {
     if (kp.d > 8) return hipErrorInvalidValue;   // two-term epilogue is instantiated for d <= 8
     hipLaunchKernelGGL((k_contract<8, EPI_GRAD, true>), dim3((unsigned)nwg), dim3(256), 0, s, kp,
                        K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);

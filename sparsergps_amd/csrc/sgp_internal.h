@@ -113,6 +113,10 @@ struct ConArgs {
   const double* cdiag = nullptr;
   int count_a2 = 0;
   double* alpha_out = nullptr;
+  // knot gradient partials (d <= 8): per 128-row tile ti and column j, sum_i G_ij K_ij t_ijc
+  // with t = scaled coordinate difference (ARD: (x_c - u_c)/l_c; sqexp/exp: x_c - u_c),
+  // written to knot_slab[(ti * mp + j) * d + c]
+  double* knot_slab = nullptr;
 };
 hipError_t launch_contract_args(const KernParams& kp, const double* K, const double* M,
                                 const double* X, int64_t ldx, int64_t n, int64_t n_pad,
@@ -219,3 +223,15 @@ hipError_t launch_lap_grad_b(int64_t n, int64_t n_pad, const double* B, const do
                              const double* y3, const double* dMt, const double* c2,
                              const double* g, double* h, double* a, double* slab, int* nblocks,
                              hipStream_t s);
+
+// knot gradients (k_mfma.hip / k_cov.hip)
+// out[j*d + c] (+)= sum over row tiles of knot_slab (deterministic two-level reduction);
+// part: 64 * mp * d doubles of work space
+hipError_t launch_knot_reduce(const double* knot_slab, int64_t ntiles, int64_t mp, int d,
+                              double* part, double* out, bool accumulate, hipStream_t s);
+// out[k*d + c] = 2 sum_l G22_kl K22_kl (u_lc - u_kc), G22 as in launch_contract_kmm
+hipError_t launch_knot_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,
+                           int64_t mp, const double* uvec, const double* Ainv,
+                           const double* Binv, const double* M3, double a, double b, double c,
+                           const double* vvec, const double* wvec, double e2, double* out,
+                           hipStream_t s);

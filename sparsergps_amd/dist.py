@@ -32,7 +32,8 @@ class HipRowBackend:
     mode "vi" (sgp_vi_*) or "fitc" (sgp_fitc_*): both are phase1 -> sum -> phase2 -> sum ->
     finish; mode "laplace" (sgp_lap_*): begin -> sum -> step -> sum -> ... -> done."""
 
-    def __init__(self, X_local, y_local, mu_local, m_max, device_index, cov_fun, mode="vi"):
+    def __init__(self, X_local, y_local, mu_local, m_max, device_index, cov_fun, mode="vi",
+                 knots=False):
         import torch
 
         from .vi import SparseGPContext
@@ -51,6 +52,10 @@ class HipRowBackend:
             n1 = n2 = self.ctx.lap_red_count(cov_fun, m_max)
         else:
             raise ValueError(mode)
+        if knots:     # knot-gradient partials ride along in the second reduction
+            self.ctx.enable_knot_grad(True)
+            n2 += self.ctx.knot_red_extra(m_max)
+        self.knots = knots
         self.red1 = torch.zeros(n1, dtype=torch.float64, device=self.dev)
         self.red2 = torch.zeros(n2, dtype=torch.float64, device=self.dev)
         # A dedicated (non-null) stream shared by libsgp's launches and torch.distributed:
@@ -74,10 +79,11 @@ class HipRowBackend:
         return buf
 
     def phase2(self, red1, n_global):
+        extra = self.ctx.knot_red_extra(self._m) if self.knots else 0
         if self.mode == "vi":
             self.ctx.vi_phase2(red1.data_ptr(), n_global, self.red2.data_ptr())
-            return self.red2
-        buf = self.red2[:self.ctx.fitc_red2_count(self.cov_fun, self._m)]
+            return self.red2[:self.ctx.vi_red2_count(self.cov_fun) + extra]
+        buf = self.red2[:self.ctx.fitc_red2_count(self.cov_fun, self._m) + extra]
         self.ctx.fitc_phase2(red1.data_ptr(), n_global, buf.data_ptr())
         return buf
 

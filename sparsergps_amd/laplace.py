@@ -18,7 +18,7 @@ from collections import OrderedDict
 import numpy as np
 
 from .covariance import theta_vector
-from .vi import _context_for, param_names
+from .vi import _context_for, _knot_outputs, knot_fun_kind, param_names
 
 
 def _prep(cov_par, cov_fun, xu, xy):
@@ -46,7 +46,7 @@ def laplace_eval(cov_par, cov_fun, xu, xy, y, mu, ff=None, m=1.0, delta=1e-6, to
     theta, names, xu_m = _prep(cov_par, cov_fun, xu, xy)
     muv = _mu_vec(mu, y)
     if ctx is None:
-        ctx = _context_for(xy, y, mu, xu_m.shape[0])
+        ctx = _context_for(xy, y, mu, xu_m.shape[0], muv)
         ctx.set_data(y, muv)
     if ff is not None:
         ctx.lap_set_f(ff)
@@ -72,11 +72,19 @@ def dlogq_dcov_par(cov_par, cov_fun, dcov_fun_dtheta=True, dcov_fun_dknot=None, 
                    transform=True, ctx=None):
     """R/laplace_approx_gradient.R:25-553 at the given ff (no NR step): {"gradient",
     "trans_par"}."""
-    if dcov_fun_dknot is not None and dcov_fun_dknot is not False:
-        raise NotImplementedError("knot gradients (xu_opt='simultaneous') are not in this build")
+    kind = knot_fun_kind(dcov_fun_dknot)
+    theta, names, xu_m = _prep(cov_par, cov_fun, xu, xy)
+    if ctx is None:
+        muv = _mu_vec(mu, y)
+        ctx = _context_for(xy, y, mu, xu_m.shape[0], muv)
+        ctx.set_data(y, muv)
+    ctx.enable_knot_grad(kind is not None)
     r = laplace_eval(cov_par, cov_fun, xu, xy, y, mu, ff, m, delta, 0.0, 0, ctx)
     grad = r["gradient"] if dcov_fun_dtheta else 0
     trans_par = OrderedDict((k, float(np.log(v))) for k, v in cov_par.items())
+    if kind is not None:
+        gk, tk = _knot_outputs(ctx, xu_m, xy, knot_opt)
+        return {"gradient": grad, "knot_gradient": gk, "trans_par": trans_par, "trans_knot": tk}
     return {"gradient": grad, "trans_par": trans_par}
 
 

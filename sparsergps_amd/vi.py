@@ -103,6 +103,7 @@ class SparseGPContext:
     # ------------------------------------------------------------------ evaluation
     def _knots(self, xu):
         U = np.asfortranarray(np.asarray(xu, dtype=np.float64).reshape(-1, self.d))
+        self._last_m = U.shape[0]
         return U, U.shape[0]
 
     def eval_vi(self, theta, cov_fun, xu, delta=1e-6, r_det=False):
@@ -130,6 +131,29 @@ class SparseGPContext:
                                      _lib.dptr(grad))
         _lib.check(st)
         return obj.value, grad
+
+    def enable_knot_grad(self, on=True):
+        """Also contract the adjoint against dK/du (knot gradients; d <= 8)."""
+        _lib.check(self._lib.sgp_ctx_enable_knot_grad(self.handle, 1 if on else 0))
+
+    def knot_red_extra(self, m):
+        return int(self._lib.sgp_knot_red_extra(self.d, int(m)))
+
+    def row_bounds(self):
+        lo = np.zeros(self.d)
+        hi = np.zeros(self.d)
+        _lib.check(self._lib.sgp_ctx_row_bounds(self.handle, _lib.dptr(lo), _lib.dptr(hi)))
+        return lo, hi
+
+    def knot_gradient(self, bounds=None):
+        """Row-major (m*d) knot gradient of the last evaluation with the reference's chain
+        factor; bounds: d x 2 [lower, upper] (None: knot_bounds of this context's rows)."""
+        m = self._last_m
+        out = np.zeros(m * self.d, dtype=np.float64)
+        b = None if bounds is None else np.asfortranarray(np.asarray(bounds, dtype=np.float64))
+        _lib.check(self._lib.sgp_knot_gradient(self.handle, None if b is None else _lib.dptr(b),
+                                               _lib.dptr(out)))
+        return out
 
     def posterior_u(self, muu):
         """Knot posterior (u_mean, u_var) of the last completed evaluation, as the drivers
@@ -258,13 +282,14 @@ class SparseGPContext:
 _CTX_CACHE = {}
 
 
-def _context_for(xy, y, mu, m):
-    """Reuse one device context per (xy, y, mu) triple, like the reference driver reuses xy."""
+def _context_for(xy, y, mu, m, mu_vec=None):
+    """Reuse one device context per (xy, y, mu) triple, like the reference driver reuses xy.
+    mu_vec: the mean actually uploaded when mu is a default marker (None)."""
     key = (id(xy), id(y), id(mu))
     ent = _CTX_CACHE.get(key)
     if ent is not None and ent[0] is xy and ent[1] is y and ent[2] is mu and ent[3].m_max >= m:
         return ent[3]
-    ctx = SparseGPContext(xy, y, mu, m_max=m)
+    ctx = SparseGPContext(xy, y, mu if mu_vec is None else mu_vec, m_max=m)
     _CTX_CACHE.clear()
     _CTX_CACHE[key] = (xy, y, mu, ctx)
     return ctx
@@ -272,6 +297,42 @@ def _context_for(xy, y, mu, m):
 
 def _mu_vec(mu, y):
     return np.broadcast_to(np.asarray(mu, dtype=np.float64), np.asarray(y).reshape(-1).shape)
+
+
+def knot_fun_kind(dcov_fun_dknot):
+    """None (knots fixed), or "sqexp" / "ard" for dsqexp_dx2 / dsqexp_dx2_ard
+    (R/covariance_function_derivatives.R:178-302): accepts those names or functions so named."""
+    if dcov_fun_dknot is None or dcov_fun_dknot is False:
+        return None
+    if isinstance(dcov_fun_dknot, float) and np.isnan(dcov_fun_dknot):
+        return None
+    name = dcov_fun_dknot if isinstance(dcov_fun_dknot, str) else getattr(dcov_fun_dknot,
+                                                                          "__name__", "")
+    if name in ("sqexp", "dsqexp_dx2"):
+        return "sqexp"
+    if name in ("ard", "dsqexp_dx2_ard"):
+        return "ard"
+    raise ValueError(f"unsupported dcov_fun_dknot {dcov_fun_dknot!r}")
+
+
+def knot_bounds(xy):
+    """vi_functions.R:175-178: column range of xy widened by a tenth on each side (d x 2)."""
+    xy = np.asarray(xy, dtype=np.float64).reshape(np.shape(xy)[0], -1)
+    lo, hi = xy.min(axis=0), xy.max(axis=0)
+    diffs = hi - lo
+    return np.column_stack([lo - diffs / 10, hi + diffs / 10])
+
+
+def _knot_outputs(ctx, xu, xy, knot_opt):
+    b = knot_bounds(xy)
+    g = ctx.knot_gradient(b)
+    U = np.asarray(xu, dtype=np.float64).reshape(-1, b.shape[0])
+    if knot_opt is not None:
+        keep = np.zeros(U.shape[0], dtype=bool)
+        keep[np.asarray(list(knot_opt), dtype=int) - 1] = True
+        g = g * np.repeat(keep, U.shape[1])
+    trans = np.log((U - b[:, 0]) + 1e-4) - np.log((b[:, 1] - U) + 1e-4)
+    return g, trans
 
 
 def vi_eval(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6, ctx=None, r_det=False):
@@ -310,14 +371,20 @@ def dlogp_dcov_par(cov_par, cov_fun, dcov_fun_dtheta=True, dcov_fun_dknot=None, 
                    xu=None, xy=None, y=None, ff=None, mu=None, transform=True, delta=1e-6,
                    ctx=None):
     """laplace_approx_gradient.R:720-971 (FITC, knots fixed): {"gradient", "trans_par"}."""
-    if dcov_fun_dknot is not None and dcov_fun_dknot is not False:
-        raise NotImplementedError("knot gradients (xu_opt='simultaneous') are not in this build")
+    kind = knot_fun_kind(dcov_fun_dknot)
     if mu is None:
         mu = np.mean(np.asarray(y, dtype=np.float64))
+    xu_m = np.asarray(xu, dtype=np.float64).reshape(-1, np.asarray(xy).reshape(len(y), -1).shape[1])
+    if ctx is None:
+        ctx = _context_for(xy, y, mu, xu_m.shape[0])
+    ctx.enable_knot_grad(kind is not None)
     _, grad = fitc_eval(cov_par, cov_fun, xu, xy, y, _mu_vec(mu, y), delta, ctx=ctx)
     if not dcov_fun_dtheta:
         grad = 0
     trans_par = OrderedDict((k, float(np.log(v))) for k, v in cov_par.items())
+    if kind is not None:
+        gk, tk = _knot_outputs(ctx, xu_m, xy, knot_opt)
+        return {"gradient": grad, "knot_gradient": gk, "trans_par": trans_par, "trans_knot": tk}
     return {"gradient": grad, "trans_par": trans_par}
 
 
@@ -330,12 +397,18 @@ def delbo_dcov_par(cov_par, cov_fun, dcov_fun_dtheta=True, dcov_fun_dknot=None, 
                    xu=None, xy=None, y=None, ff=None, mu=None, transform=True, delta=1e-6,
                    ctx=None):
     """vi_functions.R:126-602 with knots fixed: {"gradient", "trans_par"} like the reference."""
-    if dcov_fun_dknot is not None and dcov_fun_dknot is not False:
-        raise NotImplementedError("knot gradients (xu_opt='simultaneous') are not in this build")
+    kind = knot_fun_kind(dcov_fun_dknot)
     if mu is None:
         mu = np.mean(np.asarray(y, dtype=np.float64))                   # quirk Q14
+    xu_m = np.asarray(xu, dtype=np.float64).reshape(-1, np.asarray(xy).reshape(len(y), -1).shape[1])
+    if ctx is None:
+        ctx = _context_for(xy, y, mu, xu_m.shape[0])
+    ctx.enable_knot_grad(kind is not None)
     _, grad = vi_eval(cov_par, cov_fun, xu, xy, y, _mu_vec(mu, y), delta, ctx=ctx)
     if not dcov_fun_dtheta:
         grad = 0
     trans_par = OrderedDict((k, float(np.log(v))) for k, v in cov_par.items())
+    if kind is not None:
+        gk, tk = _knot_outputs(ctx, xu_m, xy, knot_opt)
+        return {"gradient": grad, "knot_gradient": gk, "trans_par": trans_par, "trans_knot": tk}
     return {"gradient": grad, "trans_par": trans_par}

@@ -104,3 +104,41 @@ def test_laplace_two_ranks_one_gpu_gloo():
     rel_obj, rel_grad, it, it_ref = q.get(timeout=5)
     assert it == it_ref
     assert rel_obj < 1e-9 and rel_grad < 1e-7
+
+
+def _knot_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import sgp_oracle as O
+        from sparsergps_amd.dist import HipRowBackend, RowShardedVI, shard_rows
+        n, m = 151, 7
+        P = O.make_gaussian_problem("C2", n=n, m=m)
+        s0, s1 = shard_rows(n, world, rank)
+        be = HipRowBackend(P["X"][s0:s1], P["y"][s0:s1], P["mu"][s0:s1], m, 0, "sqexp", "vi",
+                           knots=True)
+        theta = np.array(list(P["cov_par"].values()))
+        RowShardedVI(be, n).eval(theta, P["U"], P["delta"])
+        g = be.ctx.knot_gradient(O.knot_bounds_of(P["X"]))      # global bounds
+        be.close()
+        if rank == 0:
+            ref = O.delbo_dcov_par(P["cov_par"], "sqexp", P["U"], P["X"], P["y"], P["mu"],
+                                   P["delta"], dcov_fun_dknot="sqexp")["knot_gradient"]
+            q.put(float(np.max(np.abs(g - ref) / np.maximum(1, np.abs(ref)))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_knot_gradient_two_ranks_one_gpu_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_knot_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    assert q.get(timeout=5) < 1e-7
