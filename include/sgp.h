@@ -208,6 +208,15 @@ int64_t sgp_knot_red_extra(int d, int64_t m);
 int sgp_knot_gradient(sgp_ctx* ctx, const double* bounds, double* grad_knot);
 int sgp_ctx_row_bounds(sgp_ctx* ctx, double* col_min, double* col_max);
 
+/* OAT knot proposal scoring (VI): the ELBO at knots [U; cand_t] for each of T candidate knots
+ * (cand: T x d, column-major, ld ldc) at fixed theta -- the meta-model y values of
+ * knot_prop_random_norm_vi / knot_prop_ego_norm_vi (R/vi_functions.R:2196-2300, 1584-) --
+ * from bordered Schur complements instead of T rebuilds of K12.  NaN marks a candidate whose
+ * bordered K22 or Bm is not positive definite (the reference's try-error). */
+int sgp_vi_candidates(sgp_ctx* ctx, int kernel, const double* theta, const double* U, int64_t m,
+                      int64_t ldu, double delta, unsigned flags, const double* cand, int64_t T,
+                      int64_t ldc, double* obj_out);
+
 /* Per-kernel timing of the last evaluation (HIP events on the launch stream).
  * names: '\n'-separated kernel-phase names; ms: their durations (max n entries). */
 int sgp_ctx_enable_timing(sgp_ctx* ctx, int enable);

@@ -80,6 +80,9 @@ PROTOTYPES = {
     "sgp_knot_red_extra": (C.c_int64, [C.c_int, C.c_int64]),
     "sgp_knot_gradient": (C.c_int, [C.c_void_p, c_double_p, c_double_p]),
     "sgp_ctx_row_bounds": (C.c_int, [C.c_void_p, c_double_p, c_double_p]),
+    "sgp_vi_candidates": (C.c_int, [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_int64,
+                                    C.c_int64, C.c_double, C.c_uint, c_double_p, C.c_int64,
+                                    C.c_int64, c_double_p]),
     "sgp_ctx_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "sgp_ctx_timings": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64, c_double_p, C.c_int, c_int_p]),
 }

@@ -1672,4 +1672,119 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
   return SGP_OK;
 }
 
+
+// ------------------------------------------------------------------------- OAT candidates
+// ELBO of the knot sets [U; x*_t] for T candidate knots at fixed theta, as the meta-model
+// y values of knot_prop_random_norm_vi / knot_prop_ego_norm_vi (R/vi_functions.R:2196-2300)
+// compute them -- but without rebuilding K12 per candidate: a candidate borders K22, S and
+// Bm by one row/column, so its ELBO follows from the base evaluation plus Schur complements
+// (DESIGN.md sec. 3.5).  Work per 128 candidates: one K(X, x*) build and one n x m x 128 TN
+// GEMM (K^T Kc) instead of 128 SYRKs.
+int sgp_vi_candidates(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
+                      int64_t ldu, double delta, unsigned flags, const double* cand, int64_t T,
+                      int64_t ldc, double* obj_out) {
+  if (!c || !cand || T < 1 || ldc < T || !obj_out) {
+    set_err("invalid sgp_vi_candidates arguments");
+    return SGP_EINVAL;
+  }
+  int st = sgp_vi_phase1(c, kernel, theta, U, m, ldu, delta, c->red1);
+  if (st) return st;
+  const KernParams& kp = c->kp;
+  const int64_t mp = c->mp, mm = mp * mp, n_pad = c->n_pad, d = kp.d;
+  const double z = kp.tau2 + delta;
+  const double* S = c->red1;
+  const double* t = c->red1 + mm;
+  st = bm_stage(c, S, 1.0 / z);
+  if (st) return st;
+  {
+    Scope tm(c, "mm_vectors");
+    HIPCHK(dense_gemv(c->Binv, mp, t, 1.0 / z, c->uvec, c->stream));
+    HIPCHK(launch_dot(t, c->uvec, mp, c->slab_small, c->sc + SC_TU, c->stream));
+    HIPCHK(launch_dot(c->K22inv, S, mm, c->slab_small, c->sc + SC_TRKS, c->stream));
+    HIPCHK(hipMemcpyAsync(c->sc + SC_RR, c->red1 + mm + mp, sizeof(double),
+                          hipMemcpyDeviceToDevice, c->stream));
+  }
+  constexpr int64_t TP = 128;
+  DevBuf Kc, slab, P, part, rk, cc, Uc, K22c, W, SW, Bt, BB, base, out;
+  const int64_t slab_cap = gemm_tn_slab_doubles(n_pad, mp, TP);
+  const int64_t part_cap = lap_gemv_cols_slab(n_pad, TP, 1);
+  st = dalloc(&Kc.p, n_pad * TP);
+  st = st ? st : dalloc(&slab.p, slab_cap);
+  st = st ? st : dalloc(&P.p, mp * TP);
+  st = st ? st : dalloc(&part.p, part_cap);
+  st = st ? st : dalloc(&rk.p, TP);
+  st = st ? st : dalloc(&cc.p, TP);
+  st = st ? st : dalloc(&Uc.p, TP * d);
+  st = st ? st : dalloc(&K22c.p, mp * TP);
+  st = st ? st : dalloc(&W.p, mp * TP);
+  st = st ? st : dalloc(&SW.p, mp * TP);
+  st = st ? st : dalloc(&Bt.p, mp * TP);
+  st = st ? st : dalloc(&BB.p, mp * TP);
+  st = st ? st : dalloc(&base.p, 2);
+  st = st ? st : dalloc(&out.p, TP * 4);
+  if (st) return st;
+  // Sigma22' diagonal entry of the new knot: make_cov (sigma^2 + tau^2 + delta) - tau^2
+  const double kxx = ((kp.sig2 + kp.tau2) + delta) - kp.tau2;
+  const double hb[2] = {kxx, z};
+  HIPCHK(hipMemcpyAsync(base.p, hb, sizeof(hb), hipMemcpyHostToDevice, c->stream));
+  double sc[SC_N];
+  int status[4];
+  HIPCHK(hipMemcpyAsync(sc, c->sc, sizeof(sc), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(status, c->status, sizeof(status), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->phase = 0;
+  if (status[0] || status[1]) {
+    set_err("chol(): the leading minor of order %d of %s is not positive definite",
+            status[0] ? status[0] : status[1],
+            status[0] ? "Sigma22" : "Sigma22 + t(Sigma12) %*% ZSig12");
+    return SGP_ENOTPD;
+  }
+  const double n = (double)c->n;
+  const double ld22 = 2.0 * sc[SC_LD22], ldB = 2.0 * sc[SC_LDB];
+  const double quad = -0.5 * sc[SC_RR] / z + 0.5 * sc[SC_TU] / z;   // u = Bm^-1 t / z
+  const double trKS = sc[SC_TRKS];
+  std::vector<double> hU((size_t)(TP * d)), ho((size_t)(TP * 4));
+  for (int64_t t0 = 0; t0 < T; t0 += TP) {
+    const int64_t tc = (T - t0 < TP) ? T - t0 : TP;
+    std::fill(hU.begin(), hU.end(), 0.0);
+    for (int q = 0; q < d; ++q)
+      for (int64_t j = 0; j < tc; ++j) hU[(size_t)(q * TP + j)] = cand[(t0 + j) + q * ldc];
+    HIPCHK(hipMemcpyAsync(Uc.p, hU.data(), sizeof(double) * hU.size(), hipMemcpyHostToDevice,
+                          c->stream));
+    Scope tm(c, "candidates");
+    HIPCHK(launch_build_knm(kp, c->X, n_pad, c->n, n_pad, Uc.p, TP, tc, TP, Kc.p, c->stream));
+    HIPCHK(launch_gemm_tn(c->K, mp, mp, Kc.p, TP, TP, n_pad, slab.p, slab_cap, P.p, c->stream));
+    HIPCHK(launch_gemv_cols(Kc.p, n_pad, TP, c->r, n_pad, 1, part.p, part_cap, rk.p, c->stream));
+    HIPCHK(launch_colnorm2(Kc.p, n_pad, TP, part.p, part_cap, cc.p, c->stream));
+    HIPCHK(launch_build_knm(kp, c->U, mp, m, mp, Uc.p, TP, tc, TP, K22c.p, c->stream));
+    HIPCHK(launch_gemm64(false, false, false, mp, TP, mp, 1.0, c->K22inv, mp, K22c.p, TP, 0.0,
+                         W.p, TP, c->stream));
+    HIPCHK(launch_gemm64(false, false, false, mp, TP, mp, 1.0, S, mp, W.p, TP, 0.0, SW.p, TP,
+                         c->stream));
+    HIPCHK(dense_axpby(1.0, K22c.p, 1.0 / z, P.p, Bt.p, mp * TP, c->stream));
+    HIPCHK(launch_gemm64(false, false, false, mp, TP, mp, 1.0, c->Binv, mp, Bt.p, TP, 0.0, BB.p,
+                         TP, c->stream));
+    HIPCHK(launch_vi_cand_scalars(m, mp, tc, TP, K22c.p, W.p, SW.p, P.p, Bt.p, BB.p, c->uvec,
+                                  rk.p, cc.p, base.p, out.p, c->stream));
+    HIPCHK(hipMemcpyAsync(ho.data(), out.p, sizeof(double) * tc * 4, hipMemcpyDeviceToHost,
+                          c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int64_t j = 0; j < tc; ++j) {
+      const double sK = ho[(size_t)(j * 4)], sB = ho[(size_t)(j * 4 + 1)];
+      const double dq = ho[(size_t)(j * 4 + 2)], trinc = ho[(size_t)(j * 4 + 3)];
+      if (!(sK > 0.0) || !(sB > 0.0)) {   // the reference's chol() would fail (try-error)
+        obj_out[t0 + j] = NAN;
+        continue;
+      }
+      const double ld22c = ld22 + log(sK), ldBc = ldB + log(sB);
+      const double logdet22 = (flags & SGP_FLAG_R_DET) ? log(exp(ld22c)) : ld22c;
+      const double qd = quad + 0.5 * dq * dq / (z * z * sB);
+      const double det_part = -0.5 * (n * log(z) - logdet22 + ldBc);
+      const double tt = -(1.0 / (2.0 * kp.tau2)) * (n * (kp.sig2 + delta) - (trKS + trinc / sK));
+      obj_out[t0 + j] = qd + det_part - (n / 2.0) * log(2.0 * M_PI) + tt;
+    }
+  }
+  return SGP_OK;
+}
+
 }  // extern "C"

@@ -285,6 +285,69 @@ __global__ void __launch_bounds__(128) k_gemv_cols(const double* __restrict__ K,
   for (int v = 0; v < NV; ++v) o[v * mp] = acc[v];
 }
 
+// part[ch][j] = sum_{i in chunk ch} K_ij^2
+__global__ void __launch_bounds__(128) k_colnorm2(const double* __restrict__ K, int64_t n_pad,
+                                                  int64_t mp, int64_t chunk,
+                                                  double* __restrict__ part) {
+  const int64_t j = (int64_t)blockIdx.x * 128 + threadIdx.x;
+  const int64_t ch = blockIdx.y;
+  const int64_t i0 = ch * chunk;
+  const int64_t i1 = (i0 + chunk < n_pad) ? i0 + chunk : n_pad;
+  double acc = 0.0;
+  for (int64_t i = i0; i < i1; ++i) {
+    const double k = K[i * mp + j];
+    acc = fma(k, k, acc);
+  }
+  part[ch * mp + j] = acc;
+}
+
+// Bordered-system scalars of one candidate knot t (VI):
+//   s_K = kxx - k22c^T K22^-1 k22c,  s_B = kxx + c/z - b^T Bm^-1 b  (b = k22c + P/z),
+//   dq = k_c^T r - z b^T u,  trinc = w^T S w - 2 w^T p + c  (w = K22^-1 k22c, p = K^T k_c)
+// out[t] = {s_K, s_B, dq, trinc}; base = {kxx, z}.  One block per candidate.
+__global__ void __launch_bounds__(256) k_vi_cand_scalars(int64_t m, int64_t Tp,
+                                                         const double* __restrict__ K22c,
+                                                         const double* __restrict__ W,
+                                                         const double* __restrict__ SW,
+                                                         const double* __restrict__ P,
+                                                         const double* __restrict__ Bt,
+                                                         const double* __restrict__ BB,
+                                                         const double* __restrict__ u,
+                                                         const double* __restrict__ rk,
+                                                         const double* __restrict__ cc,
+                                                         const double* __restrict__ base,
+                                                         double* __restrict__ out) {
+  const int64_t t = blockIdx.x;
+  double a[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int64_t j = threadIdx.x; j < m; j += 256) {
+    const int64_t o = j * Tp + t;
+    const double w = W[o], b = Bt[o];
+    a[0] = fma(K22c[o], w, a[0]);
+    a[1] = fma(w, SW[o], a[1]);
+    a[2] = fma(w, P[o], a[2]);
+    a[3] = fma(b, BB[o], a[3]);
+    a[4] = fma(b, u[j], a[4]);
+  }
+  __shared__ double sh[4][5];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const double v = wave_sum(a[k]);
+    if (lane == 0) sh[wv][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double r[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) r[k] = sh[0][k] + sh[1][k] + sh[2][k] + sh[3][k];
+    const double kxx = base[0], z = base[1], c = cc[t];
+    out[t * 4 + 0] = kxx - r[0];
+    out[t * 4 + 1] = (kxx + c / z) - r[3];
+    out[t * 4 + 2] = rk[t] - z * r[4];
+    out[t * 4 + 3] = r[1] - 2.0 * r[2] + c;
+  }
+}
+
 constexpr int LAP_NB = 1024;   // blocks of the per-row kernels (slab rows)
 
 int row_blocks(int64_t n_pad) {
@@ -385,5 +448,28 @@ hipError_t launch_lap_grad_b(int64_t n, int64_t n_pad, const double* B, const do
   *nblocks = nb;
   hipLaunchKernelGGL(k_lap_grad_b, dim3(nb), dim3(256), 0, s, n, n_pad, B, sv, y3, dMt, c2, g, h,
                      a, slab);
+  return hipGetLastError();
+}
+
+hipError_t launch_colnorm2(const double* K, int64_t n_pad, int64_t mp, double* part,
+                           int64_t part_cap, double* out, hipStream_t s) {
+  const int64_t nch = lap_gemv_cols_chunks(n_pad, mp);
+  if (nch * mp > part_cap) return hipErrorInvalidValue;
+  const int64_t chunk = (n_pad + nch - 1) / nch;
+  hipLaunchKernelGGL(k_colnorm2, dim3((unsigned)(mp / 128), (unsigned)nch), dim3(128), 0, s, K,
+                     n_pad, mp, chunk, part);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_colsum(part, nch, mp, out, s);
+}
+
+hipError_t launch_vi_cand_scalars(int64_t m, int64_t mp, int64_t T, int64_t Tp,
+                                  const double* K22c, const double* W, const double* SW,
+                                  const double* P, const double* Bt, const double* BB,
+                                  const double* u, const double* rk, const double* cc,
+                                  const double* base, double* out, hipStream_t s) {
+  (void)mp;
+  hipLaunchKernelGGL(k_vi_cand_scalars, dim3((unsigned)T), dim3(256), 0, s, m, Tp, K22c, W, SW, P,
+                     Bt, BB, u, rk, cc, base, out);
   return hipGetLastError();
 }

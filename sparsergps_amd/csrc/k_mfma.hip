@@ -173,6 +173,107 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
   if (diag && ta == 0 && tid == 255) slab_rr[split] = rr_acc;
 }
 
+// ============================================================================ TN GEMM
+// C = A^T B over n rows (A: n_pad x ma, B: n_pad x mb, both row-major; ma, mb multiples of
+// 128): split-K over row chunks like k_syrk, one 128x128 tile per workgroup, deterministic
+// slabs [split][tile][128 x 128].  grid = splits * (ma/128) * (mb/128).
+__global__ void __launch_bounds__(256, 2)
+k_gemm_tn(const double* __restrict__ A, int64_t lda, const double* __restrict__ B, int64_t ldb,
+          int64_t n_pad, int nta, int ntb, int64_t chunk, double* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
+  __shared__ __attribute__((aligned(16))) double Kb[2][BK * SB];
+  const int64_t nwg = (int64_t)gridDim.x;
+  const int64_t wgid = xcd_remap(blockIdx.x, nwg);
+  const int ntile = nta * ntb;
+  const int split = (int)(wgid / ntile);
+  const int tile = (int)(wgid % ntile);
+  const int ta = tile / ntb, tb = tile % ntb;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int64_t rbeg = (int64_t)split * chunk;
+  int64_t rend = rbeg + chunk;
+  if (rend > n_pad) rend = n_pad;
+  const int nsteps = (int)((rend - rbeg) / BK);
+  d4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+  const int lrow = tid >> 4, lcol = (tid & 15) * 8;
+  const double2* gA = reinterpret_cast<const double2*>(A + (rbeg + lrow) * lda + ta * (int64_t)T128 + lcol);
+  const double2* gB = reinterpret_cast<const double2*>(B + (rbeg + lrow) * ldb + tb * (int64_t)T128 + lcol);
+  const int64_t sa = BK * lda / 2, sb = BK * ldb / 2;
+  double2 va0, va1, va2, va3, vb0, vb1, vb2, vb3;
+#define TN_GLOAD(step)                                                          \
+  {                                                                             \
+    const int64_t oa_ = (int64_t)(step) * sa, ob_ = (int64_t)(step) * sb;       \
+    va0 = gA[oa_]; va1 = gA[oa_ + 1]; va2 = gA[oa_ + 2]; va3 = gA[oa_ + 3];     \
+    vb0 = gB[ob_]; vb1 = gB[ob_ + 1]; vb2 = gB[ob_ + 2]; vb3 = gB[ob_ + 3];     \
+  }
+#define TN_SSTORE(buf)                                                          \
+  {                                                                             \
+    double2* pa_ = reinterpret_cast<double2*>(&Ka[buf][lrow * SB + lcol]);      \
+    double2* pb_ = reinterpret_cast<double2*>(&Kb[buf][lrow * SB + lcol]);      \
+    pa_[0] = va0; pa_[1] = va1; pa_[2] = va2; pa_[3] = va3;                     \
+    pb_[0] = vb0; pb_[1] = vb1; pb_[2] = vb2; pb_[3] = vb3;                     \
+  }
+  if (nsteps > 0) {
+    TN_GLOAD(0);
+    TN_SSTORE(0);
+  }
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
+    if (step + 1 < nsteps) TN_GLOAD(step + 1);
+    const double* As = Ka[cur];
+    const double* Bs = Kb[cur];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int krow = kk * 4 + (lane >> 4);
+      double af[4], bf[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        af[f] = As[krow * SB + wr * 64 + f * 16 + (lane & 15)];
+        bf[f] = Bs[krow * SB + wc * 64 + f * 16 + (lane & 15)];
+      }
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
+    }
+    if (step + 1 < nsteps) TN_SSTORE(cur ^ 1);
+    __syncthreads();
+  }
+#undef TN_GLOAD
+#undef TN_SSTORE
+  double* out = slab + ((int64_t)split * ntile + tile) * (T128 * T128);
+#pragma unroll
+  for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
+        const int col = wc * 64 + fn * 16 + (lane & 15);
+        out[row * T128 + col] = acc[fm][fn][q];
+      }
+}
+
+// C[a][b] (row-major, ld = ntb*128) = sum over splits of the tile slabs
+__global__ void __launch_bounds__(256)
+k_gemm_tn_reduce(const double* __restrict__ slab, int splits, int nta, int ntb,
+                 double* __restrict__ C) {
+  const int tile = blockIdx.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int ntile = nta * ntb;
+  double s = 0.0;
+  for (int sp = 0; sp < splits; ++sp) s += slab[((int64_t)sp * ntile + tile) * (T128 * T128) + e];
+  const int ta = tile / ntb, tb = tile % ntb;
+  const int64_t a = (int64_t)ta * T128 + e / T128, b = (int64_t)tb * T128 + e % T128;
+  C[a * (int64_t)ntb * T128 + b] = s;
+}
+
 // S (mp x mp full) from the per-split lower tiles; red = [S, t, rr]
 __global__ void __launch_bounds__(256)
 k_syrk_reduce(const double* __restrict__ slab_s, int splits, int T, int64_t mp,
@@ -650,6 +751,35 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
     hipLaunchKernelGGL(k_syrk_reduce_t, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s,
                        slab_t, slab_rr, p.splits, p.nb, mp, red);
   }
+  return hipGetLastError();
+}
+
+int64_t gemm_tn_splits(int64_t n_pad, int ntile) {
+  constexpr int64_t kSlots = 512;
+  int64_t sp = kSlots / ntile;
+  if (sp < 1) sp = 1;
+  const int64_t max_splits = n_pad / BK > 0 ? n_pad / BK : 1;
+  return sp > max_splits ? max_splits : sp;
+}
+
+int64_t gemm_tn_slab_doubles(int64_t n_pad, int64_t ma, int64_t mb) {
+  const int ntile = (int)((ma / T128) * (mb / T128));
+  return gemm_tn_splits(n_pad, ntile) * ntile * T128 * T128;
+}
+
+hipError_t launch_gemm_tn(const double* A, int64_t lda, int64_t ma, const double* B, int64_t ldb,
+                          int64_t mb, int64_t n_pad, double* slab, int64_t slab_cap, double* C,
+                          hipStream_t s) {
+  const int nta = (int)(ma / T128), ntb = (int)(mb / T128), ntile = nta * ntb;
+  int64_t splits = gemm_tn_splits(n_pad, ntile);
+  int64_t chunk = (n_pad + splits - 1) / splits;
+  chunk = (chunk + BK - 1) / BK * BK;
+  splits = (n_pad + chunk - 1) / chunk;
+  if (splits * ntile * T128 * T128 > slab_cap) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_gemm_tn, dim3((unsigned)(splits * ntile)), dim3(256), 0, s, A, lda, B, ldb,
+                     n_pad, nta, ntb, chunk, slab);
+  hipLaunchKernelGGL(k_gemm_tn_reduce, dim3(T128 * T128 / 256, ntile), dim3(256), 0, s, slab,
+                     (int)splits, nta, ntb, C);
   return hipGetLastError();
 }
 

@@ -235,3 +235,20 @@ hipError_t launch_knot_kmm(const KernParams& kp, const double* U, int64_t ldu, i
                            const double* Binv, const double* M3, double a, double b, double c,
                            const double* vvec, const double* wvec, double e2, double* out,
                            hipStream_t s);
+
+// C = A^T B over n_pad rows (A: n_pad x ma, ld lda; B: n_pad x mb, ld ldb; ma, mb multiples of
+// 128), f64 MFMA split-K; C row-major ma x mb.  slab: gemm_tn_slab_doubles(n_pad, ma, mb).
+int64_t gemm_tn_slab_doubles(int64_t n_pad, int64_t ma, int64_t mb);
+hipError_t launch_gemm_tn(const double* A, int64_t lda, int64_t ma, const double* B, int64_t ldb,
+                          int64_t mb, int64_t n_pad, double* slab, int64_t slab_cap, double* C,
+                          hipStream_t s);
+// candidate knots (VI, k_lap.hip): per column t < T of the mp x Tp row-major blocks, the
+// bordered-system scalars -> obj[t] (NaN when a Schur complement is not positive)
+hipError_t launch_vi_cand_scalars(int64_t m, int64_t mp, int64_t T, int64_t Tp,
+                                  const double* K22c, const double* W, const double* SW,
+                                  const double* P, const double* Bt, const double* BB,
+                                  const double* u, const double* rk, const double* cc,
+                                  const double* base, double* out, hipStream_t s);
+// column sums of squares: out[j] = sum_i K_ij^2 (deterministic two-level, part as gemv_cols)
+hipError_t launch_colnorm2(const double* K, int64_t n_pad, int64_t mp, double* part,
+                           int64_t part_cap, double* out, hipStream_t s);

@@ -203,6 +203,19 @@ class SparseGPContext:
                                               _lib.dptr(grad), C.byref(it)))
         return obj.value, grad, it.value
 
+    def vi_candidates(self, theta, cov_fun, xu, cand, delta=1e-6, r_det=False):
+        """ELBO at knots [xu; cand[t]] for every candidate row t (OAT proposal scoring)."""
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        U, m = self._knots(xu)
+        Cd = np.asfortranarray(np.asarray(cand, dtype=np.float64).reshape(-1, self.d))
+        T = Cd.shape[0]
+        out = np.zeros(T, dtype=np.float64)
+        _lib.check(self._lib.sgp_vi_candidates(self.handle, _lib.KERNELS[cov_fun], _lib.dptr(theta),
+                                               _lib.dptr(U), m, m, float(delta),
+                                               _lib.SGP_FLAG_R_DET if r_det else 0,
+                                               _lib.dptr(Cd), T, T, _lib.dptr(out)))
+        return out
+
     def lap_red_count(self, cov_fun, m):
         return int(self._lib.sgp_lap_red_count(_lib.KERNELS[cov_fun], self.d, int(m)))
 

@@ -430,3 +430,41 @@ def eval_laplace(kernel, theta, X, y, mu, U, f0, expo=1.0, delta=1e-6, tol=1e-5,
         red, done, res = rk.step(red)
         if done:
             return res[0], res[1], rk.f, len(rk.objs)
+
+
+# ------------------------------------------------------------------------------ OAT candidates
+def vi_candidates(kernel, theta, X, y, mu, U, cand, delta=1e-6):
+    """ELBO at [U; cand_t] from the base system by bordering (mirrors sgp_vi_candidates)."""
+    X, U = np.asarray(X, dtype=np.float64), np.asarray(U, dtype=np.float64)
+    n, d = X.shape
+    m = U.shape[0]
+    L, sigma, tau, ls = _params(kernel, theta, d)
+    z = tau ** 2 + delta
+    K, _ = _kmat(kernel, X, U, sigma, ls)
+    Kuu, _ = _kmat(kernel, U, U, sigma, ls)
+    K22 = Kuu.copy()
+    K22[np.diag_indices(m)] = ((np.diag(Kuu) + tau ** 2) + delta) - tau ** 2
+    r = np.asarray(y) - np.asarray(mu)
+    S, t, rr = K.T @ K, K.T @ r, r @ r
+    Bm = K22 + S / z
+    Binv, K22inv = np.linalg.inv(Bm), np.linalg.inv(K22)
+    u = Binv @ t / z
+    quad = -0.5 * rr / z + 0.5 * t @ u / z
+    ld22, ldB = np.linalg.slogdet(K22)[1], np.linalg.slogdet(Bm)[1]
+    trKS = np.sum(K22inv * S)
+    kxx = ((sigma ** 2 + tau ** 2) + delta) - tau ** 2
+    out = []
+    for xs in np.asarray(cand, dtype=np.float64).reshape(-1, d):
+        kc = _kmat(kernel, X, xs[None, :], sigma, ls)[0][:, 0]
+        k22c = _kmat(kernel, U, xs[None, :], sigma, ls)[0][:, 0]
+        p, c, w = K.T @ kc, kc @ kc, K22inv @ k22c
+        sK = kxx - k22c @ w
+        b = k22c + p / z
+        sB = (kxx + c / z) - b @ Binv @ b
+        dq = kc @ r - z * (b @ u)
+        trinc = w @ S @ w - 2 * w @ p + c
+        out.append(quad + 0.5 * dq * dq / (z * z * sB)
+                   - 0.5 * (n * math.log(z) - (ld22 + math.log(sK)) + (ldB + math.log(sB)))
+                   - n / 2 * math.log(2 * math.pi)
+                   - (1 / (2 * tau ** 2)) * (n * (sigma ** 2 + delta) - (trKS + trinc / sK)))
+    return np.array(out)

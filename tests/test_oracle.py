@@ -237,3 +237,17 @@ def test_laplace_adjoint_model_matches_oracle(cov_fun, coinc):
     assert it == len(nr["objective_function_values"])
     assert abs(o - nr["objective_function_values"][-1]) < 1e-10 * abs(o)
     assert np.max(np.abs(grad - g) / np.maximum(1, np.abs(g))) < 1e-10
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_vi_candidate_bordering_matches_rebuild(cfg):
+    """The bordered-system ELBO (knot proposals) equals rebuilding the whole
+    ELBO with the candidate appended, as knot_prop_random_norm_vi does."""
+    P = O.make_gaussian_problem(cfg, n=150, m=9)
+    cand = P["X"][[3, 50, 99]]
+    th = np.array(list(P["cov_par"].values()))
+    got = A.vi_candidates(P["cov_fun"], th, P["X"], P["y"], P["mu"], P["U"], cand, P["delta"])
+    for k in range(3):
+        ref = O.elbo_eval(P["cov_par"], P["cov_fun"], np.vstack([P["U"], cand[k]]), P["X"],
+                          P["y"], P["mu"], P["delta"])
+        assert abs(got[k] - ref) < 1e-10 * abs(ref)
