@@ -1027,11 +1027,10 @@ int sgp_fitc_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned f
     // the SYRK reduce wrote rr_omega at mm + mp; keep sum(omega) at mm + mp + 1
   }
   const int64_t off = fitc_rec_off(mp);
-  int64_t nrec = 0, nwg = 0;
+  const int64_t nrec = kp.L + 5;
+  double* kout = red2 + off + 2 * nrec;
   {
     Scope tm(c, "contract_knm");
-    nrec = kp.L + 5;
-    double* kout = red2 + off + 2 * nrec;
     // pass 1: G1 = alpha u^T - diag(1/Z) K Bm^-1
     ConArgs a1;
     a1.r = c->r;
@@ -1041,6 +1040,9 @@ int sgp_fitc_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned f
     a1.rs = -1.0;
     st = contract_pass(c, c->Binv, a1, red2 + off, kout, false);
     if (st) return st;
+  }
+  {
+    Scope tm(c, "contract_knm_b");
     // pass 2: G2 = -diag(omega) K K22^-1
     ConArgs a2;
     a2.rs_vec = c->omega;

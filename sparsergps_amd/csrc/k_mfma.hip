@@ -55,6 +55,7 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
   __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
   __shared__ __attribute__((aligned(16))) double Kb[2][BK * SB];
   __shared__ double rw[2][BK];
+  __shared__ double rv[2][BK];
   __shared__ double rr_acc;
 
   const int64_t nwg = (int64_t)gridDim.x;
@@ -86,7 +87,7 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
   const double2* gB = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + tb * (int64_t)T128 + lcol);
   const int64_t gstep = BK * mp / 2;   // double2 stride of one k-step
   double2 va0, va1, va2, va3, vb0, vb1, vb2, vb3;
-  double vr = 0.0, wi = 1.0;
+  double vr = 0.0, wi = 1.0, vrr = 0.0;
   double tacc = 0.0;  // t partial for column (tid) when diag
   if (tid == 0) rr_acc = 0.0;
 
@@ -99,6 +100,7 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
     if (tid < BK) {                                                             \
       const int64_t rr_ = rbeg + (int64_t)(step) * BK + tid;                    \
       const double rv_ = r[rr_];                                                \
+      vrr = rv_;                                                                \
       vr = (tv != nullptr) ? tv[rr_] : ((w != nullptr) ? w[rr_] * rv_ : rv_);   \
     }                                                                           \
   }
@@ -111,7 +113,7 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
     pa_[2] = make_double2(va2.x * wi, va2.y * wi);                              \
     pa_[3] = make_double2(va3.x * wi, va3.y * wi);                              \
     pb_[0] = vb0; pb_[1] = vb1; pb_[2] = vb2; pb_[3] = vb3;                     \
-    if (tid < BK) rw[buf][tid] = vr;                                            \
+    if (tid < BK) { rw[buf][tid] = vr; rv[buf][tid] = vrr; }                    \
   }
 
   if (nsteps > 0) {
@@ -146,10 +148,7 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
     }
     if (diag && ta == 0 && tid == 255) {
       double s = 0.0;
-      for (int q = 0; q < BK; ++q) {
-        const int64_t rr = rbeg + (int64_t)step * BK + q;
-        s += rw[cur][q] * r[rr];
-      }
+      for (int q = 0; q < BK; ++q) s += rw[cur][q] * rv[cur][q];
       rr_acc += s;
     }
     if (step + 1 < nsteps) SYRK_SSTORE(cur ^ 1);
@@ -334,6 +333,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   constexpr int B_SZ = BK * SB;     // 2304
   __shared__ __attribute__((aligned(16))) double lds[2 * (A_SZ + B_SZ)];
   __shared__ double red[4][SGP_MAXD + 4];
+  __shared__ double s_uk[2][BK];   // u slice of the staged k-step (fused alpha)
 
   const int64_t ntj = mp / T128;
   const int64_t nwg = (n_pad / T128) * ntj;
@@ -362,14 +362,17 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   double2 va0, va1, va2, va3, vb0, vb1, vb2, vb3;
   const int nsteps = (int)(mp / BK);
   // alpha folded into the k-loop: each thread dots the 8 K values it stages with u.
-  const double2* gU = reinterpret_cast<const double2*>((with_u ? uvec : M) + acol);
-  double ku = 0.0;
+  double ku = 0.0, vuk = 0.0;
 
+  // The alpha dot products K_i . u ride on the A stream: 16 threads fetch the step's u slice
+  // with the operands, it is staged in LDS with them, and each thread folds its 8 staged K
+  // values in at the top of the next step (no global load waited on inside the loop).
 #define CON_GLOAD(step)                                                          \
   {                                                                              \
     const int64_t oa_ = (int64_t)(step) * (BK / 2), ob_ = (int64_t)(step) * bstep; \
     va0 = gA[oa_]; va1 = gA[oa_ + 1]; va2 = gA[oa_ + 2]; va3 = gA[oa_ + 3];      \
     vb0 = gB[ob_]; vb1 = gB[ob_ + 1]; vb2 = gB[ob_ + 2]; vb3 = gB[ob_ + 3];      \
+    if (with_u && tid < BK) vuk = uvec[(int64_t)(step) * BK + tid];              \
   }
 #define CON_SSTORE(buf)                                                          \
   {                                                                              \
@@ -378,23 +381,23 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     double2* pb_ = reinterpret_cast<double2*>(&As_[A_SZ + bk * SB + bcol]);      \
     pa_[0] = va0; pa_[1] = va1; pa_[2] = va2; pa_[3] = va3;                      \
     pb_[0] = vb0; pb_[1] = vb1; pb_[2] = vb2; pb_[3] = vb3;                      \
+    if (with_u && tid < BK) s_uk[buf][tid] = vuk;                                \
   }
-#define CON_KU(step)                                                             \
+#define CON_KU(buf)                                                              \
   if (with_u) {                                                                  \
-    const double2* ur_ = gU + (int64_t)(step) * (BK / 2);                        \
-    const double2 u0 = ur_[0], u1 = ur_[1], u2 = ur_[2], u3 = ur_[3];            \
-    ku = fma(va0.x, u0.x, ku); ku = fma(va0.y, u0.y, ku);                        \
-    ku = fma(va1.x, u1.x, ku); ku = fma(va1.y, u1.y, ku);                        \
-    ku = fma(va2.x, u2.x, ku); ku = fma(va2.y, u2.y, ku);                        \
-    ku = fma(va3.x, u3.x, ku); ku = fma(va3.y, u3.y, ku);                        \
+    const double* u_ = &s_uk[buf][acol];                                         \
+    ku = fma(va0.x, u_[0], ku); ku = fma(va0.y, u_[1], ku);                      \
+    ku = fma(va1.x, u_[2], ku); ku = fma(va1.y, u_[3], ku);                      \
+    ku = fma(va2.x, u_[4], ku); ku = fma(va2.y, u_[5], ku);                      \
+    ku = fma(va3.x, u_[6], ku); ku = fma(va3.y, u_[7], ku);                      \
   }
 
   CON_GLOAD(0);
-  CON_KU(0);
   CON_SSTORE(0);
   __syncthreads();
   for (int step = 0; step < nsteps; ++step) {
     const int cur = step & 1;
+    CON_KU(cur);   // va still holds this step's staged K values
     if (step + 1 < nsteps) CON_GLOAD(step + 1);
     const double* As = lds + cur * (A_SZ + B_SZ);
     const double* Bs = As + A_SZ;
@@ -413,10 +416,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
         for (int fn = 0; fn < 4; ++fn)
           acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
     }
-    if (step + 1 < nsteps) {
-      CON_KU(step + 1);
-      CON_SSTORE(cur ^ 1);
-    }
+    if (step + 1 < nsteps) CON_SSTORE(cur ^ 1);
     __syncthreads();
   }
 #undef CON_GLOAD
@@ -454,22 +454,28 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     double* s_q = s_cd;                       // [2][128] (reuses s_cd / s_xs space)
     // per lane: 16 rows (fm, q) x 4 cols (fn) -> row sums over this wave's 64 columns
 #pragma unroll
-    for (int fm = 0; fm < 4; ++fm)
+    for (int fm = 0; fm < 4; ++fm) {
+      double kv[4][4];   // the 16 K values of this row fragment, issued together
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn)
+          kv[q][fn] = Kt[(int64_t)(wr * 64 + fm * 16 + (lane >> 4) + 4 * q) * mp +
+                         wc * 64 + fn * 16 + (lane & 15)];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
         double v = 0.0;
 #pragma unroll
-        for (int fn = 0; fn < 4; ++fn) {
-          const int col = wc * 64 + fn * 16 + (lane & 15);
-          v = fma(Kt[(int64_t)row * mp + col], acc[fm][fn][q], v);   // K = 0 outside (n, m)
-        }
+        for (int fn = 0; fn < 4; ++fn)
+          v = fma(kv[q][fn], acc[fm][fn][q], v);   // K = 0 outside (n, m)
         v += __shfl_xor(v, 1, 64);
         v += __shfl_xor(v, 2, 64);
         v += __shfl_xor(v, 4, 64);
         v += __shfl_xor(v, 8, 64);
         if ((lane & 15) == 0) s_q[wc * T128 + row] = v;
       }
+    }
     __syncthreads();
     if (tid < T128) rowq[tj * n_pad + i0 + tid] = s_q[tid] + s_q[T128 + tid];
     return;
@@ -516,6 +522,11 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
       }
 #pragma unroll
       for (int fm = 0; fm < 4; ++fm) {
+        // the fragment's 4 K values issued together (K is zero-padded: every address valid)
+        double kv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          kv[q] = Kt[(int64_t)(wr * 64 + fm * 16 + (lane >> 4) + 4 * q) * mp + col];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
@@ -523,7 +534,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
           double G = s_rs[row] * acc[fm][fn][q];
           if constexpr (V2) G = fma(s_beta[row], vcol, G);
           G = fma(s_alpha[row], ucol, G);
-          const double gk = valid ? G * Kt[(int64_t)row * mp + col] : 0.0;
+          const double gk = valid ? G * kv[q] : 0.0;
           e_sig += gk;
           const double* xr = &s_xs[row * d];
           double s = 0.0;
