@@ -14,6 +14,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -131,6 +132,8 @@ struct sgp_ctx {
   double *knot_slab = nullptr, *knot_part = nullptr, *knot_kmm = nullptr;
   std::vector<double> knot_raw;           // d F / d u (m x d, row-major), before the chain factor
   std::vector<double> hU;                 // host copy of the knots (m x d, column-major)
+  uint64_t* khash = nullptr;              // sorted knot coordinate hashes (k_coinc)
+  int* kidx = nullptr;                    // knot index of each sorted hash
   std::vector<double> xmin, xmax;         // column ranges of this context's rows
   int phase = 0;
   int last_mode = 0;   // 1 VI, 2 FITC, 3 Laplace: the evaluation sgp_posterior_u refers to
@@ -229,6 +232,8 @@ void ctx_free(sgp_ctx* c) {
                   c->Cprev,  c->knot_slab, c->knot_part, c->knot_kmm};
   for (void* p : ptrs)
     if (p) hipFree(p);
+  if (c->khash) hipFree(c->khash);
+  if (c->kidx) hipFree(c->kidx);
   if (c->g_bm) hipGraphExecDestroy(c->g_bm);
   if (c->g_bm_graph) hipGraphDestroy(c->g_bm_graph);
   if (c->g_k22) hipGraphExecDestroy(c->g_k22);
@@ -247,7 +252,36 @@ hipError_t upload_rows(double* dst, const double* src, int64_t n, int64_t n_pad)
   return hipMemcpy(dst, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice);
 }
 
+// FNV-1a over the coordinates' bytes, +0/-0 canonicalised (k_mfma.hip coord_hash)
+uint64_t coord_hash_host(const double* x, int64_t stride, int d) {
+  uint64_t h = 1469598103934665603ull;
+  for (int q = 0; q < d; ++q) {
+    double v = x[q * stride];
+    if (v == 0.0) v = 0.0;
+    uint64_t b;
+    memcpy(&b, &v, sizeof(b));
+    for (int k = 0; k < 8; ++k) {
+      h ^= (b >> (8 * k)) & 0xffu;
+      h *= 1099511628211ull;
+    }
+  }
+  return h;
+}
+
 int upload_knots(sgp_ctx* c, const double* U, int64_t m, int64_t ldu) {
+  {
+    std::vector<std::pair<uint64_t, int>> hk((size_t)m);
+    for (int64_t j = 0; j < m; ++j) hk[(size_t)j] = {coord_hash_host(U + j, ldu, c->d), (int)j};
+    std::sort(hk.begin(), hk.end());
+    std::vector<uint64_t> hh((size_t)m);
+    std::vector<int> hi((size_t)m);
+    for (int64_t j = 0; j < m; ++j) {
+      hh[(size_t)j] = hk[(size_t)j].first;
+      hi[(size_t)j] = hk[(size_t)j].second;
+    }
+    HIPCHK(hipMemcpy(c->khash, hh.data(), sizeof(uint64_t) * m, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->kidx, hi.data(), sizeof(int) * m, hipMemcpyHostToDevice));
+  }
   c->hU.assign((size_t)(m * c->d), 0.0);
   for (int q = 0; q < c->d; ++q)
     for (int64_t j = 0; j < m; ++j) c->hU[(size_t)(j + q * m)] = U[j + q * ldu];
@@ -483,6 +517,8 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->sc, SC_N);
   st = st ? st : dalloc(&c->y, np_);
   st = st ? st : dalloc(&c->mu, np_);
+  st = st ? st : dalloc(&c->khash, mp);
+  st = st ? st : dalloc(&c->kidx, mp);
   if (st) {
     ctx_free(c);
     delete c;
@@ -599,9 +635,15 @@ static int contract_pass(sgp_ctx* c, const double* M, ConArgs ca, double* rec_ou
                          double* knot_out, bool knot_acc) {
   int64_t nrec = 0, nwg = 0;
   if (c->knot_on) ca.knot_slab = c->knot_slab;
+  const bool fused = ca.uvec != nullptr && ca.alpha_in == nullptr;
+  if (fused) ca.alpha_out = c->alpha;   // k_coinc needs the fused alpha_i
   HIPCHK(launch_contract_args(c->kp, c->K, M, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp, c->m,
                               c->mp, ca, c->slab_con, &nrec, &nwg, c->stream));
   HIPCHK(launch_colsum(c->slab_con, nwg, nrec, rec_out, c->stream));
+  // tau's coincidence sums -> record fields 1+L .. 3+L
+  HIPCHK(launch_coinc(c->X, c->n_pad, c->n, c->kp.d, c->U, c->mp, c->m, c->khash, c->kidx, c->K,
+                      c->mp, M, ca, fused ? c->alpha : ca.alpha_in, c->slab_small,
+                      rec_out + 1 + c->kp.L, c->stream));
   if (c->knot_on)
     HIPCHK(launch_knot_reduce(c->knot_slab, c->n_pad / SGP_TILE, c->mp, c->kp.d, c->knot_part,
                               knot_out, knot_acc, c->stream));

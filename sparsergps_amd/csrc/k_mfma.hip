@@ -510,6 +510,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     for (int fn = 0; fn < 4; ++fn) {
       const int col = wc * 64 + fn * 16 + (lane & 15);
       const bool cvalid = (j0 + col) < m;
+
       double uj[DT];
 #pragma unroll
       for (int c = 0; c < DT; ++c) uj[c] = (c < d) ? s_us[col * d + c] : 0.0;
@@ -522,7 +523,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
       }
 #pragma unroll
       for (int fm = 0; fm < 4; ++fm) {
-        // the fragment's 4 K values issued together (K is zero-padded: every address valid)
+        // the fragment's 4 K values (K is zero-padded: every address valid)
         double kv[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -549,17 +550,8 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
             }
           }
           if (!ard) e_l[0] = fma(gk, s * rl2s, e_l[0]);
-          if (valid && s == 0.0) {
-            // rare path: tau's dK12 rule needs all(x_i == u_j) on the raw coordinates
-            bool eq = true;
-            for (int c = 0; c < d; ++c)
-              eq = eq && (X[(i0 + row) + c * ldx] == U[(j0 + col) + c * ldu]);
-            if (eq) {
-              c_sum += G;
-              c_cnt += 1.0;
-              c_dg += s_cd[col];
-            }
-          }
+          // tau's coincidence sums (x_i == u_j exactly) are not accumulated here: k_coinc
+          // finds those pairs by hash and recomputes their G_ij (launch_coinc)
         }
       }
       if constexpr (KNOT) {
@@ -630,6 +622,79 @@ k_knot_reduce2(const double* __restrict__ part, int rows, int64_t ncol, double* 
   double s = 0.0;
   for (int r = 0; r < rows; ++r) s += part[(int64_t)r * ncol + col];
   out[col] = accumulate ? out[col] + s : s;
+}
+
+// ============================================================================ coincidences
+// tau's dK12/dlog(tau) = 2 tau^2 exactly where a data row equals a knot (quirk Q5).  Knots are
+// hashed on the host (khash sorted, kidx the knot of each hash); thread i hashes row i,
+// binary-searches, verifies the coordinates and, per match j, recomputes
+//   G_ij = alpha_i u_j + beta_i v_j + rs_i (K M)_ij
+// with one length-m dot product.  Per-row sums, block partials [nb][3] = {sum G, count,
+// sum cdiag_j}: deterministic, and O(n d) work when nothing coincides.
+__device__ __forceinline__ uint64_t coord_hash(const double* x, int64_t stride, int d) {
+  uint64_t h = 1469598103934665603ull;
+  for (int c = 0; c < d; ++c) {
+    double v = x[c * stride];
+    if (v == 0.0) v = 0.0;   // +0 and -0 compare equal in R
+    uint64_t b = (uint64_t)__double_as_longlong(v);
+    for (int k = 0; k < 8; ++k) {
+      h ^= (b >> (8 * k)) & 0xffu;
+      h *= 1099511628211ull;
+    }
+  }
+  return h;
+}
+
+__global__ void __launch_bounds__(256)
+k_coinc(const double* __restrict__ X, int64_t ldx, int64_t n, int d, const double* __restrict__ U,
+        int64_t ldu, int64_t m, const uint64_t* __restrict__ khash, const int* __restrict__ kidx,
+        const double* __restrict__ K, int64_t mp, const double* __restrict__ M,
+        const double* __restrict__ alpha, const double* __restrict__ uvec,
+        const double* __restrict__ beta, const double* __restrict__ vvec,
+        const double* __restrict__ rs_vec, double rs, const double* __restrict__ cdiag,
+        double* __restrict__ part) {
+  double a[3] = {0.0, 0.0, 0.0};
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const uint64_t h = coord_hash(X + i, ldx, d);
+    int64_t lo = 0, hi = m;   // first position with khash >= h
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (khash[mid] < h) lo = mid + 1; else hi = mid;
+    }
+    for (int64_t p = lo; p < m && khash[p] == h; ++p) {
+      const int64_t j = kidx[p];
+      bool eq = true;
+      for (int c = 0; c < d; ++c) eq = eq && (X[i + c * ldx] == U[j + c * ldu]);
+      if (!eq) continue;
+      double t = 0.0;
+      for (int64_t k = 0; k < m; ++k) t = fma(K[i * mp + k], M[k * mp + j], t);
+      double g = (rs_vec ? rs * rs_vec[i] : rs) * t;
+      if (beta) g = fma(beta[i], vvec[j], g);
+      if (alpha && uvec) g = fma(alpha[i], uvec[j], g);
+      a[0] += g;
+      a[1] += 1.0;
+      a[2] += cdiag ? cdiag[j] : 0.0;
+    }
+  }
+  __shared__ double sh[4][3];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int k = 0; k < 3; ++k) {
+    const double v = wave_sum(a[k]);
+    if (lane == 0) sh[w][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3)
+    part[blockIdx.x * 3 + threadIdx.x] =
+        sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
+}
+
+// rec[0..2] += sum_b part[b][0..2]
+__global__ void k_coinc_add(const double* __restrict__ part, int nb, double* __restrict__ rec) {
+  if (threadIdx.x < 3) {
+    double s = 0.0;
+    for (int b = 0; b < nb; ++b) s += part[b * 3 + threadIdx.x];
+    rec[threadIdx.x] += s;
+  }
 }
 
 // rowq[tj][i] summed over the column tiles -> out[i] (deterministic order)
@@ -791,6 +856,19 @@ hipError_t launch_gemm_tn(const double* A, int64_t lda, int64_t ma, const double
                      n_pad, nta, ntb, chunk, slab);
   hipLaunchKernelGGL(k_gemm_tn_reduce, dim3(T128 * T128 / 256, ntile), dim3(256), 0, s, slab,
                      (int)splits, nta, ntb, C);
+  return hipGetLastError();
+}
+
+hipError_t launch_coinc(const double* X, int64_t ldx, int64_t n, int d, const double* U,
+                        int64_t ldu, int64_t m, const uint64_t* khash, const int* kidx,
+                        const double* K, int64_t mp, const double* M, const ConArgs& ca,
+                        const double* alpha, double* part, double* rec, hipStream_t s) {
+  int64_t nb = (n + 255) / 256;
+  if (nb > 1024) nb = 1024;
+  hipLaunchKernelGGL(k_coinc, dim3((unsigned)nb), dim3(256), 0, s, X, ldx, n, d, U, ldu, m, khash,
+                     kidx, K, mp, M, alpha, ca.uvec, ca.beta_in, ca.vvec, ca.rs_vec, ca.rs,
+                     ca.cdiag, part);
+  hipLaunchKernelGGL(k_coinc_add, dim3(1), dim3(64), 0, s, part, (int)nb, rec);
   return hipGetLastError();
 }
 

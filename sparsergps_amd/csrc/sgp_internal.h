@@ -252,3 +252,11 @@ hipError_t launch_vi_cand_scalars(int64_t m, int64_t mp, int64_t T, int64_t Tp,
 // column sums of squares: out[j] = sum_i K_ij^2 (deterministic two-level, part as gemv_cols)
 hipError_t launch_colnorm2(const double* K, int64_t n_pad, int64_t mp, double* part,
                            int64_t part_cap, double* out, hipStream_t s);
+
+// tau coincidence sums of one contraction pass (k_mfma.hip k_coinc): rec[0..2] +=
+// {sum G_ij, #pairs, sum cdiag_j} over the pairs x_i == u_j; alpha = the pass's alpha_i
+// (alpha_in, or the fused alpha written through alpha_out); part: 1024 * 3 doubles.
+hipError_t launch_coinc(const double* X, int64_t ldx, int64_t n, int d, const double* U,
+                        int64_t ldu, int64_t m, const uint64_t* khash, const int* kidx,
+                        const double* K, int64_t mp, const double* M, const ConArgs& ca,
+                        const double* alpha, double* part, double* rec, hipStream_t s);
