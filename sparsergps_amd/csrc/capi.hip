@@ -121,6 +121,7 @@ struct sgp_ctx {
   int* status = nullptr;
   double *red1 = nullptr, *red2 = nullptr;
   double *slab_syrk = nullptr, *slab_con = nullptr, *slab_small = nullptr, *sc = nullptr;
+  double* tslab = nullptr;                // builder t = K^T r partials (VI), n_pad/64 x mp
   int64_t slab_syrk_cap = 0, slab_con_cap = 0;
   // state carried between phases
   KernParams kp;
@@ -229,7 +230,7 @@ void ctx_free(sgp_ctx* c) {
                   c->red2,   c->slab_syrk, c->slab_con, c->slab_small, c->sc,
                   c->Xt22,   c->T22,    c->dinv22, c->omega, c->pvec, c->rowq, c->red2f,
                   c->y,      c->mu,     c->lv,     c->lm,    c->lslab, c->lred[0], c->lred[1],
-                  c->Cprev,  c->knot_slab, c->knot_part, c->knot_kmm};
+                  c->Cprev,  c->knot_slab, c->knot_part, c->knot_kmm, c->tslab};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->khash) hipFree(c->khash);
@@ -517,6 +518,7 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->sc, SC_N);
   st = st ? st : dalloc(&c->y, np_);
   st = st ? st : dalloc(&c->mu, np_);
+  st = st ? st : dalloc(&c->tslab, (np_ / 64) * mp);
   st = st ? st : dalloc(&c->khash, mp);
   st = st ? st : dalloc(&c->kidx, mp);
   if (st) {
@@ -755,22 +757,28 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->stream));
   st = k22_stage(c, kp.tau2);   // aux stream, overlaps the builder and the SYRK below
   if (st) return st;
+  const int64_t mpv = c->mp, mmv = mpv * mpv;
   {
+    // K12, and t = K^T r riding along in the memory-bound builder (keeps the SYRK's
+    // diagonal tiles as cheap as the others)
     Scope t(c, "build_knm");
-    HIPCHK(launch_build_knm(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp, m, c->mp, c->K,
-                            c->stream));
+    HIPCHK(launch_build_knm_t(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, mpv, m, mpv, c->K, c->r,
+                              c->tslab, c->stream));
   }
   HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_vi_red1_count(m), c->stream));
+  HIPCHK(launch_knot_reduce(c->tslab, c->n_pad / 64, mpv, 1, c->T1, red1 + mmv, false,
+                            c->stream));
+  HIPCHK(launch_dot(c->r, c->r, c->n_pad, c->slab_small, red1 + mmv + mpv, c->stream));
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));   // keep the SYRK round unshared
   {
     Scope t(c, "syrk");
-    HIPCHK(launch_syrk_aug(c->K, c->n_pad, c->mp, c->r, nullptr, c->slab_syrk,
-                           c->slab_syrk_cap, red1, c->stream, 1));
+    HIPCHK(launch_syrk_aug(c->K, c->n_pad, mpv, c->r, nullptr, c->slab_syrk, c->slab_syrk_cap,
+                           red1, c->stream, 1, nullptr, 0));
   }
   {
     Scope t(c, "syrk_reduce");
-    HIPCHK(launch_syrk_aug(c->K, c->n_pad, c->mp, c->r, nullptr, c->slab_syrk,
-                           c->slab_syrk_cap, red1, c->stream, 2));
+    HIPCHK(launch_syrk_aug(c->K, c->n_pad, mpv, c->r, nullptr, c->slab_syrk, c->slab_syrk_cap,
+                           red1, c->stream, 2, nullptr, 0));
   }
   c->phase = 1;
   return SGP_OK;
@@ -1065,7 +1073,7 @@ int sgp_fitc_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned f
   {
     Scope tm(c, "syrk_omega");
     HIPCHK(launch_syrk_aug(c->K, c->n_pad, mp, c->r, c->omega, c->slab_syrk, c->slab_syrk_cap,
-                           red2, c->stream, 3));
+                           red2, c->stream, 3, nullptr, 0));
     // the SYRK reduce wrote rr_omega at mm + mp; keep sum(omega) at mm + mp + 1
   }
   const int64_t off = fitc_rec_off(mp);
@@ -1288,7 +1296,7 @@ int sgp_lap_begin(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   {
     Scope t(c, "syrk_z");
     HIPCHK(launch_syrk_aug(c->K, c->n_pad, mp, c->r, lvec(c, LV_ZI), c->slab_syrk,
-                           c->slab_syrk_cap, red_out, c->stream, 3));
+                           c->slab_syrk_cap, red_out, c->stream, 3, nullptr, 0));
   }
   st = lap_obj_partials(c, red_out, lap_obj_off(mp));
   if (st) return st;
@@ -1432,7 +1440,7 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
     const int64_t off = lap_rec_off(mp);
     HIPCHK(hipMemsetAsync(red_out, 0, sizeof(double) * (off + 2 * (kp.L + 5)), c->stream));
     HIPCHK(launch_syrk_aug(c->K, n_pad, mp, c->r, lvec(c, LV_A), c->slab_syrk, c->slab_syrk_cap,
-                           red_out, c->stream, 3));
+                           red_out, c->stream, 3, nullptr, 0));
     HIPCHK(launch_colsum(c->slab_small, nb, 1, red_out + mm + mp + 1, c->stream));
     int64_t nrec = kp.L + 5;
     double* kout = red_out + off + 2 * nrec;

@@ -105,8 +105,12 @@ __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* 
                                                    int64_t ldx, int64_t n,
                                                    const double* __restrict__ U, int64_t ldu,
                                                    int64_t m, int64_t mp,
-                                                   double* __restrict__ K) {
+                                                   double* __restrict__ K,
+                                                   const double* __restrict__ rvec,
+                                                   double* __restrict__ tslab) {
   __shared__ __attribute__((aligned(16))) double xs[64 * DT];
+  __shared__ double rsh[64];
+  __shared__ double tsh[4][64];
   const int d = kp.d;
   const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
   const int64_t i0 = (int64_t)blockIdx.y * 64;
@@ -118,6 +122,8 @@ __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* 
     if (c < d && i < n) v = ARD ? X[i + c * ldx] * kp.rl[c] : X[i + c * ldx];
     xs[e] = v;
   }
+  if (rvec && tid < 64) rsh[tid] = (i0 + tid < n) ? rvec[i0 + tid] : 0.0;
+  double tpart = 0.0;
   double uj[DT];
   const bool jv = j < m;
 #pragma unroll
@@ -139,6 +145,14 @@ __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* 
     }
     const double v = (jv && i < n) ? sig2 * sgp_exp_nonpos(scale * s) : 0.0;
     K[i * mp + j] = v;
+    if (rvec) tpart = fma(v, rsh[r], tpart);
+  }
+  if (rvec) {   // t_j partial of this block's 64 rows, fixed combination order
+    tsh[threadIdx.y][threadIdx.x] = tpart;
+    __syncthreads();
+    if (threadIdx.y == 0)
+      tslab[(int64_t)blockIdx.y * mp + j] =
+          ((tsh[0][threadIdx.x] + tsh[1][threadIdx.x]) + tsh[2][threadIdx.x]) + tsh[3][threadIdx.x];
   }
 }
 
@@ -294,20 +308,33 @@ hipError_t launch_fill_dcov(const KernParams& kp, const double* x, int64_t n, in
   return hipGetLastError();
 }
 
-hipError_t launch_build_knm(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
-                            int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
-                            double* K, hipStream_t s) {
+static hipError_t build_knm_impl(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
+                                 int64_t n_pad, const double* U, int64_t ldu, int64_t m,
+                                 int64_t mp, double* K, const double* r, double* tslab,
+                                 hipStream_t s) {
   dim3 grid((unsigned)(mp / 64), (unsigned)(n_pad / 64));
   const bool ard = kp.kernel == 1;
   if (kp.kernel == 2) return hipErrorInvalidValue;
   if (kp.d <= 8) {
-    if (ard) hipLaunchKernelGGL((k_build_knm<true, 8>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K);
-    else hipLaunchKernelGGL((k_build_knm<false, 8>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K);
+    if (ard) hipLaunchKernelGGL((k_build_knm<true, 8>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab);
+    else hipLaunchKernelGGL((k_build_knm<false, 8>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab);
   } else {
-    if (ard) hipLaunchKernelGGL((k_build_knm<true, SGP_MAXD>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K);
-    else hipLaunchKernelGGL((k_build_knm<false, SGP_MAXD>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K);
+    if (ard) hipLaunchKernelGGL((k_build_knm<true, SGP_MAXD>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab);
+    else hipLaunchKernelGGL((k_build_knm<false, SGP_MAXD>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab);
   }
   return hipGetLastError();
+}
+
+hipError_t launch_build_knm(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
+                            int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
+                            double* K, hipStream_t s) {
+  return build_knm_impl(kp, X, ldx, n, n_pad, U, ldu, m, mp, K, nullptr, nullptr, s);
+}
+
+hipError_t launch_build_knm_t(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
+                              int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
+                              double* K, const double* r, double* tslab, hipStream_t s) {
+  return build_knm_impl(kp, X, ldx, n, n_pad, U, ldu, m, mp, K, r, tslab, s);
 }
 
 hipError_t launch_build_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,

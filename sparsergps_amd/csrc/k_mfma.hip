@@ -50,7 +50,8 @@ __device__ __forceinline__ void store8(double* s, const double2 (&v)[4]) {
 // grid = splits * T (T = lower 128-tiles); block 256 = 4 waves as 2x2 of 64x64.
 __global__ void __launch_bounds__(256, 2)
 k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __restrict__ r,
-       const double* __restrict__ w, const double* __restrict__ tv, int64_t chunk, int T, int nb,
+       const double* __restrict__ w, const double* __restrict__ tv, int with_t, int64_t chunk,
+       int T, int nb,
        double* __restrict__ slab_s, double* __restrict__ slab_t, double* __restrict__ slab_rr) {
   __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
   __shared__ __attribute__((aligned(16))) double Kb[2][BK * SB];
@@ -141,12 +142,12 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
         for (int fn = 0; fn < 4; ++fn)
           acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
     }
-    if (diag && tid < T128) {
+    if (with_t && diag && tid < T128) {
       // t_a += sum_i (w_i r_i) K_ia over this step's rows (unscaled operand image)
 #pragma unroll
       for (int q = 0; q < BK; ++q) tacc = fma(rw[cur][q], Bs[q * SB + tid], tacc);
     }
-    if (diag && ta == 0 && tid == 255) {
+    if (with_t && diag && ta == 0 && tid == 255) {
       double s = 0.0;
       for (int q = 0; q < BK; ++q) s += rw[cur][q] * rv[cur][q];
       rr_acc += s;
@@ -812,7 +813,7 @@ int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp) {
 
 hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const double* r,
                            const double* w, double* slab, int64_t slab_cap, double* red,
-                           hipStream_t s, int part, const double* tv) {
+                           hipStream_t s, int part, const double* tv, int with_t) {
   SyrkPlan p = syrk_plan(n_pad, mp);
   double* slab_s = slab;
   double* slab_t = slab_s + (int64_t)p.splits * p.T * T128 * T128;
@@ -820,12 +821,13 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
   if (slab_rr + p.splits > slab + slab_cap) return hipErrorInvalidValue;
   if (part & 1)
     hipLaunchKernelGGL(k_syrk, dim3((unsigned)(p.splits * p.T)), dim3(256), 0, s, K, n_pad, mp,
-                       r, w, tv, p.chunk, p.T, p.nb, slab_s, slab_t, slab_rr);
+                       r, w, tv, with_t, p.chunk, p.T, p.nb, slab_s, slab_t, slab_rr);
   if (part & 2) {
     hipLaunchKernelGGL(k_syrk_reduce, dim3(T128 * T128 / 256, p.T), dim3(256), 0, s, slab_s,
                        p.splits, p.T, mp, red);
-    hipLaunchKernelGGL(k_syrk_reduce_t, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s,
-                       slab_t, slab_rr, p.splits, p.nb, mp, red);
+    if (with_t)
+      hipLaunchKernelGGL(k_syrk_reduce_t, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s,
+                         slab_t, slab_rr, p.splits, p.nb, mp, red);
   }
   return hipGetLastError();
 }

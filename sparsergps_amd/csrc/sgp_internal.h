@@ -63,6 +63,11 @@ hipError_t launch_fill_cov(const KernParams& kp, const double* x, int64_t n, int
 hipError_t launch_fill_dcov(const KernParams& kp, const double* x, int64_t n, int64_t ldx,
                             const double* xp, int64_t np, int64_t ldxp, bool sym, int param,
                             double* out, int64_t ldo, hipStream_t s);
+// t partials of the builder (VI): tslab[row block of 64][j] = sum_i K_ij r_i; reduce with
+// launch_knot_reduce(tslab, n_pad / 64, mp, 1, ...).
+hipError_t launch_build_knm_t(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
+                              int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
+                              double* K, const double* r, double* tslab, hipStream_t s);
 // K12 (n_pad x mp, row-major, ld = mp).  Rows >= n and columns >= m are written as 0.
 hipError_t launch_build_knm(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
                             int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
@@ -88,7 +93,8 @@ hipError_t launch_contract_kmm(const KernParams& kp, const double* U, int64_t ld
 hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const double* r,
                            const double* w, double* slab, int64_t slab_cap, double* red,
                            hipStream_t s, int part = 3,  // part: 1 = main kernel, 2 = reduce
-                           const double* tv = nullptr);
+                           const double* tv = nullptr,
+                           int with_t = 1);              // 0: S only (red[mm..] untouched)
 int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp);
 // Gradient contraction on T = K M (K: n_pad x mp, M: mp x mp):
 //   G_ij = alpha_i u_j + rs_i T_ij,  alpha_i = (r_i - K_i u) * iz_i computed in the same pass
