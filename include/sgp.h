@@ -62,6 +62,9 @@ typedef enum {
 
 /* flags for the fused evaluations */
 #define SGP_FLAG_R_DET 1u /* reproduce R's det() overflow in log(det(K22)) */
+/* objective only (elbo_fun, obj_fun_norm, newtrap_sparseGP without dlogq_dcov_par): every
+ * gradient pass is skipped and grad may be NULL; the knot posterior stays available */
+#define SGP_FLAG_OBJ_ONLY 2u
 
 const char* sgp_last_error(void);
 int sgp_abi_version(void);
@@ -166,10 +169,16 @@ int sgp_eval_laplace(sgp_ctx* ctx, int kernel, const double* theta, const double
  * are functions of the summed buffers only).  Buffers hold sgp_lap_red_count doubles. */
 int64_t sgp_lap_red_count(int kernel, int d, int64_t m);
 int sgp_lap_begin(sgp_ctx* ctx, int kernel, const double* theta, const double* U, int64_t m,
-                  int64_t ldu, double delta, double expo, double tol, int maxit, double* red_out,
-                  int64_t* count);
+                  int64_t ldu, double delta, double expo, double tol, int maxit, unsigned flags,
+                  double* red_out, int64_t* count);
 int sgp_lap_step(sgp_ctx* ctx, const double* red_in, double* red_out, int64_t* count,
                  int* done, double* obj, double* grad, int* nr_iters);
+/* newtrap_sparseGP alone (R/newtrap_sparseGP.R:6-186): the NR loop from the resident f, f left
+ * at the mode; obj = the last entry of objective_function_values (= sgp_lap_begin with
+ * SGP_FLAG_OBJ_ONLY driven to completion) */
+int sgp_lap_nr(sgp_ctx* ctx, int kernel, const double* theta, const double* U, int64_t m,
+               int64_t ldu, double delta, double expo, double tol, int maxit, double* obj,
+               int* nr_iters);
 
 /* Posterior of the knot values u at the end of a fit, from the context's last completed
  * evaluation (VI: vi_functions.R:1161-1180; FITC: laplace_gradient_ascent.R:1635-1655;
@@ -216,6 +225,21 @@ int sgp_ctx_row_bounds(sgp_ctx* ctx, double* col_min, double* col_max);
 int sgp_vi_candidates(sgp_ctx* ctx, int kernel, const double* theta, const double* U, int64_t m,
                       int64_t ldu, double delta, unsigned flags, const double* cand, int64_t T,
                       int64_t ldc, double* obj_out);
+
+/* OAT knot proposal scoring for FITC (knot_prop_random_norm / knot_prop_ego_norm,
+ * R/knot_proposal_functions.R:1176-1363, 498-): obj_fun_norm at knots [U; cand_t] with
+ * Sigma22 = Kuu + delta I, for each of T candidates (m + 1 <= m_max).  NaN = try-error. */
+int sgp_fitc_candidates(sgp_ctx* ctx, int kernel, const double* theta, const double* U,
+                        int64_t m, int64_t ldu, double delta, unsigned flags, const double* cand,
+                        int64_t T, int64_t ldc, double* obj_out);
+
+/* OAT knot proposal scoring for Poisson Laplace (knot_prop_random / knot_prop_ego,
+ * R/knot_proposal_functions.R:1001-1173, 46-): for each candidate, newtrap_sparseGP at knots
+ * [U; cand_t] warm-started from the resident f (the fit's fmax); obj_out[t] = its last
+ * objective value.  The resident f is restored afterwards.  NaN = try-error. */
+int sgp_lap_candidates(sgp_ctx* ctx, int kernel, const double* theta, const double* U, int64_t m,
+                       int64_t ldu, double delta, double expo, double tol, int maxit,
+                       const double* cand, int64_t T, int64_t ldc, double* obj_out);
 
 /* Per-kernel timing of the last evaluation (HIP events on the launch stream).
  * names: '\n'-separated kernel-phase names; ms: their durations (max n entries). */

@@ -20,6 +20,7 @@ c_int_p = C.POINTER(C.c_int)
 SGP_OK, SGP_EINVAL, SGP_ENOTPD, SGP_EHIP, SGP_ENOMEM = 0, 1, 2, 3, 4
 KERNELS = {"sqexp": 0, "ard": 1, "exp": 2}
 SGP_FLAG_R_DET = 1
+SGP_FLAG_OBJ_ONLY = 2
 SGP_PRED_VI, SGP_PRED_LAPLACE = 0, 1
 
 # name -> (restype, argtypes); exactly the functions declared in include/sgp.h
@@ -67,10 +68,12 @@ PROTOTYPES = {
                                    c_double_p, c_double_p, c_int_p]),
     "sgp_lap_red_count": (C.c_int64, [C.c_int, C.c_int, C.c_int64]),
     "sgp_lap_begin": (C.c_int, [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_int64, C.c_int64,
-                                C.c_double, C.c_double, C.c_double, C.c_int, C.c_void_p,
-                                C.POINTER(C.c_int64)]),
+                                C.c_double, C.c_double, C.c_double, C.c_int, C.c_uint,
+                                C.c_void_p, C.POINTER(C.c_int64)]),
     "sgp_lap_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_int64), c_int_p,
                                c_double_p, c_double_p, c_int_p]),
+    "sgp_lap_nr": (C.c_int, [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_int64, C.c_int64,
+                             C.c_double, C.c_double, C.c_double, C.c_int, c_double_p, c_int_p]),
     "sgp_posterior_u": (C.c_int, [C.c_void_p, c_double_p, c_double_p, c_double_p]),
     "sgp_predict": (C.c_int, [C.c_int, C.c_int, c_double_p, C.c_double, C.c_int, C.c_int, c_double_p,
                               C.c_int64, C.c_int64, c_double_p, c_double_p, c_double_p, C.c_int64,
@@ -83,6 +86,12 @@ PROTOTYPES = {
     "sgp_vi_candidates": (C.c_int, [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_int64,
                                     C.c_int64, C.c_double, C.c_uint, c_double_p, C.c_int64,
                                     C.c_int64, c_double_p]),
+    "sgp_fitc_candidates": (C.c_int, [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_int64,
+                                      C.c_int64, C.c_double, C.c_uint, c_double_p, C.c_int64,
+                                      C.c_int64, c_double_p]),
+    "sgp_lap_candidates": (C.c_int, [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_int64,
+                                     C.c_int64, C.c_double, C.c_double, C.c_double, C.c_int,
+                                     c_double_p, C.c_int64, C.c_int64, c_double_p]),
     "sgp_ctx_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "sgp_ctx_timings": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64, c_double_p, C.c_int, c_int_p]),
 }

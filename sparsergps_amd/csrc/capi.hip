@@ -880,9 +880,13 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
     HIPCHK(dense_gemv(c->Binv, mp, t, 1.0 / z, c->uvec, c->stream));         // u = Binv t / z
     HIPCHK(launch_dot(t, c->uvec, mp, c->slab_small, c->sc + SC_TU, c->stream));
     HIPCHK(launch_dot(c->K22inv, S, mm, c->slab_small, c->sc + SC_TRKS, c->stream));
-    HIPCHK(launch_dot(c->Binv, S, mm, c->slab_small, c->sc + SC_TRBS, c->stream));
     HIPCHK(hipMemcpyAsync(c->sc + SC_RR, red1 + mm + mp, sizeof(double), hipMemcpyDeviceToDevice,
                           c->stream));
+    if (flags & SGP_FLAG_OBJ_ONLY) {   // elbo_fun alone: no adjoint work
+      c->phase = 2;
+      return SGP_OK;
+    }
+    HIPCHK(launch_dot(c->Binv, S, mm, c->slab_small, c->sc + SC_TRBS, c->stream));
     // P = tau^-2 K22inv - z^-1 Binv ; M3 = K22inv S K22inv
     HIPCHK(dense_axpby(1.0 / kp.tau2, c->K22inv, -1.0 / z, c->Binv, c->Pm, mm, c->stream));
     HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->K22inv, mp, S, mp, 0.0, c->T1,
@@ -915,7 +919,11 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
 }
 
 int sgp_vi_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
-  if (!c || !red2 || !obj || !grad) { set_err("invalid arguments"); return SGP_EINVAL; }
+  const bool obj_only = c && (c->flags & SGP_FLAG_OBJ_ONLY);
+  if (!c || !red2 || !obj || (!grad && !obj_only)) {
+    set_err("invalid arguments");
+    return SGP_EINVAL;
+  }
   if (c->phase != 2) { set_err("sgp_vi_finish called before sgp_vi_phase2"); return SGP_EINVAL; }
   HIPCHK(hipSetDevice(c->device));
   const KernParams& kp = c->kp;
@@ -924,7 +932,8 @@ int sgp_vi_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
   int status[4];
   const int64_t n2 = sgp_vi_red2_count(kp.kernel, kp.d);
   HIPCHK(hipMemcpyAsync(sc, c->sc, sizeof(sc), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(r2, red2, sizeof(double) * n2, hipMemcpyDeviceToHost, c->stream));
+  if (!obj_only)
+    HIPCHK(hipMemcpyAsync(r2, red2, sizeof(double) * n2, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(status, c->status, sizeof(status), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   c->phase = 0;
@@ -951,6 +960,10 @@ int sgp_vi_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
   const double det_part = -0.5 * (n * log(z) - logdet22 + ldB);
   const double trace_term = -(1.0 / (2.0 * kp.tau2)) * (n * (kp.sig2 + c->delta) - trKS);
   *obj = quad + det_part - (n / 2.0) * log(2.0 * M_PI) + trace_term;
+  if (obj_only) {
+    c->knot_raw.clear();
+    return SGP_OK;
+  }
   // delbo_dcov_par (vi_functions.R:259-419) in adjoint form
   // red2 = [e_sig, e_l(L), c_sum, c_cnt, c_dg, alpha^T alpha]
   const double e_sig = r2[0];
@@ -1061,6 +1074,10 @@ int sgp_fitc_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned f
     HIPCHK(hipMemcpyAsync(c->sc + SC_RR, red1 + mm + mp, 2 * sizeof(double),
                           hipMemcpyDeviceToDevice, c->stream));               // rr_w, sum log Z
   }
+  if (flags & SGP_FLAG_OBJ_ONLY) {   // obj_fun_norm alone
+    c->phase = 12;
+    return SGP_OK;
+  }
   {
     Scope tm(c, "rowquad_p");
     HIPCHK(launch_rowquad_knm(kp, c->K, c->Binv, c->n, c->n_pad, c->m, mp, c->r, 0.0, c->zinv,
@@ -1105,13 +1122,17 @@ int sgp_fitc_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned f
 }
 
 int sgp_fitc_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
-  if (!c || !red2 || !obj || !grad) { set_err("invalid arguments"); return SGP_EINVAL; }
+  const bool obj_only = c && (c->flags & SGP_FLAG_OBJ_ONLY);
+  if (!c || !red2 || !obj || (!grad && !obj_only)) {
+    set_err("invalid arguments");
+    return SGP_EINVAL;
+  }
   if (c->phase != 12) { set_err("sgp_fitc_finish called before sgp_fitc_phase2"); return SGP_EINVAL; }
   HIPCHK(hipSetDevice(c->device));
   const KernParams& kp = c->kp;
   const int L = kp.L;
   const int64_t mp = c->mp;
-  {
+  if (!obj_only) {
     Scope tm(c, "contract_kmm");
     // M3 = K22^-1 S_omega K22^-1 ; G22 = -1/2 uu^T + 1/2 (K22^-1 - Bm^-1) + 1/2 M3
     HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->K22inv, mp, red2, mp, 0.0,
@@ -1129,10 +1150,12 @@ int sgp_fitc_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
   const int64_t off = fitc_rec_off(mp);
   const int nrec = L + 5;
   HIPCHK(hipMemcpyAsync(sc, c->sc, sizeof(sc), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(r2, red2 + mp * mp + mp + 1, sizeof(double), hipMemcpyDeviceToHost,
-                        c->stream));
-  HIPCHK(hipMemcpyAsync(r2 + 1, red2 + off, sizeof(double) * 2 * nrec, hipMemcpyDeviceToHost,
-                        c->stream));
+  if (!obj_only) {
+    HIPCHK(hipMemcpyAsync(r2, red2 + mp * mp + mp + 1, sizeof(double), hipMemcpyDeviceToHost,
+                          c->stream));
+    HIPCHK(hipMemcpyAsync(r2 + 1, red2 + off, sizeof(double) * 2 * nrec, hipMemcpyDeviceToHost,
+                          c->stream));
+  }
   HIPCHK(hipMemcpyAsync(status, c->status, sizeof(status), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   c->phase = 0;
@@ -1148,6 +1171,10 @@ int sgp_fitc_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
   const double rr = sc[SC_RR], sumlogz = sc[SC_RR + 1], tu = sc[SC_TU];
   const double logdet22 = (c->flags & SGP_FLAG_R_DET) ? log(exp(ld22)) : ld22;
   *obj = -0.5 * rr + 0.5 * tu - 0.5 * (sumlogz - logdet22 + ldB) - (n / 2.0) * log(2.0 * M_PI);
+  if (obj_only) {
+    c->knot_raw.clear();
+    return SGP_OK;
+  }
   const double sum_omega = r2[0];
   const double* a = r2 + 1;
   const double* b = r2 + 1 + nrec;
@@ -1248,8 +1275,8 @@ static int lap_obj_partials(sgp_ctx* c, double* red, int64_t o) {
 }
 
 int sgp_lap_begin(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
-                  int64_t ldu, double delta, double expo, double tol, int maxit, double* red_out,
-                  int64_t* count) {
+                  int64_t ldu, double delta, double expo, double tol, int maxit, unsigned flags,
+                  double* red_out, int64_t* count) {
   KernParams kp;
   int st = check_eval_args(c, kernel, theta, U, m, ldu, delta, &kp);
   if (st) return st;
@@ -1270,6 +1297,7 @@ int sgp_lap_begin(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   c->lap_expo = expo;
   c->lap_tol = tol;
   c->lap_maxit = maxit;
+  c->flags = flags;
   c->lap_it = 0;
   c->lap_cnt = 0.0;
   c->lap_objs.clear();
@@ -1383,6 +1411,16 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
       HIPCHK(launch_colsum(c->slab_small, nb, 1, red_out + mp, c->stream));
       *count = mp + 1;
       c->lap_state = LS_NRB;
+      return SGP_OK;
+    }
+    if (c->flags & SGP_FLAG_OBJ_ONLY) {   // newtrap_sparseGP alone: stop at the mode
+      if (obj) *obj = c->lap_obj;
+      if (nr_iters) *nr_iters = c->lap_it;
+      c->last_mode = 3;
+      c->knot_raw.clear();
+      *count = 0;
+      *done = 1;
+      c->lap_state = LS_NONE;
       return SGP_OK;
     }
     // gradient part a (dlogq_dcov_par at the final f)
@@ -1533,11 +1571,32 @@ int sgp_eval_laplace(sgp_ctx* c, int kernel, const double* theta, const double* 
   int st = lap_ensure(c);
   if (st) return st;
   int64_t count = 0;
-  st = sgp_lap_begin(c, kernel, theta, U, m, ldu, delta, expo, tol, maxit, c->lred[0], &count);
+  st = sgp_lap_begin(c, kernel, theta, U, m, ldu, delta, expo, tol, maxit, 0u, c->lred[0],
+                     &count);
   if (st) return st;
   int cur = 0, done = 0;
   while (!done) {
     st = sgp_lap_step(c, c->lred[cur], c->lred[cur ^ 1], &count, &done, obj, grad, nr_iters);
+    if (st) return st;
+    cur ^= 1;
+  }
+  return SGP_OK;
+}
+
+int sgp_lap_nr(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
+               int64_t ldu, double delta, double expo, double tol, int maxit, double* obj,
+               int* nr_iters) {
+  if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
+  HIPCHK(hipSetDevice(c->device));
+  int st = lap_ensure(c);
+  if (st) return st;
+  int64_t count = 0;
+  st = sgp_lap_begin(c, kernel, theta, U, m, ldu, delta, expo, tol, maxit, SGP_FLAG_OBJ_ONLY,
+                     c->lred[0], &count);
+  if (st) return st;
+  int cur = 0, done = 0;
+  while (!done) {
+    st = sgp_lap_step(c, c->lred[cur], c->lred[cur ^ 1], &count, &done, obj, nullptr, nr_iters);
     if (st) return st;
     cur ^= 1;
   }
@@ -1837,6 +1896,94 @@ int sgp_vi_candidates(sgp_ctx* c, int kernel, const double* theta, const double*
     }
   }
   return SGP_OK;
+}
+
+// [U; cand_t] (m + 1) x d column-major on the host
+static void bordered_knots(const double* U, int64_t m, int64_t ldu, int d, const double* cand,
+                           int64_t t, int64_t ldc, std::vector<double>& Ub) {
+  Ub.resize((size_t)((m + 1) * d));
+  for (int q = 0; q < d; ++q) {
+    for (int64_t k = 0; k < m; ++k) Ub[(size_t)(k + q * (m + 1))] = U[k + q * ldu];
+    Ub[(size_t)(m + q * (m + 1))] = cand[t + q * ldc];
+  }
+}
+
+// FITC meta-model values (knot_proposal_functions.R:1292-1319 per candidate): obj_fun_norm at
+// [U; cand_t].  Each candidate changes Z for every row, so unlike VI there is no bordered
+// shortcut for the weighted Gram matrix; each one is an objective-only FITC evaluation
+// (builder, row-quadratic, SYRK, m x m inverse) on the resident rows.
+int sgp_fitc_candidates(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
+                        int64_t ldu, double delta, unsigned flags, const double* cand, int64_t T,
+                        int64_t ldc, double* obj_out) {
+  if (!c || !U || !cand || T < 1 || ldc < T || !obj_out || m < 1 || ldu < m) {
+    set_err("invalid sgp_fitc_candidates arguments");
+    return SGP_EINVAL;
+  }
+  if (m + 1 > c->m_max) {
+    set_err("m + 1 = %lld knots exceed the context's m_max = %lld", (long long)(m + 1),
+            (long long)c->m_max);
+    return SGP_EINVAL;
+  }
+  std::vector<double> Ub;
+  for (int64_t t = 0; t < T; ++t) {
+    bordered_knots(U, m, ldu, c->d, cand, t, ldc, Ub);
+    double o = 0.0;
+    int st = sgp_eval_fitc(c, kernel, theta, Ub.data(), m + 1, m + 1, delta,
+                           flags | SGP_FLAG_OBJ_ONLY, &o, nullptr);
+    if (st == SGP_ENOTPD) {   // the reference's try-error
+      obj_out[t] = NAN;
+      continue;
+    }
+    if (st) return st;
+    obj_out[t] = o;
+  }
+  c->last_mode = 0;   // the context's posterior state belongs to the last candidate
+  return SGP_OK;
+}
+
+// Laplace meta-model values (knot_proposal_functions.R:1116-1160 per candidate): the last NR
+// objective value of newtrap_sparseGP at [U; cand_t], started from the same f every time.
+int sgp_lap_candidates(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
+                       int64_t ldu, double delta, double expo, double tol, int maxit,
+                       const double* cand, int64_t T, int64_t ldc, double* obj_out) {
+  if (!c || !U || !cand || T < 1 || ldc < T || !obj_out || m < 1 || ldu < m) {
+    set_err("invalid sgp_lap_candidates arguments");
+    return SGP_EINVAL;
+  }
+  if (m + 1 > c->m_max) {
+    set_err("m + 1 = %lld knots exceed the context's m_max = %lld", (long long)(m + 1),
+            (long long)c->m_max);
+    return SGP_EINVAL;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  int st = lap_ensure(c);
+  if (st) return st;
+  DevBuf f0;
+  st = dalloc(&f0.p, c->n_pad);
+  if (st) return st;
+  HIPCHK(hipMemcpyAsync(f0.p, lvec(c, LV_F), sizeof(double) * c->n_pad, hipMemcpyDeviceToDevice,
+                        c->stream));
+  std::vector<double> Ub;
+  for (int64_t t = 0; t < T && st == SGP_OK; ++t) {
+    bordered_knots(U, m, ldu, c->d, cand, t, ldc, Ub);
+    if (t > 0)
+      HIPCHK(hipMemcpyAsync(lvec(c, LV_F), f0.p, sizeof(double) * c->n_pad,
+                            hipMemcpyDeviceToDevice, c->stream));
+    double o = 0.0;
+    int it = 0;
+    st = sgp_lap_nr(c, kernel, theta, Ub.data(), m + 1, m + 1, delta, expo, tol, maxit, &o, &it);
+    if (st == SGP_ENOTPD) {
+      obj_out[t] = NAN;
+      st = SGP_OK;
+      continue;
+    }
+    if (st == SGP_OK) obj_out[t] = o;
+  }
+  HIPCHK(hipMemcpyAsync(lvec(c, LV_F), f0.p, sizeof(double) * c->n_pad, hipMemcpyDeviceToDevice,
+                        c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->last_mode = 0;   // the context's posterior state belongs to the last candidate
+  return st;
 }
 
 }  // extern "C"

@@ -59,12 +59,24 @@ def laplace_eval(cov_par, cov_fun, xu, xy, y, mu, ff=None, m=1.0, delta=1e-6, to
             "nr_iter": it}
 
 
+def _lap_ctx(cov_par, cov_fun, xu, xy, y, mu, ctx):
+    theta, names, xu_m = _prep(cov_par, cov_fun, xu, xy)
+    if ctx is None:
+        muv = _mu_vec(mu, y)
+        ctx = _context_for(xy, y, mu, xu_m.shape[0], muv)
+        ctx.set_data(y, muv)
+    return ctx, theta, xu_m
+
+
 def newtrap_sparseGP(start_vals, cov_par, cov_fun, xy, xu, y, mu, m=1.0, delta=1e-6,
                      maxit=1000, tol=1e-6, ctx=None):
     """R/newtrap_sparseGP.R:6-186 for the Poisson likelihood: {"gp",
-    "objective_function_values"} (the fused evaluation also forms the gradient at the mode)."""
-    r = laplace_eval(cov_par, cov_fun, xu, xy, y, mu, start_vals, m, delta, tol, maxit, ctx)
-    return {"gp": r["gp"], "objective_function_values": r["objective_function_values"]}
+    "objective_function_values"} (sgp_lap_nr: the NR loop alone, no gradient work)."""
+    ctx, theta, xu_m = _lap_ctx(cov_par, cov_fun, xu, xy, y, mu, ctx)
+    if start_vals is not None:
+        ctx.lap_set_f(start_vals)
+    ctx.lap_nr(theta, cov_fun, xu_m, delta, m, tol, maxit)
+    return {"gp": ctx.lap_get_f(), "objective_function_values": ctx.lap_objective_values()}
 
 
 def dlogq_dcov_par(cov_par, cov_fun, dcov_fun_dtheta=True, dcov_fun_dknot=None, knot_opt=None,
@@ -90,4 +102,7 @@ def dlogq_dcov_par(cov_par, cov_fun, dcov_fun_dtheta=True, dcov_fun_dknot=None, 
 
 def obj_fun_pois(ff, cov_par, cov_fun, xu, xy, y, mu, m=1.0, delta=1e-6, ctx=None):
     """R/laplace_approx_obj_funs.R:108-174 at ff (log q(y | theta, xu, ff))."""
-    return laplace_eval(cov_par, cov_fun, xu, xy, y, mu, ff, m, delta, 0.0, 0, ctx)["objective"]
+    ctx, theta, xu_m = _lap_ctx(cov_par, cov_fun, xu, xy, y, mu, ctx)
+    if ff is not None:
+        ctx.lap_set_f(ff)
+    return ctx.lap_nr(theta, cov_fun, xu_m, delta, m, 0.0, 0)[0]

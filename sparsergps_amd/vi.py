@@ -106,29 +106,33 @@ class SparseGPContext:
         self._last_m = U.shape[0]
         return U, U.shape[0]
 
-    def eval_vi(self, theta, cov_fun, xu, delta=1e-6, r_det=False):
-        """ELBO and d ELBO / d log(theta) with theta in [sigma, l.., tau] layout."""
+    @staticmethod
+    def _flags(r_det, obj_only):
+        return (_lib.SGP_FLAG_R_DET if r_det else 0) | (_lib.SGP_FLAG_OBJ_ONLY if obj_only else 0)
+
+    def eval_vi(self, theta, cov_fun, xu, delta=1e-6, r_det=False, obj_only=False):
+        """ELBO and d ELBO / d log(theta) with theta in [sigma, l.., tau] layout
+        (obj_only: elbo_fun alone, grad None)."""
         theta = np.ascontiguousarray(theta, dtype=np.float64)
         U, m = self._knots(xu)
         obj = C.c_double(0.0)
-        grad = np.zeros(theta.size, dtype=np.float64)
+        grad = None if obj_only else np.zeros(theta.size, dtype=np.float64)
         st = self._lib.sgp_eval_vi(self.handle, _lib.KERNELS[cov_fun], _lib.dptr(theta),
-                                   _lib.dptr(U), m, m, float(delta),
-                                   _lib.SGP_FLAG_R_DET if r_det else 0, C.byref(obj),
-                                   _lib.dptr(grad))
+                                   _lib.dptr(U), m, m, float(delta), self._flags(r_det, obj_only),
+                                   C.byref(obj), None if grad is None else _lib.dptr(grad))
         _lib.check(st)
         return obj.value, grad
 
-    def eval_fitc(self, theta, cov_fun, xu, delta=1e-6, r_det=False):
-        """FITC log marginal likelihood and d/d log(theta) (obj_fun_norm + dlogp_dcov_par)."""
+    def eval_fitc(self, theta, cov_fun, xu, delta=1e-6, r_det=False, obj_only=False):
+        """FITC log marginal likelihood and d/d log(theta) (obj_fun_norm + dlogp_dcov_par;
+        obj_only: obj_fun_norm alone, grad None)."""
         theta = np.ascontiguousarray(theta, dtype=np.float64)
         U, m = self._knots(xu)
         obj = C.c_double(0.0)
-        grad = np.zeros(theta.size, dtype=np.float64)
+        grad = None if obj_only else np.zeros(theta.size, dtype=np.float64)
         st = self._lib.sgp_eval_fitc(self.handle, _lib.KERNELS[cov_fun], _lib.dptr(theta),
-                                     _lib.dptr(U), m, m, float(delta),
-                                     _lib.SGP_FLAG_R_DET if r_det else 0, C.byref(obj),
-                                     _lib.dptr(grad))
+                                     _lib.dptr(U), m, m, float(delta), self._flags(r_det, obj_only),
+                                     C.byref(obj), None if grad is None else _lib.dptr(grad))
         _lib.check(st)
         return obj.value, grad
 
@@ -216,16 +220,57 @@ class SparseGPContext:
                                                _lib.dptr(Cd), T, T, _lib.dptr(out)))
         return out
 
+    def fitc_candidates(self, theta, cov_fun, xu, cand, delta=1e-6, r_det=False):
+        """obj_fun_norm at knots [xu; cand[t]] for every candidate row t (FITC OAT scoring)."""
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        U, m = self._knots(xu)
+        Cd = np.asfortranarray(np.asarray(cand, dtype=np.float64).reshape(-1, self.d))
+        T = Cd.shape[0]
+        out = np.zeros(T, dtype=np.float64)
+        _lib.check(self._lib.sgp_fitc_candidates(self.handle, _lib.KERNELS[cov_fun],
+                                                 _lib.dptr(theta), _lib.dptr(U), m, m,
+                                                 float(delta), self._flags(r_det, False),
+                                                 _lib.dptr(Cd), T, T, _lib.dptr(out)))
+        return out
+
+    def lap_candidates(self, theta, cov_fun, xu, cand, delta=1e-6, expo=1.0, tol=1e-5,
+                       maxit=1000):
+        """Last NR objective of newtrap_sparseGP at knots [xu; cand[t]] from the resident f, for
+        every candidate row t (Laplace OAT scoring); the resident f is left unchanged."""
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        U, m = self._knots(xu)
+        Cd = np.asfortranarray(np.asarray(cand, dtype=np.float64).reshape(-1, self.d))
+        T = Cd.shape[0]
+        out = np.zeros(T, dtype=np.float64)
+        _lib.check(self._lib.sgp_lap_candidates(self.handle, _lib.KERNELS[cov_fun],
+                                                _lib.dptr(theta), _lib.dptr(U), m, m,
+                                                float(delta), float(expo), float(tol),
+                                                int(maxit), _lib.dptr(Cd), T, T, _lib.dptr(out)))
+        return out
+
+    def lap_nr(self, theta, cov_fun, xu, delta=1e-6, expo=1.0, tol=1e-5, maxit=1000):
+        """newtrap_sparseGP alone from the resident f: (last objective value, NR iterations);
+        f is left at the mode."""
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        U, m = self._knots(xu)
+        obj = C.c_double(0.0)
+        it = C.c_int(0)
+        _lib.check(self._lib.sgp_lap_nr(self.handle, _lib.KERNELS[cov_fun], _lib.dptr(theta),
+                                        _lib.dptr(U), m, m, float(delta), float(expo), float(tol),
+                                        int(maxit), C.byref(obj), C.byref(it)))
+        return obj.value, it.value
+
     def lap_red_count(self, cov_fun, m):
         return int(self._lib.sgp_lap_red_count(_lib.KERNELS[cov_fun], self.d, int(m)))
 
-    def lap_begin(self, theta, cov_fun, xu, delta, expo, tol, maxit, red_ptr):
+    def lap_begin(self, theta, cov_fun, xu, delta, expo, tol, maxit, red_ptr, obj_only=False):
         theta = np.ascontiguousarray(theta, dtype=np.float64)
         U, m = self._knots(xu)
         cnt = C.c_int64(0)
         _lib.check(self._lib.sgp_lap_begin(self.handle, _lib.KERNELS[cov_fun], _lib.dptr(theta),
                                            _lib.dptr(U), m, m, float(delta), float(expo),
-                                           float(tol), int(maxit), C.c_void_p(red_ptr),
+                                           float(tol), int(maxit),
+                                           self._flags(False, obj_only), C.c_void_p(red_ptr),
                                            C.byref(cnt)))
         return cnt.value
 
@@ -348,8 +393,9 @@ def _knot_outputs(ctx, xu, xy, knot_opt):
     return g, trans
 
 
-def vi_eval(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6, ctx=None, r_det=False):
-    """One fused evaluation: (ELBO, OrderedDict gradient in names(cov_par) order)."""
+def vi_eval(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6, ctx=None, r_det=False, obj_only=False):
+    """One fused evaluation: (ELBO, OrderedDict gradient in names(cov_par) order; None with
+    obj_only)."""
     xy_m = np.asarray(xy, dtype=np.float64)
     d = 1 if xy_m.ndim == 1 else xy_m.shape[1]
     lnames = [f"l{c + 1}" for c in range(d)] if cov_fun == "ard" else None
@@ -358,15 +404,19 @@ def vi_eval(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6, ctx=None, r_det=False):
     xu_m = np.asarray(xu, dtype=np.float64).reshape(-1, d)
     if ctx is None:
         ctx = _context_for(xy, y, mu, xu_m.shape[0])
-    obj, g = ctx.eval_vi(theta, cov_fun, xu_m, delta, r_det=r_det)
+    obj, g = ctx.eval_vi(theta, cov_fun, xu_m, delta, r_det=r_det, obj_only=obj_only)
+    if obj_only:
+        return obj, None
     byname = dict(zip(names, g))
     grad = OrderedDict((k, float(byname[k])) for k in cov_par.keys())
     return obj, grad
 
 
-def fitc_eval(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6, ctx=None, r_det=False):
+def fitc_eval(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6, ctx=None, r_det=False,
+              obj_only=False):
     """One fused FITC evaluation: (log marginal likelihood, OrderedDict gradient) with Z and the
-    matrices built as norm_grad_ascent does (laplace_gradient_ascent.R:1238-1263)."""
+    matrices built as norm_grad_ascent does (laplace_gradient_ascent.R:1238-1263); obj_only:
+    obj_fun_norm alone (gradient None)."""
     xy_m = np.asarray(xy, dtype=np.float64)
     d = 1 if xy_m.ndim == 1 else xy_m.shape[1]
     lnames = [f"l{c + 1}" for c in range(d)] if cov_fun == "ard" else None
@@ -375,7 +425,9 @@ def fitc_eval(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6, ctx=None, r_det=False
     xu_m = np.asarray(xu, dtype=np.float64).reshape(-1, d)
     if ctx is None:
         ctx = _context_for(xy, y, mu, xu_m.shape[0])
-    obj, g = ctx.eval_fitc(theta, cov_fun, xu_m, delta, r_det=r_det)
+    obj, g = ctx.eval_fitc(theta, cov_fun, xu_m, delta, r_det=r_det, obj_only=obj_only)
+    if obj_only:
+        return obj, None
     byname = dict(zip(names, g))
     return obj, OrderedDict((k, float(byname[k])) for k in cov_par.keys())
 
@@ -403,7 +455,8 @@ def dlogp_dcov_par(cov_par, cov_fun, dcov_fun_dtheta=True, dcov_fun_dknot=None, 
 
 def elbo_fun(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6, ctx=None, r_det=False):
     """ELBO value (vi_functions.R:64-121) at (cov_par, xu)."""
-    return vi_eval(cov_par, cov_fun, xu, xy, y, mu, delta, ctx=ctx, r_det=r_det)[0]
+    return vi_eval(cov_par, cov_fun, xu, xy, y, mu, delta, ctx=ctx, r_det=r_det,
+                   obj_only=True)[0]
 
 
 def delbo_dcov_par(cov_par, cov_fun, dcov_fun_dtheta=True, dcov_fun_dknot=None, knot_opt=None,
