@@ -20,7 +20,11 @@ namespace {
 constexpr int T128 = 128;
 constexpr int BK = 16;
 constexpr int SB = 144;   // LDS row stride (doubles) of [k][128] operand images: 2*144 % 64 == 32
-constexpr int SA = 18;    // LDS row stride of the [128][16] A image: conflict-free f64 reads
+// LDS row stride of the [128][16] A image.  Odd, because hipcc fuses the A-fragment reads of
+// two k-substeps into ds_read2_b64, which banks 16-lane groups mod 32 dwords: an even stride of
+// 18 put rows r and r+8 on one bank (2-way conflicts on every A read); 17 is conflict-free for
+// ds_read2_b64 and ds_write_b64 alike (rows are then 8-byte aligned only: no b128 stores)
+constexpr int SA = 17;
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -82,10 +86,12 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
 
-  // loader mapping: 16 rows x 128 cols, 8 doubles per thread
-  const int lrow = tid >> 4, lcol = (tid & 15) * 8;
-  const double2* gA = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + ta * (int64_t)T128 + lcol);
-  const double2* gB = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + tb * (int64_t)T128 + lcol);
+  // loader mapping: 16 rows x 128 cols, 4 double2 per thread at double2 columns lc + 16 q, so
+  // 8 consecutive lanes store 128 contiguous bytes (conflict-free ds_write_b128; 8 doubles per
+  // thread contiguous gave 4-way bank conflicts on every store)
+  const int lrow = tid >> 4, lc = tid & 15;
+  const double2* gA = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + ta * (int64_t)T128) + lc;
+  const double2* gB = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + tb * (int64_t)T128) + lc;
   const int64_t gstep = BK * mp / 2;   // double2 stride of one k-step
   double2 va0, va1, va2, va3, vb0, vb1, vb2, vb3;
   double vr = 0.0, wi = 1.0, vrr = 0.0;
@@ -95,8 +101,8 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
 #define SYRK_GLOAD(step)                                                        \
   {                                                                             \
     const int64_t o_ = (int64_t)(step) * gstep;                                 \
-    va0 = gA[o_]; va1 = gA[o_ + 1]; va2 = gA[o_ + 2]; va3 = gA[o_ + 3];         \
-    vb0 = gB[o_]; vb1 = gB[o_ + 1]; vb2 = gB[o_ + 2]; vb3 = gB[o_ + 3];         \
+    va0 = gA[o_]; va1 = gA[o_ + 16]; va2 = gA[o_ + 32]; va3 = gA[o_ + 48];      \
+    vb0 = gB[o_]; vb1 = gB[o_ + 16]; vb2 = gB[o_ + 32]; vb3 = gB[o_ + 48];      \
     if (w != nullptr) wi = w[rbeg + (int64_t)(step) * BK + lrow];               \
     if (tid < BK) {                                                             \
       const int64_t rr_ = rbeg + (int64_t)(step) * BK + tid;                    \
@@ -107,13 +113,13 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
   }
 #define SYRK_SSTORE(buf)                                                        \
   {                                                                             \
-    double2* pa_ = reinterpret_cast<double2*>(&Ka[buf][lrow * SB + lcol]);      \
-    double2* pb_ = reinterpret_cast<double2*>(&Kb[buf][lrow * SB + lcol]);      \
+    double2* pa_ = reinterpret_cast<double2*>(&Ka[buf][lrow * SB]) + lc;        \
+    double2* pb_ = reinterpret_cast<double2*>(&Kb[buf][lrow * SB]) + lc;        \
     pa_[0] = make_double2(va0.x * wi, va0.y * wi);                              \
-    pa_[1] = make_double2(va1.x * wi, va1.y * wi);                              \
-    pa_[2] = make_double2(va2.x * wi, va2.y * wi);                              \
-    pa_[3] = make_double2(va3.x * wi, va3.y * wi);                              \
-    pb_[0] = vb0; pb_[1] = vb1; pb_[2] = vb2; pb_[3] = vb3;                     \
+    pa_[16] = make_double2(va1.x * wi, va1.y * wi);                             \
+    pa_[32] = make_double2(va2.x * wi, va2.y * wi);                             \
+    pa_[48] = make_double2(va3.x * wi, va3.y * wi);                             \
+    pb_[0] = vb0; pb_[16] = vb1; pb_[32] = vb2; pb_[48] = vb3;                  \
     if (tid < BK) { rw[buf][tid] = vr; rv[buf][tid] = vrr; }                    \
   }
 
@@ -199,23 +205,23 @@ k_gemm_tn(const double* __restrict__ A, int64_t lda, const double* __restrict__ 
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-  const int lrow = tid >> 4, lcol = (tid & 15) * 8;
-  const double2* gA = reinterpret_cast<const double2*>(A + (rbeg + lrow) * lda + ta * (int64_t)T128 + lcol);
-  const double2* gB = reinterpret_cast<const double2*>(B + (rbeg + lrow) * ldb + tb * (int64_t)T128 + lcol);
+  const int lrow = tid >> 4, lc = tid & 15;   // double2 columns lc + 16 q (as k_syrk)
+  const double2* gA = reinterpret_cast<const double2*>(A + (rbeg + lrow) * lda + ta * (int64_t)T128) + lc;
+  const double2* gB = reinterpret_cast<const double2*>(B + (rbeg + lrow) * ldb + tb * (int64_t)T128) + lc;
   const int64_t sa = BK * lda / 2, sb = BK * ldb / 2;
   double2 va0, va1, va2, va3, vb0, vb1, vb2, vb3;
 #define TN_GLOAD(step)                                                          \
   {                                                                             \
     const int64_t oa_ = (int64_t)(step) * sa, ob_ = (int64_t)(step) * sb;       \
-    va0 = gA[oa_]; va1 = gA[oa_ + 1]; va2 = gA[oa_ + 2]; va3 = gA[oa_ + 3];     \
-    vb0 = gB[ob_]; vb1 = gB[ob_ + 1]; vb2 = gB[ob_ + 2]; vb3 = gB[ob_ + 3];     \
+    va0 = gA[oa_]; va1 = gA[oa_ + 16]; va2 = gA[oa_ + 32]; va3 = gA[oa_ + 48];  \
+    vb0 = gB[ob_]; vb1 = gB[ob_ + 16]; vb2 = gB[ob_ + 32]; vb3 = gB[ob_ + 48];  \
   }
 #define TN_SSTORE(buf)                                                          \
   {                                                                             \
-    double2* pa_ = reinterpret_cast<double2*>(&Ka[buf][lrow * SB + lcol]);      \
-    double2* pb_ = reinterpret_cast<double2*>(&Kb[buf][lrow * SB + lcol]);      \
-    pa_[0] = va0; pa_[1] = va1; pa_[2] = va2; pa_[3] = va3;                     \
-    pb_[0] = vb0; pb_[1] = vb1; pb_[2] = vb2; pb_[3] = vb3;                     \
+    double2* pa_ = reinterpret_cast<double2*>(&Ka[buf][lrow * SB]) + lc;        \
+    double2* pb_ = reinterpret_cast<double2*>(&Kb[buf][lrow * SB]) + lc;        \
+    pa_[0] = va0; pa_[16] = va1; pa_[32] = va2; pa_[48] = va3;                  \
+    pb_[0] = vb0; pb_[16] = vb1; pb_[32] = vb2; pb_[48] = vb3;                  \
   }
   if (nsteps > 0) {
     TN_GLOAD(0);
@@ -330,7 +336,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   const double* __restrict__ r = ca.r;
   const double* __restrict__ uvec = ca.uvec;
   const double* __restrict__ cdiag = ca.cdiag;
-  constexpr int A_SZ = T128 * SA;   // 2304
+  constexpr int A_SZ = T128 * SA;   // 2176 (keeps the B image 16-byte aligned)
   constexpr int B_SZ = BK * SB;     // 2304
   __shared__ __attribute__((aligned(16))) double lds[2 * (A_SZ + B_SZ)];
   __shared__ double red[4][SGP_MAXD + 4];
@@ -356,9 +362,10 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   // A loader: 128 rows x 16 k, thread -> (row = tid>>1, 8 doubles at (tid&1)*8)
   const int arow = tid >> 1, acol = (tid & 1) * 8;
   const double2* gA = reinterpret_cast<const double2*>(K + (i0 + arow) * mp + acol);
-  // B loader: 16 k x 128 cols, thread -> (k = tid>>4, 8 doubles at (tid&15)*8)
-  const int bk = tid >> 4, bcol = (tid & 15) * 8;
-  const double2* gB = reinterpret_cast<const double2*>(M + (int64_t)bk * mp + j0 + bcol);
+  // B loader: 16 k x 128 cols, thread -> (k = tid>>4, double2 columns (tid&15) + 16 q):
+  // 8 consecutive lanes store 128 contiguous bytes (conflict-free ds_write_b128)
+  const int bk = tid >> 4, bc = tid & 15;
+  const double2* gB = reinterpret_cast<const double2*>(M + (int64_t)bk * mp + j0) + bc;
   const int64_t bstep = BK * mp / 2;
   double2 va0, va1, va2, va3, vb0, vb1, vb2, vb3;
   const int nsteps = (int)(mp / BK);
@@ -372,16 +379,17 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   {                                                                              \
     const int64_t oa_ = (int64_t)(step) * (BK / 2), ob_ = (int64_t)(step) * bstep; \
     va0 = gA[oa_]; va1 = gA[oa_ + 1]; va2 = gA[oa_ + 2]; va3 = gA[oa_ + 3];      \
-    vb0 = gB[ob_]; vb1 = gB[ob_ + 1]; vb2 = gB[ob_ + 2]; vb3 = gB[ob_ + 3];      \
+    vb0 = gB[ob_]; vb1 = gB[ob_ + 16]; vb2 = gB[ob_ + 32]; vb3 = gB[ob_ + 48];   \
     if (with_u && tid < BK) vuk = uvec[(int64_t)(step) * BK + tid];              \
   }
 #define CON_SSTORE(buf)                                                          \
   {                                                                              \
     double* As_ = lds + (buf) * (A_SZ + B_SZ);                                   \
-    double2* pa_ = reinterpret_cast<double2*>(&As_[arow * SA + acol]);           \
-    double2* pb_ = reinterpret_cast<double2*>(&As_[A_SZ + bk * SB + bcol]);      \
-    pa_[0] = va0; pa_[1] = va1; pa_[2] = va2; pa_[3] = va3;                      \
-    pb_[0] = vb0; pb_[1] = vb1; pb_[2] = vb2; pb_[3] = vb3;                      \
+    double* pa_ = &As_[arow * SA + acol];                                        \
+    double2* pb_ = reinterpret_cast<double2*>(&As_[A_SZ + bk * SB]) + bc;        \
+    pa_[0] = va0.x; pa_[1] = va0.y; pa_[2] = va1.x; pa_[3] = va1.y;              \
+    pa_[4] = va2.x; pa_[5] = va2.y; pa_[6] = va3.x; pa_[7] = va3.y;              \
+    pb_[0] = vb0; pb_[16] = vb1; pb_[32] = vb2; pb_[48] = vb3;                   \
     if (with_u && tid < BK) s_uk[buf][tid] = vuk;                                \
   }
 #define CON_KU(buf)                                                              \
@@ -432,7 +440,9 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   double* s_beta = s_cd + T128;             // 128
   double* s_v = s_beta + T128;              // 128
   double* s_xs = s_v + T128;                // 128 x d   ([row][c], scaled)
-  double* s_us = s_xs + T128 * kp.d;        // 128 x d   ([col][c], scaled)
+  // s_xs: [row][c] scaled rows (128 x d), or for DT == 8 the MFMA B image [x~ | x~^2] (128 x 16)
+  double* s_us = s_xs + T128 * (DT == 8 ? 16 : kp.d);   // 128 x (d|1) ([col][c], scaled; odd
+                                                      // stride: 16 columns on distinct banks)
   ku += __shfl_xor(ku, 1, 64);                       // the two halves of row `arow`
   double a2 = 0.0;                                    // alpha^2, counted once (tj == 0)
   if ((tid & 1) == 0) {
@@ -483,91 +493,195 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   } else {
     // ---------------- gradient epilogue ----------------
     const int d = kp.d;
+    const int sus = d | 1;
     const bool ard = (kp.kernel == 1);
     const double rl2s = kp.rl2[0];
+    const int L = kp.L;
     for (int e = tid; e < T128; e += 256) {
       const int64_t j = j0 + e;
       s_u[e] = (uvec && j < m) ? uvec[j] : 0.0;
       s_v[e] = (with_v && j < m) ? ca.vvec[j] : 0.0;
       s_cd[e] = (cdiag && j < m) ? cdiag[j] : 0.0;
     }
-    for (int e = tid; e < T128 * d; e += 256) {
-      const int rr = e % T128, c = e / T128;
-      const int64_t i = i0 + rr, j = j0 + rr;
-      const double sc = ard ? kp.rl[c] : 1.0;
-      s_xs[rr * d + c] = (i < n) ? X[i + c * ldx] * sc : 0.0;
-      s_us[rr * d + c] = (j < m) ? U[j + c * ldu] * sc : 0.0;
-    }
-    __syncthreads();
-
-    const int L = kp.L;
-    double* s_kn = s_us + T128 * d;           // KNOT: [2 (wr)][128 cols][d]
-    double e_sig = 0.0, c_sum = 0.0, c_cnt = 0.0, c_dg = 0.0;
+    double e_sig = 0.0;
     double e_l[DT];
 #pragma unroll
     for (int c = 0; c < DT; ++c) e_l[c] = 0.0;
+    double* s_kn;
 
-#pragma unroll
-    for (int fn = 0; fn < 4; ++fn) {
-      const int col = wc * 64 + fn * 16 + (lane & 15);
-      const bool cvalid = (j0 + col) < m;
+    if constexpr (DT == 8) {
+      // MFMA epilogue.  With W = G o K (zero outside (n, m)) and x~, u~ the (ARD-scaled)
+      // coordinates, every per-pair sum the gradient needs is a small product over rows:
+      //   D[j][c']   = sum_i W_ij XB_ic',  XB = [x~ | x~^2]  (c' < 8 | c' >= 8)
+      //   C_j        = sum_i W_ij
+      //   e_l[c]     = sum_ij W_ij (x~_ic - u~_jc)^2 = sum_j D[j][8+c] - 2 u~_jc D[j][c] + u~_jc^2 C_j
+      //   knot (j,c) = sum_i W_ij (x~_ic - u~_jc)   = D[j][c] - u~_jc C_j
+      // The C fragment of K P is read directly as the A operand of v_mfma_f64_16x16x4 (its lane
+      // map is that of W^T), so D costs 4 MFMAs per 16x16 fragment instead of ~3 d VALU ops
+      // per pair.
+      for (int e = tid; e < T128 * 8; e += 256) {
+        const int rr = e % T128, c = e / T128;
+        const int64_t i = i0 + rr, j = j0 + rr;
+        double xv = 0.0;
+        if (c < d) {
+          const double sc = ard ? kp.rl[c] : 1.0;
+          xv = (i < n) ? X[i + c * ldx] * sc : 0.0;
+          s_us[rr * sus + c] = (j < m) ? U[j + c * ldu] * sc : 0.0;
+        }
+        s_xs[rr * 16 + c] = xv;
+        s_xs[rr * 16 + 8 + c] = xv * xv;
+      }
+      __syncthreads();
+      s_kn = s_us + T128 * sus;                // KNOT: [2 (wr)][128 cols][d]
 
-      double uj[DT];
+      d4 P[4];
+      double Cc[4], ucol[4], vcol[4];
+      bool cval[4];
 #pragma unroll
-      for (int c = 0; c < DT; ++c) uj[c] = (c < d) ? s_us[col * d + c] : 0.0;
-      const double ucol = s_u[col];
-      const double vcol = with_v ? s_v[col] : 0.0;
-      double kn[DT];
-      if constexpr (KNOT) {
-#pragma unroll
-        for (int c = 0; c < DT; ++c) kn[c] = 0.0;
+      for (int fn = 0; fn < 4; ++fn) {
+        const int col = wc * 64 + fn * 16 + (lane & 15);
+        P[fn] = d4{0.0, 0.0, 0.0, 0.0};
+        Cc[fn] = 0.0;
+        cval[fn] = (j0 + col) < m;
+        ucol[fn] = s_u[col];
+        vcol[fn] = with_v ? s_v[col] : 0.0;
       }
 #pragma unroll
       for (int fm = 0; fm < 4; ++fm) {
-        // the fragment's 4 K values (K is zero-padded: every address valid)
-        double kv[4];
+        double xb[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          kv[q] = Kt[(int64_t)(wr * 64 + fm * 16 + (lane >> 4) + 4 * q) * mp + col];
+        for (int r4 = 0; r4 < 4; ++r4)
+          xb[r4] = s_xs[(wr * 64 + fm * 16 + 4 * r4 + (lane >> 4)) * 16 + (lane & 15)];
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn) {
+          const int col = wc * 64 + fn * 16 + (lane & 15);
+          double kv[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            kv[q] = Kt[(int64_t)(wr * 64 + fm * 16 + (lane >> 4) + 4 * q) * mp + col];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
+            const bool valid = cval[fn] && ((i0 + row) < n);
+            double G = s_rs[row] * acc[fm][fn][q];
+            if constexpr (V2) G = fma(s_beta[row], vcol[fn], G);
+            G = fma(s_alpha[row], ucol[fn], G);
+            const double w = valid ? G * kv[q] : 0.0;
+            Cc[fn] += w;
+            acc[fm][fn][q] = w;
+          }
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4)
+            P[fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[fm][fn][r4], xb[r4], P[fn], 0, 0, 0);
+        }
+      }
+      // D fragment fn: lane l, register q -> column wc*64 + fn*16 + (l>>4) + 4q, c' = l & 15
+      const int cp = lane & 15, cc = cp & 7;
+      double E = 0.0;
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn) {
+        double C = Cc[fn];
+        C += __shfl_xor(C, 16, 64);
+        C += __shfl_xor(C, 32, 64);            // every lane: C of column (lane & 15)
+        if ((lane >> 4) == 0) e_sig += C;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
-          const bool valid = cvalid && ((i0 + row) < n);
-          double G = s_rs[row] * acc[fm][fn][q];
-          if constexpr (V2) G = fma(s_beta[row], vcol, G);
-          G = fma(s_alpha[row], ucol, G);
-          const double gk = valid ? G * kv[q] : 0.0;
-          e_sig += gk;
-          const double* xr = &s_xs[row * d];
-          double s = 0.0;
+          const int jl = wc * 64 + fn * 16 + (lane >> 4) + 4 * q;
+          const double Cq = __shfl(C, (lane >> 4) + 4 * q, 64);
+          const double u = (cc < d) ? s_us[jl * sus + cc] : 0.0;
+          const double pv = P[fn][q];
+          E += (cp >= 8) ? pv : u * fma(u, Cq, -2.0 * pv);
+          if constexpr (KNOT) {
+            if (cp < 8 && cc < d) s_kn[(wr * T128 + jl) * d + cc] = pv - u * Cq;
+          }
+        }
+      }
+      E += __shfl_xor(E, 8, 64);
+      E += __shfl_xor(E, 16, 64);
+      E += __shfl_xor(E, 32, 64);              // lanes c (0..7): sum_ij W_ij (x~_ic - u~_jc)^2
+      if (ard) {
+#pragma unroll
+        for (int c = 0; c < DT; ++c) e_l[c] = __shfl(E, c, 64);
+      } else {
+        double t = E;
+        t += __shfl_xor(t, 1, 64);
+        t += __shfl_xor(t, 2, 64);
+        t += __shfl_xor(t, 4, 64);
+        e_l[0] = t * rl2s;
+      }
+    } else {
+      for (int e = tid; e < T128 * d; e += 256) {
+        const int rr = e % T128, c = e / T128;
+        const int64_t i = i0 + rr, j = j0 + rr;
+        const double sc = ard ? kp.rl[c] : 1.0;
+        s_xs[rr * d + c] = (i < n) ? X[i + c * ldx] * sc : 0.0;
+        s_us[rr * sus + c] = (j < m) ? U[j + c * ldu] * sc : 0.0;
+      }
+      __syncthreads();
+      s_kn = s_us + T128 * sus;
+
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn) {
+        const int col = wc * 64 + fn * 16 + (lane & 15);
+        const bool cvalid = (j0 + col) < m;
+
+        double uj[DT];
+#pragma unroll
+        for (int c = 0; c < DT; ++c) uj[c] = (c < d) ? s_us[col * sus + c] : 0.0;
+        const double ucol = s_u[col];
+        const double vcol = with_v ? s_v[col] : 0.0;
+        double kn[DT];
+        if constexpr (KNOT) {
+#pragma unroll
+          for (int c = 0; c < DT; ++c) kn[c] = 0.0;
+        }
+#pragma unroll
+        for (int fm = 0; fm < 4; ++fm) {
+          // the fragment's 4 K values (K is zero-padded: every address valid)
+          double kv[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            kv[q] = Kt[(int64_t)(wr * 64 + fm * 16 + (lane >> 4) + 4 * q) * mp + col];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
+            const bool valid = cvalid && ((i0 + row) < n);
+            double G = s_rs[row] * acc[fm][fn][q];
+            if constexpr (V2) G = fma(s_beta[row], vcol, G);
+            G = fma(s_alpha[row], ucol, G);
+            const double gk = valid ? G * kv[q] : 0.0;
+            e_sig += gk;
+            const double* xr = &s_xs[row * d];
+            double s2 = 0.0;
+#pragma unroll
+            for (int c = 0; c < DT; ++c) {
+              if (c < d) {
+                const double t = xr[c] - uj[c];
+                const double tt = t * t;
+                s2 += tt;
+                if (ard) e_l[c] = fma(gk, tt, e_l[c]);
+                if constexpr (KNOT) kn[c] = fma(gk, t, kn[c]);
+              }
+            }
+            if (!ard) e_l[0] = fma(gk, s2 * rl2s, e_l[0]);
+            // tau's coincidence sums (x_i == u_j exactly) are not accumulated here: k_coinc
+            // finds those pairs by hash and recomputes their G_ij (launch_coinc)
+          }
+        }
+        if constexpr (KNOT) {
+          // column sums over this wave's 64 rows: the 4 lanes sharing (lane & 15)
 #pragma unroll
           for (int c = 0; c < DT; ++c) {
             if (c < d) {
-              const double t = xr[c] - uj[c];
-              const double tt = t * t;
-              s += tt;
-              if (ard) e_l[c] = fma(gk, tt, e_l[c]);
-              if constexpr (KNOT) kn[c] = fma(gk, t, kn[c]);
+              double v2 = kn[c];
+              v2 += __shfl_xor(v2, 16, 64);
+              v2 += __shfl_xor(v2, 32, 64);
+              if ((lane >> 4) == 0) s_kn[(wr * T128 + col) * d + c] = v2;
             }
           }
-          if (!ard) e_l[0] = fma(gk, s * rl2s, e_l[0]);
-          // tau's coincidence sums (x_i == u_j exactly) are not accumulated here: k_coinc
-          // finds those pairs by hash and recomputes their G_ij (launch_coinc)
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      if constexpr (KNOT) {
-        // column sums over this wave's 64 rows: the 4 lanes sharing (lane & 15)
-#pragma unroll
-        for (int c = 0; c < DT; ++c) {
-          if (c < d) {
-            double v2 = kn[c];
-            v2 += __shfl_xor(v2, 16, 64);
-            v2 += __shfl_xor(v2, 32, 64);
-            if ((lane >> 4) == 0) s_kn[(wr * T128 + col) * d + c] = v2;
-          }
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (KNOT) {
       __syncthreads();
@@ -579,24 +693,24 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     }
 
     // record = [e_sig, e_l[0..L-1], c_sum, c_cnt, c_dg, alpha^T alpha]
+    // (the coincidence fields stay zero here; k_coinc adds them)
     double v;
     v = wave_sum(e_sig);
     if (lane == 0) red[wv][0] = v;
 #pragma unroll
     for (int c = 0; c < DT; ++c) {
       if (c < L) {
-        v = wave_sum(e_l[c]);
+        v = (DT == 8) ? e_l[c] : wave_sum(e_l[c]);   // DT == 8: already wave totals
         if (lane == 0) red[wv][1 + c] = v;
       }
     }
-    v = wave_sum(c_sum);
-    if (lane == 0) red[wv][1 + L] = v;
-    v = wave_sum(c_cnt);
-    if (lane == 0) red[wv][2 + L] = v;
-    v = wave_sum(c_dg);
-    if (lane == 0) red[wv][3 + L] = v;
     v = wave_sum(a2);
-    if (lane == 0) red[wv][4 + L] = v;
+    if (lane == 0) {
+      red[wv][1 + L] = 0.0;
+      red[wv][2 + L] = 0.0;
+      red[wv][3 + L] = 0.0;
+      red[wv][4 + L] = v;
+    }
     __syncthreads();
     if (tid < nrec)
       slab[wgid * nrec + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
