@@ -241,9 +241,12 @@ int sgp_lap_candidates(sgp_ctx* ctx, int kernel, const double* theta, const doub
                        int64_t ldu, double delta, double expo, double tol, int maxit,
                        const double* cand, int64_t T, int64_t ldc, double* obj_out);
 
-/* Per-kernel timing of the last evaluation (HIP events on the launch stream).
- * names: '\n'-separated kernel-phase names; ms: their durations (max n entries). */
+/* Per-phase timing (HIP events on the launch stream).  Enabling clears the record; every
+ * evaluation after it appends its phases, and sgp_ctx_timings returns the per-phase totals
+ * over those sgp_ctx_timing_evals() evaluations (names: '\n'-separated phase names; ms: their
+ * total durations, max n entries).  Nothing is read back while evaluations run. */
 int sgp_ctx_enable_timing(sgp_ctx* ctx, int enable);
+int64_t sgp_ctx_timing_evals(const sgp_ctx* ctx);
 int sgp_ctx_timings(sgp_ctx* ctx, char* names, int64_t names_len, double* ms, int max_n, int* count);
 
 #ifdef __cplusplus

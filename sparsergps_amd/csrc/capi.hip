@@ -133,6 +133,10 @@ struct sgp_ctx {
   double *knot_slab = nullptr, *knot_part = nullptr, *knot_kmm = nullptr;
   std::vector<double> knot_raw;           // d F / d u (m x d, row-major), before the chain factor
   std::vector<double> hU;                 // host copy of the knots (m x d, column-major)
+  double* pin = nullptr;                  // pinned staging for knot uploads
+  hipEvent_t ev_pin = nullptr;            // the last upload's copies have been issued before it
+  bool knots_valid = false;               // c->U / khash / kidx hold hU (layout knots_mp)
+  int64_t knots_mp = 0;
   uint64_t* khash = nullptr;              // sorted knot coordinate hashes (k_coinc)
   int* kidx = nullptr;                    // knot index of each sorted hash
   std::vector<double> xmin, xmax;         // column ranges of this context's rows
@@ -161,6 +165,7 @@ struct sgp_ctx {
   std::vector<double> lap_objs;           // objective_function_values of the last NR run
   // timing
   bool timing = false;
+  int64_t timing_evals = 0;               // evaluations recorded since timing was enabled
   std::vector<Timer> timers;
   std::vector<hipEvent_t> pool;
   size_t pool_used = 0;
@@ -174,6 +179,34 @@ constexpr int SC_N = 64;
 // per-block partials of the small reductions: k_contract_kmm writes up to 1024 blocks x (P-1)
 // records (P <= SGP_MAXD + 2), the dot/colsum helpers at most 1024 x 1
 constexpr int SLAB_SMALL = 1024 * (SGP_MAXD + 2);
+constexpr int KNOT_PART_ROWS = 256;   // row groups of the knot / t column-sum first pass
+constexpr int RB_N = 256;             // pinned readback doubles at the end of c->pin
+
+// The end-of-evaluation D2H copies land in pinned memory (true async DMA, one synchronisation)
+// and are unpacked into the caller's host arrays afterwards.
+struct Readback {
+  sgp_ctx* c;
+  double* base;
+  size_t off = 0;
+  struct Item { void* host; size_t off, bytes; };
+  std::vector<Item> items;
+  explicit Readback(sgp_ctx* ctx)
+      : c(ctx), base(ctx->pin + ctx->mp_max * ctx->d + ctx->m_max + (ctx->m_max + 1) / 2 + 8) {}
+  hipError_t add(void* host, const void* dev, size_t bytes) {
+    if (off + bytes > sizeof(double) * RB_N) return hipErrorInvalidValue;
+    items.push_back({host, off, bytes});
+    hipError_t e = hipMemcpyAsync(reinterpret_cast<char*>(base) + off, dev, bytes,
+                                  hipMemcpyDeviceToHost, c->stream);
+    off += (bytes + 7) & ~size_t(7);
+    return e;
+  }
+  hipError_t wait() {
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return e;
+    for (const Item& it : items) memcpy(it.host, reinterpret_cast<char*>(base) + it.off, it.bytes);
+    return hipSuccess;
+  }
+};
 
 hipEvent_t pool_event(sgp_ctx* c) {
   if (c->pool_used < c->pool.size()) return c->pool[c->pool_used++];
@@ -205,7 +238,13 @@ struct Scope {
   }
 };
 
+// start of an evaluation: with timing on, its scopes are appended to those of the earlier
+// evaluations (read out once, after the timed loop, by sgp_ctx_timings)
 void timers_reset(sgp_ctx* c) {
+  if (c->timing) {
+    ++c->timing_evals;
+    return;
+  }
   c->timers.clear();
   c->pool_used = 0;
 }
@@ -240,6 +279,8 @@ void ctx_free(sgp_ctx* c) {
   if (c->g_k22) hipGraphExecDestroy(c->g_k22);
   if (c->g_k22_graph) hipGraphDestroy(c->g_k22_graph);
   if (c->ev_knots) hipEventDestroy(c->ev_knots);
+  if (c->ev_pin) hipEventDestroy(c->ev_pin);
+  if (c->pin) hipHostFree(c->pin);
   if (c->ev_k22) hipEventDestroy(c->ev_k22);
   if (c->aux) hipStreamDestroy(c->aux);
   for (hipEvent_t e : c->pool) hipEventDestroy(e);
@@ -270,28 +311,42 @@ uint64_t coord_hash_host(const double* x, int64_t stride, int d) {
 }
 
 int upload_knots(sgp_ctx* c, const double* U, int64_t m, int64_t ldu) {
+  // optimizer iterations with fixed knots (xu_opt = "fixed") pass the same U every time: keep
+  // the resident copy and its hash table
+  if (c->knots_valid && c->knots_mp == c->mp && (int64_t)c->hU.size() == m * c->d) {
+    bool same = true;
+    for (int q = 0; q < c->d && same; ++q)
+      same = memcmp(&c->hU[(size_t)(q * m)], U + q * ldu, sizeof(double) * m) == 0;
+    if (same) return SGP_OK;
+  }
+  c->knots_valid = false;
+  // staging through pinned host memory, copies async on the context stream; the previous
+  // upload's copies must have drained before the buffer is rewritten
+  HIPCHK(hipEventSynchronize(c->ev_pin));
+  double* hU_dev = c->pin;                                        // mp x d (device layout)
+  uint64_t* hh = reinterpret_cast<uint64_t*>(c->pin + c->mp_max * c->d);
+  int* hi = reinterpret_cast<int*>(hh + c->m_max);
   {
     std::vector<std::pair<uint64_t, int>> hk((size_t)m);
     for (int64_t j = 0; j < m; ++j) hk[(size_t)j] = {coord_hash_host(U + j, ldu, c->d), (int)j};
     std::sort(hk.begin(), hk.end());
-    std::vector<uint64_t> hh((size_t)m);
-    std::vector<int> hi((size_t)m);
     for (int64_t j = 0; j < m; ++j) {
-      hh[(size_t)j] = hk[(size_t)j].first;
-      hi[(size_t)j] = hk[(size_t)j].second;
+      hh[j] = hk[(size_t)j].first;
+      hi[j] = hk[(size_t)j].second;
     }
-    HIPCHK(hipMemcpy(c->khash, hh.data(), sizeof(uint64_t) * m, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->kidx, hi.data(), sizeof(int) * m, hipMemcpyHostToDevice));
   }
   c->hU.assign((size_t)(m * c->d), 0.0);
   for (int q = 0; q < c->d; ++q)
     for (int64_t j = 0; j < m; ++j) c->hU[(size_t)(j + q * m)] = U[j + q * ldu];
-  std::vector<double> h((size_t)(c->mp * c->d), 0.0);
   for (int q = 0; q < c->d; ++q)
-    for (int64_t j = 0; j < m; ++j) h[(size_t)(q * c->mp + j)] = U[j + q * ldu];
-  HIPCHK(hipMemcpyAsync(c->U, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice,
+    for (int64_t j = 0; j < c->mp; ++j) hU_dev[q * c->mp + j] = j < m ? U[j + q * ldu] : 0.0;
+  HIPCHK(hipMemcpyAsync(c->khash, hh, sizeof(uint64_t) * m, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->kidx, hi, sizeof(int) * m, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->U, hU_dev, sizeof(double) * c->mp * c->d, hipMemcpyHostToDevice,
                         c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));  // h goes out of scope
+  HIPCHK(hipEventRecord(c->ev_pin, c->stream));
+  c->knots_valid = true;
+  c->knots_mp = c->mp;
   return SGP_OK;
 }
 
@@ -482,7 +537,7 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   }
   if (getenv("SGP_GRAPHS") && !getenv("SGP_NO_GRAPHS")) c->use_graphs = true;
   c->slab_syrk_cap = syrk_slab_doubles(np_, mp);
-  c->slab_con_cap = (np_ / SGP_TILE) * (mp / SGP_TILE) * (SGP_MAXD + 4);
+  c->slab_con_cap = (np_ / SGP_TILE) * (mp / SGP_TILE) * (SGP_MAXD + 5);   // nrec <= L + 5
   st = st ? st : dalloc(&c->X, np_ * d);
   st = st ? st : dalloc(&c->r, np_);
   st = st ? st : dalloc(&c->K, np_ * mp);
@@ -521,6 +576,13 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->tslab, (np_ / 64) * mp);
   st = st ? st : dalloc(&c->khash, mp);
   st = st ? st : dalloc(&c->kidx, mp);
+  if (!st && (hipHostMalloc(reinterpret_cast<void**>(&c->pin),
+                            sizeof(double) * (mp * d + m_max + (m_max + 1) / 2 + 8 + RB_N),
+                            hipHostMallocDefault) != hipSuccess ||
+              hipEventCreateWithFlags(&c->ev_pin, hipEventDisableTiming) != hipSuccess)) {
+    set_err("pinned staging allocation failed");
+    st = SGP_ENOMEM;
+  }
   if (st) {
     ctx_free(c);
     delete c;
@@ -593,8 +655,15 @@ int64_t sgp_ctx_rows(const sgp_ctx* c) { return c ? c->n : -1; }
 int sgp_ctx_enable_timing(sgp_ctx* c, int enable) {
   if (!c) return SGP_EINVAL;
   c->timing = enable != 0;
+  if (c->timing) {
+    c->timers.clear();
+    c->pool_used = 0;
+    c->timing_evals = 0;
+  }
   return SGP_OK;
 }
+
+int64_t sgp_ctx_timing_evals(const sgp_ctx* c) { return c ? c->timing_evals : -1; }
 
 int sgp_ctx_timings(sgp_ctx* c, char* names, int64_t names_len, double* ms, int max_n,
                     int* count) {
@@ -602,16 +671,26 @@ int sgp_ctx_timings(sgp_ctx* c, char* names, int64_t names_len, double* ms, int 
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipStreamSynchronize(c->aux));
-  std::string all;
-  int k = 0;
+  // per-phase totals over the recorded evaluations, in first-seen order
+  std::vector<std::string> nm;
+  std::vector<double> tot;
   for (const Timer& t : c->timers) {
-    if (k >= max_n) break;
     float v = 0.f;
     HIPCHK(hipEventElapsedTime(&v, t.a, t.b));
-    if (ms) ms[k] = v;
-    all += t.name;
+    size_t q = 0;
+    while (q < nm.size() && nm[q] != t.name) ++q;
+    if (q == nm.size()) {
+      nm.push_back(t.name);
+      tot.push_back(0.0);
+    }
+    tot[q] += v;
+  }
+  std::string all;
+  int k = 0;
+  for (size_t q = 0; q < nm.size() && k < max_n; ++q, ++k) {
+    if (ms) ms[k] = tot[q];
+    all += nm[q];
     all += '\n';
-    ++k;
   }
   *count = k;
   if (names && names_len > 0) {
@@ -641,13 +720,14 @@ static int contract_pass(sgp_ctx* c, const double* M, ConArgs ca, double* rec_ou
   if (fused) ca.alpha_out = c->alpha;   // k_coinc needs the fused alpha_i
   HIPCHK(launch_contract_args(c->kp, c->K, M, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp, c->m,
                               c->mp, ca, c->slab_con, &nrec, &nwg, c->stream));
-  HIPCHK(launch_colsum(c->slab_con, nwg, nrec, rec_out, c->stream));
+  HIPCHK(launch_rowsum(c->slab_con, nrec, nwg, c->slab_small, SLAB_SMALL, rec_out, c->stream));
   // tau's coincidence sums -> record fields 1+L .. 3+L
   HIPCHK(launch_coinc(c->X, c->n_pad, c->n, c->kp.d, c->U, c->mp, c->m, c->khash, c->kidx, c->K,
                       c->mp, M, ca, fused ? c->alpha : ca.alpha_in, c->slab_small,
                       rec_out + 1 + c->kp.L, c->stream));
   if (c->knot_on)
     HIPCHK(launch_knot_reduce(c->knot_slab, c->n_pad / SGP_TILE, c->mp, c->kp.d, c->knot_part,
+                              KNOT_PART_ROWS * c->mp_max * c->d,
                               knot_out, knot_acc, c->stream));
   return SGP_OK;
 }
@@ -691,7 +771,7 @@ int sgp_ctx_enable_knot_grad(sgp_ctx* c, int enable) {
   HIPCHK(hipSetDevice(c->device));
   if (!c->knot_slab) {
     int st = dalloc(&c->knot_slab, (c->n_pad / SGP_TILE) * c->mp_max * c->d);
-    st = st ? st : dalloc(&c->knot_part, 64 * c->mp_max * c->d);
+    st = st ? st : dalloc(&c->knot_part, KNOT_PART_ROWS * c->mp_max * c->d);
     st = st ? st : dalloc(&c->knot_kmm, c->mp_max * c->d);
     if (st) return st;
   }
@@ -766,7 +846,8 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
                               c->tslab, c->stream));
   }
   HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_vi_red1_count(m), c->stream));
-  HIPCHK(launch_knot_reduce(c->tslab, c->n_pad / 64, mpv, 1, c->T1, red1 + mmv, false,
+  HIPCHK(launch_knot_reduce(c->tslab, c->n_pad / 64, mpv, 1, c->T1, c->mp_max * c->mp_max,
+                            red1 + mmv, false,
                             c->stream));
   HIPCHK(launch_dot(c->r, c->r, c->n_pad, c->slab_small, red1 + mmv + mpv, c->stream));
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));   // keep the SYRK round unshared
@@ -931,11 +1012,13 @@ int sgp_vi_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
   double sc[SC_N], r2[SGP_MAXD + 8];
   int status[4];
   const int64_t n2 = sgp_vi_red2_count(kp.kernel, kp.d);
-  HIPCHK(hipMemcpyAsync(sc, c->sc, sizeof(sc), hipMemcpyDeviceToHost, c->stream));
-  if (!obj_only)
-    HIPCHK(hipMemcpyAsync(r2, red2, sizeof(double) * n2, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(status, c->status, sizeof(status), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  {
+    Readback rb(c);
+    HIPCHK(rb.add(sc, c->sc, sizeof(sc)));
+    if (!obj_only) HIPCHK(rb.add(r2, red2, sizeof(double) * n2));
+    HIPCHK(rb.add(status, c->status, sizeof(status)));
+    HIPCHK(rb.wait());
+  }
   c->phase = 0;
   if (status[0] || status[1]) {
     set_err("chol(): the leading minor of order %d of %s is not positive definite",
@@ -1149,15 +1232,16 @@ int sgp_fitc_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
   int status[4];
   const int64_t off = fitc_rec_off(mp);
   const int nrec = L + 5;
-  HIPCHK(hipMemcpyAsync(sc, c->sc, sizeof(sc), hipMemcpyDeviceToHost, c->stream));
-  if (!obj_only) {
-    HIPCHK(hipMemcpyAsync(r2, red2 + mp * mp + mp + 1, sizeof(double), hipMemcpyDeviceToHost,
-                          c->stream));
-    HIPCHK(hipMemcpyAsync(r2 + 1, red2 + off, sizeof(double) * 2 * nrec, hipMemcpyDeviceToHost,
-                          c->stream));
+  {
+    Readback rb(c);
+    HIPCHK(rb.add(sc, c->sc, sizeof(sc)));
+    if (!obj_only) {
+      HIPCHK(rb.add(r2, red2 + mp * mp + mp + 1, sizeof(double)));
+      HIPCHK(rb.add(r2 + 1, red2 + off, sizeof(double) * 2 * nrec));
+    }
+    HIPCHK(rb.add(status, c->status, sizeof(status)));
+    HIPCHK(rb.wait());
   }
-  HIPCHK(hipMemcpyAsync(status, c->status, sizeof(status), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
   c->phase = 0;
   if (status[0] || status[1]) {
     set_err("chol(): the leading minor of order %d of %s is not positive definite",

@@ -339,7 +339,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   constexpr int A_SZ = T128 * SA;   // 2176 (keeps the B image 16-byte aligned)
   constexpr int B_SZ = BK * SB;     // 2304
   __shared__ __attribute__((aligned(16))) double lds[2 * (A_SZ + B_SZ)];
-  __shared__ double red[4][SGP_MAXD + 4];
+  __shared__ double red[4][SGP_MAXD + 5];
   __shared__ double s_uk[2][BK];   // u slice of the staged k-step (fused alpha)
 
   const int64_t ntj = mp / T128;
@@ -712,8 +712,8 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
       red[wv][4 + L] = v;
     }
     __syncthreads();
-    if (tid < nrec)
-      slab[wgid * nrec + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+    if (tid < nrec)   // field-major [nrec][nwg]: coalesced for the reduction (launch_rowsum)
+      slab[tid * nwg + wgid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
   }
 }
 
@@ -803,13 +803,27 @@ k_coinc(const double* __restrict__ X, int64_t ldx, int64_t n, int d, const doubl
         sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
 }
 
-// rec[0..2] += sum_b part[b][0..2]
-__global__ void k_coinc_add(const double* __restrict__ part, int nb, double* __restrict__ rec) {
-  if (threadIdx.x < 3) {
-    double s = 0.0;
-    for (int b = 0; b < nb; ++b) s += part[b * 3 + threadIdx.x];
-    rec[threadIdx.x] += s;
+// rec[0..2] += sum_b part[b][0..2]  (one 256-thread block, fixed summation order)
+__global__ void __launch_bounds__(256) k_coinc_add(const double* __restrict__ part, int nb,
+                                                   double* __restrict__ rec) {
+  __shared__ double sh[3][4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  for (int b = tid; b < nb; b += 256) {
+    s0 += part[b * 3];
+    s1 += part[b * 3 + 1];
+    s2 += part[b * 3 + 2];
   }
+  s0 = wave_sum(s0);
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (lane == 0) {
+    sh[0][wv] = s0;
+    sh[1][wv] = s1;
+    sh[2][wv] = s2;
+  }
+  __syncthreads();
+  if (tid < 3) rec[tid] += sh[tid][0] + sh[tid][1] + sh[tid][2] + sh[tid][3];
 }
 
 // rowq[tj][i] summed over the column tiles -> out[i] (deterministic order)
@@ -984,17 +998,61 @@ hipError_t launch_coinc(const double* X, int64_t ldx, int64_t n, int d, const do
   hipLaunchKernelGGL(k_coinc, dim3((unsigned)nb), dim3(256), 0, s, X, ldx, n, d, U, ldu, m, khash,
                      kidx, K, mp, M, alpha, ca.uvec, ca.beta_in, ca.vvec, ca.rs_vec, ca.rs,
                      ca.cdiag, part);
-  hipLaunchKernelGGL(k_coinc_add, dim3(1), dim3(64), 0, s, part, (int)nb, rec);
+  hipLaunchKernelGGL(k_coinc_add, dim3(1), dim3(256), 0, s, part, (int)nb, rec);
   return hipGetLastError();
 }
 
 hipError_t launch_knot_reduce(const double* knot_slab, int64_t ntiles, int64_t mp, int d,
-                              double* part, double* out, bool accumulate, hipStream_t s) {
+                              double* part, int64_t part_cap, double* out, bool accumulate,
+                              hipStream_t s) {
   const int64_t ncol = mp * d;
   const unsigned gx = (unsigned)((ncol + 255) / 256);
-  hipLaunchKernelGGL(k_knot_reduce1, dim3(gx, 64), dim3(256), 0, s, knot_slab, ntiles, ncol, part);
-  hipLaunchKernelGGL(k_knot_reduce2, dim3(gx), dim3(256), 0, s, part, 64, ncol, out,
+  // enough row groups that each thread of the first pass sums ~32 rows (latency, not
+  // bandwidth, bounds this tall column sum), within the partials' capacity
+  int64_t gy = ntiles / 32;
+  if (gy > 256) gy = 256;
+  if (gy > part_cap / ncol) gy = part_cap / ncol;
+  if (gy < 1) gy = 1;
+  if (gy * ncol > part_cap) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_knot_reduce1, dim3(gx, (unsigned)gy), dim3(256), 0, s, knot_slab, ntiles,
+                     ncol, part);
+  hipLaunchKernelGGL(k_knot_reduce2, dim3(gx), dim3(256), 0, s, part, (int)gy, ncol, out,
                      accumulate ? 1 : 0);
+  return hipGetLastError();
+}
+
+// out[c] = sum_k slab[c * len + k] for c < nrow (field-major records), two deterministic passes
+// through part (nrow * 32 doubles)
+__global__ void __launch_bounds__(256) k_rowsum1(const double* __restrict__ slab, int64_t len,
+                                                 double* __restrict__ part) {
+  __shared__ double sh[4];
+  const int64_t c = blockIdx.x, g = blockIdx.y, G = gridDim.y;
+  const int64_t b = len * g / G, e = len * (g + 1) / G;
+  double v = 0.0;
+  for (int64_t k = b + threadIdx.x; k < e; k += 256) v += slab[c * len + k];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) part[c * G + g] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+__global__ void k_rowsum2(const double* __restrict__ part, int G, int nrow,
+                          double* __restrict__ out) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= nrow) return;
+  double v = 0.0;
+  for (int g = 0; g < G; ++g) v += part[c * G + g];
+  out[c] = v;
+}
+
+hipError_t launch_rowsum(const double* slab, int64_t nrow, int64_t len, double* part,
+                         int64_t part_cap, double* out, hipStream_t s) {
+  if (nrow <= 0) return hipSuccess;
+  const int G = 32;
+  if (nrow * G > part_cap) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_rowsum1, dim3((unsigned)nrow, G), dim3(256), 0, s, slab, len, part);
+  hipLaunchKernelGGL(k_rowsum2, dim3((unsigned)((nrow + 63) / 64)), dim3(64), 0, s, part, G,
+                     (int)nrow, out);
   return hipGetLastError();
 }
 

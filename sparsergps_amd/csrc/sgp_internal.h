@@ -234,7 +234,12 @@ hipError_t launch_lap_grad_b(int64_t n, int64_t n_pad, const double* B, const do
 // out[j*d + c] (+)= sum over row tiles of knot_slab (deterministic two-level reduction);
 // part: 64 * mp * d doubles of work space
 hipError_t launch_knot_reduce(const double* knot_slab, int64_t ntiles, int64_t mp, int d,
-                              double* part, double* out, bool accumulate, hipStream_t s);
+                              double* part, int64_t part_cap, double* out, bool accumulate,
+                              hipStream_t s);
+// out[c] = sum_k slab[c * len + k], c < nrow (field-major contraction records); part holds
+// nrow * 32 doubles
+hipError_t launch_rowsum(const double* slab, int64_t nrow, int64_t len, double* part,
+                         int64_t part_cap, double* out, hipStream_t s);
 // out[k*d + c] = 2 sum_l G22_kl K22_kl (u_lc - u_kc), G22 as in launch_contract_kmm
 hipError_t launch_knot_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,
                            int64_t mp, const double* uvec, const double* Ainv,

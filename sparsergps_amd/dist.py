@@ -125,7 +125,10 @@ class RowShardedVI:
 
     def eval(self, theta, U, delta=1e-6):
         b = self.backend
-        with (b.stream_context() if hasattr(b, "stream_context") else contextlib.nullcontext()):
+        # the torch stream context orders the collectives after libsgp's kernels; one rank
+        # issues no collective and skips it
+        use_ctx = self.world > 1 and hasattr(b, "stream_context")
+        with (b.stream_context() if use_ctx else contextlib.nullcontext()):
             red1 = b.phase1(theta, U, delta)
             if self.world > 1:
                 self.dist.all_reduce(red1, group=self.group)

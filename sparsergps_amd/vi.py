@@ -74,8 +74,13 @@ class SparseGPContext:
     def enable_timing(self, on=True):
         _lib.check(self._lib.sgp_ctx_enable_timing(self.handle, 1 if on else 0))
 
+    def timing_evals(self):
+        """Evaluations recorded since enable_timing(True)."""
+        return int(self._lib.sgp_ctx_timing_evals(self.handle))
+
     def timings(self):
-        """[(phase name, ms)] of the last evaluation (HIP events on the launch stream)."""
+        """[(phase name, total ms)] over the evaluations recorded since enable_timing(True)
+        (HIP events on the launch stream, read back only here)."""
         names = C.create_string_buffer(65536)
         ms = (C.c_double * 2048)()
         cnt = C.c_int(0)
