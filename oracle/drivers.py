@@ -1,0 +1,212 @@
+"""CPU oracle for the reference's optimizer drivers -- TEST INFRASTRUCTURE ONLY.
+
+Literal restatement (numpy) of the three gradient-ascent drivers that call the hot path once
+per iteration, on top of the objective / gradient restatements in ``sgp_oracle``:
+  norm_grad_ascent_vi  R/vi_functions.R:606-1218          (elbo_fun + delbo_dcov_par)
+  norm_grad_ascent     R/laplace_gradient_ascent.R:1111-1693  (obj_fun_norm + dlogp_dcov_par)
+  laplace_grad_ascent  R/laplace_gradient_ascent.R:10-623    (newtrap_sparseGP + dlogq_dcov_par)
+Only tests/ may import it (the checker for sparsergps_amd.drivers, never the thing measured).
+Parity status as in sgp_oracle: unpinned relative to the reference (R is absent here).
+
+Reproduced literally: the opt() defaults, the "ga" and modified-Adadelta updates in the
+log-parameter space, the sign-change damping (1/eta)^s with s halved for theta but not for the
+knots, the stop rule `iter < maxit && (any(|grad| > grad_tol) || |obj_k - obj_{k-1}| >
+obj_tol)`, the bounded knot transform (ub sigmoid(t) + lb sigmoid(-t)) with the knot
+coordinates accumulated in transformed space, and the end-of-fit knot posterior.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import numpy as np
+
+from . import sgp_oracle as O
+
+OPT_DEFAULTS = {"optim_method": "adadelta", "decay": 0.95, "epsilon": 1e-6, "learn_rate": 1e-2,
+                "eta": 1e3, "maxit": 1000, "obj_tol": 1e-3, "grad_tol": np.inf, "delta": 1e-6}
+
+
+def _opts(opt, extra=None):
+    o = dict(OPT_DEFAULTS)
+    if extra:
+        o.update(extra)
+    for k, v in (opt or {}).items():        # unknown names are skipped (vi_functions.R:664-677)
+        if k in o:
+            o[k] = v
+    return o
+
+
+def _trans_fun_knots(t, bounds):
+    """trans_fun of dsqexp_dx2(_ard) (covariance_function_derivatives.R:191-197), row-wise."""
+    return bounds[:, 1] * (1 / (1 + np.exp(-t))) + bounds[:, 0] * (1 / (1 + np.exp(t)))
+
+
+def _ascent(evaluate, posterior, cov_par_start, xu, xy, dtheta, dknot, opt, nr=False):
+    """Shared skeleton of the three drivers.  evaluate(cov_par, xu) -> (obj, grad OrderedDict
+    or None, knot_grad or None[, extras]); posterior(cov_par, xu) -> (u_mean, u_var)."""
+    o = opt
+    xy = np.asarray(xy, dtype=np.float64)
+    xu = np.array(xu, dtype=np.float64, copy=True)
+    names = list(cov_par_start.keys())
+    cur = np.array([float(cov_par_start[k]) for k in names])
+    cov_par = OrderedDict(zip(names, cur))
+    m, d = xu.shape
+    res = evaluate(cov_par, xu)
+    obj, g, gk = res[:3]
+    extras = [res[3:]]
+    obj_vals = [obj]
+    cov_hist = [cur.copy()]
+    gt = np.array([g[k] for k in names]) if dtheta else 0.0
+    grad_vals = [gt if dtheta else np.full(len(names), np.nan)]
+    gkn = np.asarray(gk) if dknot else 0.0
+    knot_grads = [gkn] if dknot else []
+    trans = np.log(cur)
+    if dknot:
+        bounds = O.knot_bounds_of(xy)
+        xu_trans = O.knot_trans(xu, bounds)
+        xu_hist = [xu.copy()]
+    it = 1
+
+    def keep_going():
+        gall = np.concatenate([np.atleast_1d(gt), np.atleast_1d(gkn)])
+        return it < o["maxit"] and (bool(np.any(np.abs(gall) > o["grad_tol"])) or
+                                    (abs(obj - obj_vals[it - 2]) > o["obj_tol"] if it > 1 else True))
+
+    sg2_t = np.zeros(len(names))
+    sd2_t = np.zeros(len(names))
+    sc_t = np.zeros(len(names))
+    sg2_k = np.zeros(m * d)
+    sd2_k = np.zeros(m * d)
+    sc_k = np.zeros(m * d)
+    while keep_going():
+        it += 1
+        if o["optim_method"] == "ga":
+            if dtheta:
+                trans = trans + o["learn_rate"] * gt
+            if dknot:
+                xu_trans = xu_trans + o["learn_rate"] * gkn.reshape(m, d)   # byrow = TRUE
+        else:
+            if dtheta:
+                sg2_t = o["decay"] * sg2_t + (1 - o["decay"]) * gt ** 2
+                dt = ((1 / o["eta"]) ** sc_t) * (np.sqrt(sd2_t + o["epsilon"]) /
+                                                 np.sqrt(sg2_t + o["epsilon"])) * gt
+                sd2_t = o["decay"] * sd2_t + (1 - o["decay"]) * dt ** 2
+                trans = trans + dt
+            if dknot:
+                sg2_k = o["decay"] * sg2_k + (1 - o["decay"]) * gkn ** 2
+                dk = ((1 / o["eta"]) ** sc_k) * (np.sqrt(sd2_k + o["epsilon"]) /
+                                                 np.sqrt(sg2_k + o["epsilon"])) * gkn
+                sd2_k = o["decay"] * sd2_k + (1 - o["decay"]) * dk ** 2
+                xu_trans = xu_trans + dk.reshape(m, d)
+        if dknot:
+            xu = np.vstack([_trans_fun_knots(xu_trans[k], bounds) for k in range(m)])
+            xu_hist.append(xu.copy())
+        if dtheta:
+            cur = np.exp(trans)                # real_to_pos / the trans_fun exp of every theta
+            cov_par = OrderedDict(zip(names, cur))
+        res = evaluate(cov_par, xu)
+        obj, g, gk = res[:3]
+        extras.append(res[3:])
+        obj_vals.append(obj)
+        cov_hist.append(cur.copy())
+        if dtheta:
+            gnew = np.array([g[k] for k in names])
+            if o["optim_method"] != "ga":
+                sc_t = o["decay"] * sc_t + (1 - o["decay"]) * np.abs(np.sign(gnew) - np.sign(gt)) / 2
+            gt = gnew
+            trans = np.log(cur)                # trans_par of the new evaluation
+            grad_vals.append(gt)
+        if dknot:
+            gknew = np.asarray(gk)
+            if o["optim_method"] != "ga":      # no /2 for the knots (vi_functions.R:1142-1143)
+                sc_k = o["decay"] * sc_k + (1 - o["decay"]) * np.abs(np.sign(gknew) - np.sign(gkn))
+            gkn = gknew
+            knot_grads.append(gkn)
+    u_mean, u_var = posterior(cov_par, xu, extras[-1])
+    out = {"cov_par": cov_par, "xu": xu, "u_mean": u_mean, "u_var": u_var, "iter": it,
+           "obj_fun": np.array(obj_vals), "grad": np.array(grad_vals),
+           "cov_par_history": np.array(cov_hist)}
+    out["knot_grad"] = np.array(knot_grads) if dknot else 0
+    out["knot_history"] = np.stack(xu_hist, axis=2) if dknot else xu
+    out["extras"] = extras
+    return out
+
+
+def norm_grad_ascent_vi(cov_par_start, cov_fun, xu, xy, y, mu=None, muu=None, dtheta=True,
+                        dcov_fun_dknot=None, knot_opt=None, opt=None):
+    """vi_functions.R:606-1218 (obj_fun = elbo_fun)."""
+    o = _opts(opt)
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    mu = np.full(y.size, y.mean()) if mu is None else np.asarray(mu, dtype=np.float64)
+    muu = np.full(np.shape(xu)[0], y.mean()) if muu is None else np.asarray(muu, dtype=np.float64)
+    dl = o["delta"]
+
+    def evaluate(cp, U):
+        obj = O.elbo_eval(cp, cov_fun, U, xy, y, mu, dl)
+        r = O.delbo_dcov_par(cp, cov_fun, U, xy, y, mu, dl, dcov_fun_dknot, knot_opt)
+        return obj, r["gradient"], r.get("knot_gradient")
+
+    def posterior(cp, U, _):
+        return O.vi_posterior_u(cp, cov_fun, U, xy, y, mu, muu, dl)
+
+    out = _ascent(evaluate, posterior, cov_par_start, xu, xy, dtheta, dcov_fun_dknot is not None,
+                  o)
+    out.update({"cov_fun": cov_fun, "xy": xy, "mu": mu, "muu": muu})
+    return out
+
+
+def norm_grad_ascent(cov_par_start, cov_fun, xu, xy, y, mu=None, muu=None, dtheta=True,
+                     dcov_fun_dknot=None, knot_opt=None, opt=None):
+    """laplace_gradient_ascent.R:1111-1693 (FITC: obj_fun_norm + dlogp_dcov_par)."""
+    o = _opts(opt)
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    mu = np.full(y.size, y.mean()) if mu is None else np.asarray(mu, dtype=np.float64)
+    muu = np.full(np.shape(xu)[0], y.mean()) if muu is None else np.asarray(muu, dtype=np.float64)
+    dl = o["delta"]
+
+    def evaluate(cp, U):
+        obj = O.fitc_obj_eval(cp, cov_fun, U, xy, y, mu, dl)
+        r = O.dlogp_dcov_par(cp, cov_fun, U, xy, y, mu, dl, dcov_fun_dknot, knot_opt)
+        return obj, r["gradient"], r.get("knot_gradient")
+
+    def posterior(cp, U, _):
+        return O.fitc_posterior_u(cp, cov_fun, U, xy, y, mu, muu, dl)
+
+    out = _ascent(evaluate, posterior, cov_par_start, xu, xy, dtheta, dcov_fun_dknot is not None,
+                  o)
+    out.update({"cov_fun": cov_fun, "xy": xy, "mu": mu, "muu": muu})
+    return out
+
+
+def laplace_grad_ascent(cov_par_start, cov_fun, xu, xy, y, ff, mu, muu, m=1.0, dtheta=True,
+                        dcov_fun_dknot=None, knot_opt=None, opt=None):
+    """laplace_gradient_ascent.R:10-623 for the Poisson likelihood: each iteration runs
+    newtrap_sparseGP warm-started from the previous mode, then dlogq_dcov_par at the mode."""
+    o = _opts(opt, {"maxit_nr": 1000, "tol_nr": 1e-6})
+    for k in ("maxit_nr", "tol_nr"):
+        if opt and k in opt:
+            o[k] = opt[k]
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    mu = np.asarray(mu, dtype=np.float64).reshape(-1)
+    muu = np.asarray(muu, dtype=np.float64).reshape(-1)
+    dl = o["delta"]
+    state = {"f": np.asarray(ff, dtype=np.float64).copy()}
+
+    def evaluate(cp, U):
+        nr = O.newtrap_sparseGP(state["f"], cp, cov_fun, xy, U, y, mu, m, dl, o["maxit_nr"],
+                                o["tol_nr"], muu=muu)
+        state["f"] = nr["gp"]
+        ov = nr["objective_function_values"]
+        r = O.dlogq_dcov_par(cp, cov_fun, U, xy, y, nr["gp"], mu, m, dl, dcov_fun_dknot,
+                             knot_opt)
+        return (ov[-1], r["gradient"], r.get("knot_gradient"), len(ov),
+                nr["u_posterior_mean"], nr["u_posterior_variance"])
+
+    def posterior(cp, U, last):
+        return last[1], last[2]
+
+    out = _ascent(evaluate, posterior, cov_par_start, xu, xy, dtheta, dcov_fun_dknot is not None,
+                  o)
+    out.update({"cov_fun": cov_fun, "xy": xy, "mu": mu, "muu": muu, "fmax": state["f"],
+                "nr_iter": np.array([e[0] for e in out["extras"]])})
+    return out

@@ -7,6 +7,7 @@ from ._build import build
 from ._lib import NotPositiveDefinite, SGPError
 from .covariance import (cov_fun_expC, cov_fun_sqrd_exp_ardC, cov_fun_sqrd_expC, dsig_dtheta_ardC,
                          dsig_dthetaC, make_cov_mat_ardC, make_cov_matC)
+from .drivers import laplace_grad_ascent, norm_grad_ascent, norm_grad_ascent_vi
 from .predict import predict_gp, predict_laplace, predict_vi
 from .laplace import dlogq_dcov_par, laplace_eval, newtrap_sparseGP, obj_fun_pois
 from .vi import (SparseGPContext, delbo_dcov_par, dlogp_dcov_par, elbo_fun, fitc_eval, param_names,
@@ -20,4 +21,5 @@ __all__ = [
     "fitc_eval", "dlogp_dcov_par",
     "laplace_eval", "newtrap_sparseGP", "dlogq_dcov_par", "obj_fun_pois",
     "predict_vi", "predict_laplace", "predict_gp",
+    "norm_grad_ascent_vi", "norm_grad_ascent", "laplace_grad_ascent",
 ]

@@ -189,3 +189,27 @@ def test_repeated_evals_full_knot_count(sgp):
     o, g = A.eval_vi("ard", th * (1 + 3e-3), P["X"], P["y"], P["mu"], P["U"], P["delta"])
     assert abs(outs[-1][0] - o) / abs(o) < 1e-9
     assert _rel(outs[-1][1], g) < 1e-7
+
+
+@pytest.mark.parametrize("d", [12, 32])
+def test_high_dimension_ard_matches_oracle(sgp, d):
+    """d > 8 runs the generic contraction epilogue (k_contract<32>); d = 32 is SGP_MAXD, the
+    widest gradient record (L + 5 = 37 fields)."""
+    rng = np.random.default_rng(100 + d)
+    n, m = 300, 24
+    X = rng.uniform(0, 10, size=(n, d))
+    U = rng.uniform(0, 10, size=(m, d))
+    y = np.sin(X).sum(axis=1) / math.sqrt(d) + rng.normal(0, 0.5, size=n)
+    mu = np.full(n, y.mean())
+    ls = 2.0 * math.sqrt(d)
+    cp = OrderedDict([("sigma", 1.2)] + [(f"l{c + 1}", ls * (1 + 0.02 * c)) for c in range(d)]
+                     + [("tau", 0.5)])
+    for fun, ref_obj, ref_grad in (
+            (sgp.vi_eval, O.elbo_eval, O.delbo_dcov_par),
+            (sgp.fitc_eval, O.fitc_obj_eval, O.dlogp_dcov_par)):
+        obj, grad = fun(cp, "ard", U, X, y, mu, 1e-6)
+        ro = ref_obj(cp, "ard", U, X, y, mu, 1e-6)
+        rg = ref_grad(cp, "ard", U, X, y, mu, 1e-6)["gradient"]
+        assert abs(obj - ro) / abs(ro) < EVAL_RTOL
+        for k in cp:
+            assert abs(grad[k] - rg[k]) / max(1.0, abs(rg[k])) < EVAL_RTOL, (fun.__name__, k)
