@@ -180,6 +180,14 @@ int sgp_lap_nr(sgp_ctx* ctx, int kernel, const double* theta, const double* U, i
                int64_t ldu, double delta, double expo, double tol, int maxit, double* obj,
                int* nr_iters);
 
+/* Full (non-sparse) Gaussian GP over the context's n rows (config 1; requires m_max >= n):
+ * obj = log dmvnorm(y; mu, Sigma11) (obj_fun_norm_full, R/laplace_approx_obj_funs.R:56-61) and
+ * grad = dlogp_dcov_par_full (R/laplace_approx_gradient.R:1140-1269; its alpha is Sigma11^-1 y,
+ * not Sigma11^-1 (y - mu)), Sigma11 = k(xy, xy) + (tau^2 + delta) I.  SGP_FLAG_OBJ_ONLY skips
+ * the gradient (grad may be NULL). */
+int sgp_eval_full(sgp_ctx* ctx, int kernel, const double* theta, double delta, unsigned flags,
+                  double* obj, double* grad);
+
 /* Posterior of the knot values u at the end of a fit, from the context's last completed
  * evaluation (VI: vi_functions.R:1161-1180; FITC: laplace_gradient_ascent.R:1635-1655;
  * Laplace: newtrap_sparseGP.R:137-176).  muu, u_mean: m host values; u_var: m x m host,
@@ -190,10 +198,12 @@ int sgp_posterior_u(sgp_ctx* ctx, const double* muu, double* u_mean, double* u_v
  *   SGP_PRED_VI      predict_vi      (R/vi_functions.R:1222-1333; gaussian only)
  *   SGP_PRED_LAPLACE predict_laplace (R/laplace_approx_prediction.R:3-123; FITC or Laplace fits,
  *                    gaussian != 0 selects the family == "gaussian" Sigma22)
+ *   SGP_PRED_FULL    predict_gp_full (R/laplace_approx_prediction.R:281-405): a full Gaussian
+ *                    GP -- U = xy, u_mean = y, muu = mu, u_var unused (may be NULL)
  * as dispatched by predict_gp (R/laplace_approx_prediction.R:408-542).  u_var is m x m
  * column-major (ld ldv).  pred_var: np values, or with full_cov the np x np matrix
  * (column-major, ld ldpv).  Host buffers; device work space is allocated per call. */
-enum { SGP_PRED_VI = 0, SGP_PRED_LAPLACE = 1 };
+enum { SGP_PRED_VI = 0, SGP_PRED_LAPLACE = 1, SGP_PRED_FULL = 2 };
 int sgp_predict(int device, int kernel, const double* theta, double delta, int method,
                 int gaussian, const double* U, int64_t m, int64_t ldu, const double* u_mean,
                 const double* muu, const double* u_var, int64_t ldv, const double* x_pred,

@@ -5,6 +5,7 @@ per iteration, on top of the objective / gradient restatements in ``sgp_oracle``
   norm_grad_ascent_vi  R/vi_functions.R:606-1218          (elbo_fun + delbo_dcov_par)
   norm_grad_ascent     R/laplace_gradient_ascent.R:1111-1693  (obj_fun_norm + dlogp_dcov_par)
   laplace_grad_ascent  R/laplace_gradient_ascent.R:10-623    (newtrap_sparseGP + dlogq_dcov_par)
+  norm_grad_ascent_full R/laplace_gradient_ascent.R:1700-2011 (obj_fun_norm_full + dlogp_dcov_par_full)
 Only tests/ may import it (the checker for sparsergps_amd.drivers, never the thing measured).
 Parity status as in sgp_oracle: unpinned relative to the reference (R is absent here).
 
@@ -210,3 +211,20 @@ def laplace_grad_ascent(cov_par_start, cov_fun, xu, xy, y, ff, mu, muu, m=1.0, d
     out.update({"cov_fun": cov_fun, "xy": xy, "mu": mu, "muu": muu, "fmax": state["f"],
                 "nr_iter": np.array([e[0] for e in out["extras"]])})
     return out
+
+
+def norm_grad_ascent_full(cov_par_start, cov_fun, xy, y, mu=None, opt=None):
+    """laplace_gradient_ascent.R:1700-2011 (full Gaussian GP; no knots, no posterior)."""
+    o = _opts(opt)
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    mu = np.full(y.size, y.mean()) if mu is None else np.asarray(mu, dtype=np.float64)
+    dl = o["delta"]
+
+    def evaluate(cp, _U):
+        obj = O.full_obj_eval(cp, cov_fun, xy, y, mu, dl)
+        return obj, O.dlogp_dcov_par_full(cp, cov_fun, xy, y, mu, dl)["gradient"], None
+
+    out = _ascent(evaluate, lambda cp, U, e: (None, None), cov_par_start, np.zeros((1, 1)), xy,
+                  True, False, o)
+    return {"cov_par": out["cov_par"], "iter": out["iter"], "obj_fun": out["obj_fun"],
+            "grad": out["grad"], "cov_par_history": out["cov_par_history"]}

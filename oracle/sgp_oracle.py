@@ -779,6 +779,72 @@ def predict_vi(u_mean, u_var, xu, x_pred, cov_fun, cov_par, mu, muu, full_cov=Fa
     return {"pred_mean": pred_mean, "pred_var": pred_var}
 
 
+# --------------------------------------------------------------------------------------
+# Full (non-sparse) Gaussian GP, config 1
+# --------------------------------------------------------------------------------------
+
+
+def obj_fun_norm_full(mu, Sigma, y):
+    """laplace_approx_obj_funs.R:56-61: mvtnorm::dmvnorm(y, mu, Sigma, log = TRUE)
+    (Cholesky-based, no det() overflow)."""
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    r = y - np.asarray(mu, dtype=np.float64).reshape(-1)
+    R = r_chol(Sigma)
+    z = np.linalg.solve(R.T, r)
+    return float(-0.5 * z @ z - np.sum(np.log(np.diag(R))) - (y.size / 2) * math.log(2 * math.pi))
+
+
+def full_sigma(cov_par, cov_fun, xy, delta):
+    """Sigma11 of norm_grad_ascent_full (laplace_gradient_ascent.R:1756-1766): symmetric
+    make_cov_matC / make_cov_mat_ardC, i.e. k(xy, xy) + (tau^2 + delta) I."""
+    xy = _as_matrix(xy)
+    lnames = lnames_for(cov_fun, xy.shape[1])
+    if cov_fun == "ard":
+        return make_cov_mat_ardC(xy, None, cov_par, cov_fun, delta, lnames)
+    return make_cov_matC(xy, None, cov_par, cov_fun, delta)
+
+
+def full_obj_eval(cov_par, cov_fun, xy, y, mu, delta=1e-6):
+    return obj_fun_norm_full(mu, full_sigma(cov_par, cov_fun, xy, delta), y)
+
+
+def dlogp_dcov_par_full(cov_par, cov_fun, xy, y, mu, delta=1e-6):
+    """laplace_approx_gradient.R:1140-1269.  alpha = solve(Sigma11, y) -- y, not y - mu
+    (l.1186); grad_p = 1/2 sum(diag(alpha alpha^T dS - solve(Sigma11, dS)))."""
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    xy = _as_matrix(xy)
+    lnames = lnames_for(cov_fun, xy.shape[1])
+    S = full_sigma(cov_par, cov_fun, xy, delta)
+    alpha = r_solve(S, y)
+    grad = OrderedDict()
+    for par_name in cov_par.keys():
+        if cov_fun == "ard":
+            dS = dsig_dtheta_ardC(xy, None, cov_par, cov_fun, par_name, lnames)
+        else:
+            dS = dsig_dthetaC(xy, None, cov_par, cov_fun, par_name)
+        grad[par_name] = float(0.5 * np.sum(np.diag(np.outer(alpha, alpha) @ dS - r_solve(S, dS))))
+    trans_par = OrderedDict((k, math.log(float(v))) for k, v in cov_par.items())
+    return {"gradient": grad, "trans_par": trans_par}
+
+
+def predict_gp_full(xy, y, x_pred, cov_fun, cov_par, mu, mu_pred, full_cov=False, delta=1e-6):
+    """laplace_approx_prediction.R:281-405."""
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    xy, x_pred = _as_matrix(xy), _as_matrix(x_pred)
+    lnames = lnames_for(cov_fun, xy.shape[1])
+    if cov_fun == "ard":
+        S22 = make_cov_mat_ardC(xy, None, cov_par, cov_fun, delta, lnames)
+        S12 = make_cov_mat_ardC(x_pred, xy, cov_par, cov_fun, delta, lnames)
+        S11 = make_cov_mat_ardC(x_pred, None, cov_par, cov_fun, delta, lnames)
+    else:
+        S22 = make_cov_matC(xy, None, cov_par, cov_fun, delta)
+        S12 = make_cov_matC(x_pred, xy, cov_par, cov_fun, delta)
+        S11 = make_cov_matC(x_pred, None, cov_par, cov_fun, delta)
+    pred_mean = np.asarray(mu_pred, dtype=np.float64).reshape(-1) + S12 @ r_solve(S22, y - mu)
+    V = S11 - S12 @ r_solve(S22, S12.T)
+    return {"pred_mean": pred_mean.reshape(-1, 1), "pred_var": V if full_cov else np.diag(V)}
+
+
 def predict_laplace(u_mean, u_var, xu, x_pred, cov_fun, cov_par, mu, muu, full_cov=False,
                     family="gaussian", delta=1e-6):
     """laplace_approx_prediction.R:3-123 (FITC / Laplace sparse prediction)."""

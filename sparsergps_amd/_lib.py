@@ -21,7 +21,7 @@ SGP_OK, SGP_EINVAL, SGP_ENOTPD, SGP_EHIP, SGP_ENOMEM = 0, 1, 2, 3, 4
 KERNELS = {"sqexp": 0, "ard": 1, "exp": 2}
 SGP_FLAG_R_DET = 1
 SGP_FLAG_OBJ_ONLY = 2
-SGP_PRED_VI, SGP_PRED_LAPLACE = 0, 1
+SGP_PRED_VI, SGP_PRED_LAPLACE, SGP_PRED_FULL = 0, 1, 2
 
 # name -> (restype, argtypes); exactly the functions declared in include/sgp.h
 PROTOTYPES = {
@@ -74,6 +74,8 @@ PROTOTYPES = {
                                c_double_p, c_double_p, c_int_p]),
     "sgp_lap_nr": (C.c_int, [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_int64, C.c_int64,
                              C.c_double, C.c_double, C.c_double, C.c_int, c_double_p, c_int_p]),
+    "sgp_eval_full": (C.c_int, [C.c_void_p, C.c_int, c_double_p, C.c_double, C.c_uint,
+                                c_double_p, c_double_p]),
     "sgp_posterior_u": (C.c_int, [C.c_void_p, c_double_p, c_double_p, c_double_p]),
     "sgp_predict": (C.c_int, [C.c_int, C.c_int, c_double_p, C.c_double, C.c_int, C.c_int, c_double_p,
                               C.c_int64, C.c_int64, c_double_p, c_double_p, c_double_p, C.c_int64,

@@ -1688,6 +1688,89 @@ int sgp_lap_nr(sgp_ctx* c, int kernel, const double* theta, const double* U, int
 }
 
 
+// ------------------------------------------------------------------------- full GP
+// Config 1 (norm_grad_ascent_full, R/laplace_gradient_ascent.R:1700-2011): the n x n system
+// Sigma11 = k(xy, xy) + (tau^2 + delta) I over the context's own rows, factored like K22.
+//   obj  = obj_fun_norm_full = log dmvnorm(y; mu, Sigma11)  (R/laplace_approx_obj_funs.R:56-61)
+//   grad = dlogp_dcov_par_full (R/laplace_approx_gradient.R:1140-1269):
+//          1/2 tr((a a^T - Sigma11^-1) dSigma11/dlog theta) with a = Sigma11^-1 y -- y, not
+//          y - mu (the reference's quirk) -- contracted by k_contract_kmm with
+//          G = 1/2 a a^T - 1/2 Sigma11^-1; tau's derivative is 2 tau^2 on coincident pairs.
+int sgp_eval_full(sgp_ctx* c, int kernel, const double* theta, double delta, unsigned flags,
+                  double* obj, double* grad) {
+  if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
+  const bool obj_only = (flags & SGP_FLAG_OBJ_ONLY) != 0;
+  if (!obj || (!grad && !obj_only)) { set_err("invalid arguments"); return SGP_EINVAL; }
+  if (kernel == SGP_KERNEL_EXP) {
+    set_err("fused evaluation supports 'sqexp' and 'ard' (optimize_gp.R:263 rejects others)");
+    return SGP_EINVAL;
+  }
+  if (c->n > c->m_max) {
+    set_err("the full GP needs m_max >= n (n = %lld, m_max = %lld)", (long long)c->n,
+            (long long)c->m_max);
+    return SGP_EINVAL;
+  }
+  KernParams kp;
+  int st = make_params(kernel, c->d, theta, delta, &kp);
+  if (st) return st;
+  HIPCHK(hipSetDevice(c->device));
+  timers_reset(c);
+  c->kp = kp;
+  c->m = c->n;
+  c->mp = round_up(c->n, SGP_TILE);
+  c->delta = delta;
+  c->flags = flags;
+  c->phase = 0;
+  c->last_mode = 0;
+  c->knot_raw.clear();
+  const int64_t mp = c->mp, mm = mp * mp;
+  // the rows are the "knots": X (ld n_pad) -> U (ld mp), zero padded alike (mp == n_pad)
+  HIPCHK(hipMemcpy2DAsync(c->U, sizeof(double) * mp, c->X, sizeof(double) * c->n_pad,
+                          sizeof(double) * mp, (size_t)c->d, hipMemcpyDeviceToDevice, c->stream));
+  c->knots_valid = false;
+  HIPCHK(hipMemsetAsync(c->status, 0, sizeof(int) * 4, c->stream));
+  HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->stream));
+  st = k22_stage(c, 0.0);   // Sigma11 = k(xy, xy) + (tau^2 + delta) I and its inverse
+  if (st) return st;
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
+  {
+    Scope t(c, "full_vectors");
+    HIPCHK(dense_gemv(c->K22inv, mp, c->y, 1.0, c->uvec, c->stream));    // a = Sigma11^-1 y
+    HIPCHK(dense_gemv(c->K22inv, mp, c->r, 1.0, c->alpha, c->stream));   // Sigma11^-1 (y - mu)
+    HIPCHK(launch_dot(c->r, c->alpha, mp, c->slab_small, c->sc + SC_RR, c->stream));
+  }
+  if (!obj_only) {
+    Scope t(c, "contract_kmm");
+    HIPCHK(hipMemsetAsync(c->T1, 0, sizeof(double) * mm, c->stream));
+    int nb = 0;
+    HIPCHK(launch_contract_kmm(kp, c->U, mp, c->m, mp, c->uvec, c->T1, c->K22inv, c->T1, 0.5,
+                               0.5, 0.0, nullptr, nullptr, 0.0, c->slab_small, SLAB_SMALL, &nb,
+                               c->stream));
+    HIPCHK(launch_colsum(c->slab_small, nb, kp.P, c->sc + SC_G22, c->stream));
+  }
+  double sc[SC_N];
+  int status[4];
+  {
+    Readback rb(c);
+    HIPCHK(rb.add(sc, c->sc, sizeof(sc)));
+    HIPCHK(rb.add(status, c->status, sizeof(status)));
+    HIPCHK(rb.wait());
+  }
+  if (status[0]) {
+    set_err("Sigma11 is not positive definite (leading minor of order %d)", status[0]);
+    return SGP_ENOTPD;
+  }
+  const double n = (double)c->n;
+  *obj = -0.5 * sc[SC_RR] - sc[SC_LD22] - (n / 2.0) * log(2.0 * M_PI);   // sc: 1/2 log det
+  if (!obj_only) {
+    const double* g22 = sc + SC_G22;
+    grad[0] = g22[0];
+    for (int q = 0; q < kp.L; ++q) grad[1 + q] = g22[1 + q];
+    grad[kp.L + 1] = 2.0 * kp.tau2 * g22[kp.P - 1];
+  }
+  return SGP_OK;
+}
+
 // ------------------------------------------------------------------------- knot posterior
 // u | y at the end of the drivers, from the replicated state of the last evaluation:
 //   VI / FITC (vi_functions.R:1161-1180, laplace_gradient_ascent.R:1635-1655):
@@ -1750,12 +1833,14 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
   KernParams kp;
   int st = make_params(kernel, d, theta, delta, &kp);
   if (st) return st;
-  if (!U || m < 1 || ldu < m || !u_mean || !muu || !u_var || ldv < m || !x_pred || np < 1 ||
+  const bool full = method == SGP_PRED_FULL;   // u_var unused (zero): Sigma22 = the data block
+  if (!U || m < 1 || ldu < m || !u_mean || !muu || (!u_var && !full) || (!full && ldv < m) ||
+      !x_pred || np < 1 ||
       ldxp < np || !mu_pred || !pred_mean || !pred_var || (full_cov && ldpv < np)) {
     set_err("invalid sgp_predict arguments");
     return SGP_EINVAL;
   }
-  if (method != SGP_PRED_VI && method != SGP_PRED_LAPLACE) {
+  if (method != SGP_PRED_VI && method != SGP_PRED_LAPLACE && method != SGP_PRED_FULL) {
     set_err("invalid prediction method %d", method);
     return SGP_EINVAL;
   }
@@ -1799,8 +1884,9 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
     }
     std::vector<double> hd((size_t)mp, 0.0), hV((size_t)mm, 0.0);
     for (int64_t j = 0; j < m; ++j) hd[(size_t)j] = u_mean[j] - muu[j];
-    for (int64_t i = 0; i < m; ++i)
-      for (int64_t j = 0; j < m; ++j) hV[(size_t)(i * mp + j)] = u_var[i + j * ldv];
+    if (!full)
+      for (int64_t i = 0; i < m; ++i)
+        for (int64_t j = 0; j < m; ++j) hV[(size_t)(i * mp + j)] = u_var[i + j * ldv];
     HIPCHK(hipMemcpy(dU.p, hU.data(), sizeof(double) * hU.size(), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(Xp.p, hX.data(), sizeof(double) * hX.size(), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(wv.p + mp, hd.data(), sizeof(double) * mp, hipMemcpyHostToDevice));
@@ -1809,7 +1895,8 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
   }
   // Sigma22: the gaussian family subtracts tau^2 I again (vi_functions.R:1246-1260,
   // laplace_approx_prediction.R:25-43) -> diagonal sigma^2 + delta; otherwise Kuu+(tau^2+delta)I
-  const double diag_sub = gaussian ? kp.tau2 : 0.0;
+  // (predict_gp_full, laplace_approx_prediction.R:281-405: Sigma22 = k(xy, xy) + (tau^2+delta) I)
+  const double diag_sub = (gaussian && !full) ? kp.tau2 : 0.0;
   HIPCHK(launch_build_kmm(kp, dU.p, mp, m, mp, diag_sub, K22.p, s));
   HIPCHK(hipMemcpyAsync(Kinv.p, K22.p, sizeof(double) * mm, hipMemcpyDeviceToDevice, s));
   HIPCHK(dense_spd_inverse(Kinv.p, mp, R.p, nullptr, Pb.p, logd.p, status.p, s));
@@ -1830,7 +1917,7 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
     if (lap_full)
       HIPCHK(launch_rowquad_knm(kp, Kp.p, Kinv.p, np, npp, m, mp, nullptr, 0.0, nullptr, nullptr,
                                 nullptr, rowq.p, q.p, s));
-    if (method == SGP_PRED_VI)
+    if (method == SGP_PRED_VI || full)   // Sigma11 of x_pred with its tau^2 + delta diagonal
       HIPCHK(launch_fill_cov(kp, Xp.p, np, npp, Xp.p, np, npp, true, S.p, npp, s));
     else
       HIPCHK(hipMemsetAsync(S.p, 0, sizeof(double) * npp * npp, s));
@@ -1851,7 +1938,10 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
   for (int64_t i = 0; i < np; ++i) pred_mean[i] = mu_pred[i] + hy[(size_t)i];
   if (!full_cov) {
     // vi_functions.R:1321: tau^2 + sigma^2 + delta; laplace_approx_prediction.R:114: sigma^2 + tau^2
-    const double c0 = (method == SGP_PRED_VI) ? (kp.tau2 + kp.sig2) + delta : kp.sig2 + kp.tau2;
+    // predict_gp_full: diag(Sigma11) = sigma^2 + tau^2 + delta
+    const double c0 = (method == SGP_PRED_VI) ? (kp.tau2 + kp.sig2) + delta
+                                              : (full ? (kp.sig2 + kp.tau2) + delta
+                                                      : kp.sig2 + kp.tau2);
     for (int64_t i = 0; i < np; ++i) pred_var[i] = c0 + hq[(size_t)i];
     return SGP_OK;
   }

@@ -3,7 +3,8 @@
 Host-side mirror of the reference's prediction functions:
   predict_vi       R/vi_functions.R:1222-1333
   predict_laplace  R/laplace_approx_prediction.R:3-123   (FITC and Poisson-Laplace fits)
-  predict_gp       R/laplace_approx_prediction.R:408-542 (dispatcher; sparse fits only)
+  predict_gp       R/laplace_approx_prediction.R:408-542 (dispatcher; sparse fits and the
+                   full Gaussian GP via sparsergps_amd.full.predict_gp_full)
 The knot posterior (u_mean, u_var) that these consume comes from
 ``SparseGPContext.posterior_u`` (the drivers' end-of-fit computation).  K(x_pred, xu), the
 m x m solves and the per-row variance quadratic forms run in libsgp.so (sgp_predict).
@@ -34,13 +35,15 @@ def _predict(method, gaussian, u_mean, u_var, xu, x_pred, cov_fun, cov_par, mu, 
     theta = np.ascontiguousarray(theta_vector(cov_par, cov_fun, d, lnames))
     um = np.ascontiguousarray(np.asarray(u_mean, dtype=np.float64).reshape(-1))
     mu_u = np.ascontiguousarray(np.broadcast_to(np.asarray(muu, dtype=np.float64), (m,)))
-    uv = np.asfortranarray(np.asarray(u_var, dtype=np.float64).reshape(m, m))
+    uv = (None if u_var is None
+          else np.asfortranarray(np.asarray(u_var, dtype=np.float64).reshape(m, m)))
     mu_p = np.ascontiguousarray(np.broadcast_to(np.asarray(mu, dtype=np.float64), (npred,)))
     pm = np.zeros(npred, dtype=np.float64)
     pv = np.zeros((npred, npred) if full_cov else npred, dtype=np.float64, order="F")
     _lib.check(lib.sgp_predict(_device(), _lib.KERNELS[cov_fun], _lib.dptr(theta), float(delta),
                                method, 1 if gaussian else 0, _lib.dptr(U), m, m, _lib.dptr(um),
-                               _lib.dptr(mu_u), _lib.dptr(uv), m, _lib.dptr(xp), npred, npred, d,
+                               _lib.dptr(mu_u), None if uv is None else _lib.dptr(uv), m,
+                               _lib.dptr(xp), npred, npred, d,
                                _lib.dptr(mu_p), 1 if full_cov else 0, _lib.dptr(pm),
                                _lib.dptr(pv), npred))
     return {"pred_mean": pm.reshape(-1, 1), "pred_var": pv}
@@ -80,8 +83,14 @@ def predict_gp(mod, x_pred, mu_pred=None, full_cov=False, vi=False):
               "to make predictions. Setting the mean to be zero.")
         mu_pred = np.zeros(x_pred.shape[0])
     if not mod.get("sparse", True):
-        raise NotImplementedError("full-GP prediction (predict_gp_full / predict_laplace_full) "
-                                  "is outside this build's scope (DESIGN.md sec. 8)")
+        if family != "gaussian":
+            raise NotImplementedError("predict_laplace_full (full-GP Poisson / Bernoulli fits) "
+                                      "is outside this build's scope (DESIGN.md sec. 8)")
+        from .full import predict_gp_full
+        pred = predict_gp_full(res["xy"], res["y"], x_pred, res["cov_fun"], res["cov_par"],
+                               res["mu"], mu_pred, full_cov, delta)
+        return {"pred": pred, "sparse": False, "family": family, "x_pred": x_pred,
+                "inverse_link": inv_link}
     m = np.asarray(res["xu"]).shape[0]
     if vi:
         pred = predict_vi(res["u_mean"], res["u_var"], res["xu"], x_pred, res["cov_fun"],

@@ -141,6 +141,17 @@ class SparseGPContext:
         _lib.check(st)
         return obj.value, grad
 
+    def eval_full(self, theta, cov_fun, delta=1e-6, obj_only=False):
+        """Full Gaussian GP over this context's rows (m_max >= n): log dmvnorm(y; mu, Sigma11)
+        and dlogp_dcov_par_full (grad None with obj_only)."""
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        obj = C.c_double(0.0)
+        grad = None if obj_only else np.zeros(theta.size, dtype=np.float64)
+        _lib.check(self._lib.sgp_eval_full(self.handle, _lib.KERNELS[cov_fun], _lib.dptr(theta),
+                                           float(delta), self._flags(False, obj_only),
+                                           C.byref(obj), None if grad is None else _lib.dptr(grad)))
+        return obj.value, grad
+
     def enable_knot_grad(self, on=True):
         """Also contract the adjoint against dK/du (knot gradients; d <= 8)."""
         _lib.check(self._lib.sgp_ctx_enable_knot_grad(self.handle, 1 if on else 0))

@@ -251,3 +251,39 @@ def test_vi_candidate_bordering_matches_rebuild(cfg):
         ref = O.elbo_eval(P["cov_par"], P["cov_fun"], np.vstack([P["U"], cand[k]]), P["X"],
                           P["y"], P["mu"], P["delta"])
         assert abs(got[k] - ref) < 1e-10 * abs(ref)
+
+
+def test_full_gp_gradient_is_the_objective_derivative_at_zero_mean():
+    """dlogp_dcov_par_full uses alpha = Sigma11^-1 y (not y - mu): it is the derivative of
+    obj_fun_norm_full exactly when mu = 0 (central differences in log theta)."""
+    import math
+    from collections import OrderedDict
+    rng = np.random.default_rng(3)
+    X = rng.uniform(0, 10, (40, 2))
+    y = np.sin(X).sum(1) + rng.normal(0, .3, 40)
+    z = np.zeros(40)
+    for cov_fun, cp in (("sqexp", OrderedDict(sigma=1.2, l=1.5, tau=0.4)),
+                        ("ard", OrderedDict(sigma=0.9, l1=1.1, l2=2.0, tau=0.3))):
+        g = O.dlogp_dcov_par_full(cp, cov_fun, X, y, z)["gradient"]
+        for k in cp:
+            a, b = OrderedDict(cp), OrderedDict(cp)
+            a[k] *= math.exp(1e-6)
+            b[k] *= math.exp(-1e-6)
+            fd = (O.full_obj_eval(a, cov_fun, X, y, z) - O.full_obj_eval(b, cov_fun, X, y, z)) / 2e-6
+            assert abs(g[k] - fd) < 1e-6 * max(1.0, abs(fd)), (cov_fun, k, g[k], fd)
+    # duplicate rows: Sigma11 carries the nugget on its diagonal only, but dsig_dthetaC puts
+    # 2 tau^2 on every coincident pair (quirk Q5), so tau's reference gradient gains
+    # 2 tau^2 * G_ij * 2 over the off-diagonal coincident pair (i, j), G = (a a^T - S^-1) / 2
+    Xd = X.copy()
+    Xd[5] = Xd[9]
+    cp = OrderedDict(sigma=1.2, l=1.5, tau=0.4)
+    g = O.dlogp_dcov_par_full(cp, "sqexp", Xd, y, z)["gradient"]
+    a, b = OrderedDict(cp), OrderedDict(cp)
+    a["tau"] *= math.exp(1e-6)
+    b["tau"] *= math.exp(-1e-6)
+    fd = (O.full_obj_eval(a, "sqexp", Xd, y, z) - O.full_obj_eval(b, "sqexp", Xd, y, z)) / 2e-6
+    S = O.full_sigma(cp, "sqexp", Xd, 1e-6)
+    al = np.linalg.solve(S, y)
+    Si = np.linalg.inv(S)
+    extra = 2 * 0.4 ** 2 * (al[5] * al[9] - Si[5, 9])      # (1/2) * 2 entries (5,9), (9,5)
+    assert abs(g["tau"] - (fd + extra)) < 1e-6 * abs(fd)
