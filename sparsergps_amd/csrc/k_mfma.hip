@@ -104,11 +104,10 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
     va0 = gA[o_]; va1 = gA[o_ + 16]; va2 = gA[o_ + 32]; va3 = gA[o_ + 48];      \
     vb0 = gB[o_]; vb1 = gB[o_ + 16]; vb2 = gB[o_ + 32]; vb3 = gB[o_ + 48];      \
     if (w != nullptr) wi = w[rbeg + (int64_t)(step) * BK + lrow];               \
-    if (tid < BK) {                                                             \
+    if (tid < BK) {   /* raw loads only: arithmetic here would wait on every load above */ \
       const int64_t rr_ = rbeg + (int64_t)(step) * BK + tid;                    \
-      const double rv_ = r[rr_];                                                \
-      vrr = rv_;                                                                \
-      vr = (tv != nullptr) ? tv[rr_] : ((w != nullptr) ? w[rr_] * rv_ : rv_);   \
+      vrr = r[rr_];                                                             \
+      vr = (tv != nullptr) ? tv[rr_] : ((w != nullptr) ? w[rr_] : 1.0);         \
     }                                                                           \
   }
 #define SYRK_SSTORE(buf)                                                        \
@@ -120,7 +119,10 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
     pa_[32] = make_double2(va2.x * wi, va2.y * wi);                             \
     pa_[48] = make_double2(va3.x * wi, va3.y * wi);                             \
     pb_[0] = vb0; pb_[16] = vb1; pb_[32] = vb2; pb_[48] = vb3;                  \
-    if (tid < BK) { rw[buf][tid] = vr; rv[buf][tid] = vrr; }                    \
+    if (tid < BK) {                                                             \
+      rw[buf][tid] = (tv != nullptr) ? vr : vr * vrr;   /* (w r)_i or tv_i */      \
+      rv[buf][tid] = vrr;                                                       \
+    }                                                                           \
   }
 
   if (nsteps > 0) {
