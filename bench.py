@@ -31,7 +31,7 @@ HBM_PEAK_GBS = 8000.0
 
 def make_problem(config, n=None, m=None):
     """Synthetic inputs of SURVEY.md 8(d) (numpy PCG64 streams); no reference files read."""
-    from oracle.sgp_oracle import make_gaussian_problem, make_poisson_problem  # generators only
+    from sparsergps_amd.workloads import make_gaussian_problem, make_poisson_problem
     if config == "C5":
         return make_poisson_problem(n=n, m=m)
     return make_gaussian_problem(config, n=n, m=m)
@@ -45,7 +45,7 @@ def cpu_baseline(sizes=(500, 1000, 2000), n_target=1_000_000, m=1024):
     from oracle import sgp_oracle as O
     ts = []
     for ns in sizes:
-        P = O.make_gaussian_problem("C3", n=ns, m=m)
+        P = make_problem("C3", n=ns, m=m)
         t0 = time.perf_counter()
         O.elbo_eval(P["cov_par"], "ard", P["U"], P["X"], P["y"], P["mu"], P["delta"])
         O.delbo_dcov_par(P["cov_par"], "ard", P["U"], P["X"], P["y"], P["mu"], P["delta"])

@@ -15,7 +15,7 @@ def main():
     import torch
 
     import sparsergps_amd as S
-    from oracle.sgp_oracle import make_gaussian_problem
+    from sparsergps_amd.workloads import make_gaussian_problem
     from sparsergps_amd.dist import HipRowBackend
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     P = make_gaussian_problem("C3")
