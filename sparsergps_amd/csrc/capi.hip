@@ -145,6 +145,10 @@ struct sgp_ctx {
   // K22 stage runs on `aux` concurrently with phase 1 (it depends only on U and theta)
   hipStream_t aux = nullptr;
   hipEvent_t ev_knots = nullptr, ev_k22 = nullptr;
+  // phase 2's Bm-independent m x m work (K22inv S K22inv, tr(K22inv S)) also runs on `aux`,
+  // concurrently with the latency-bound Bm inversion on the main stream
+  hipEvent_t ev_s = nullptr, ev_m3 = nullptr;
+  double* slab_aux = nullptr;             // partials of the aux stream's small reductions
   // launch-bound Bm factorisation captured once per (mp, S pointer) and replayed
   hipGraphExec_t g_bm = nullptr, g_k22 = nullptr;
   hipGraph_t g_bm_graph = nullptr, g_k22_graph = nullptr;
@@ -266,7 +270,7 @@ void ctx_free(sgp_ctx* c) {
   void* ptrs[] = {c->X,      c->r,     c->K,      c->alpha,   c->zinv,  c->U,    c->K22,
                   c->K22inv, c->Bm,    c->Binv,   c->Pm,      c->Xt,    c->T1,   c->M3,
                   c->dinv,   c->logd22, c->logdB, c->uvec,    c->cdiag, c->status, c->red1,
-                  c->red2,   c->slab_syrk, c->slab_con, c->slab_small, c->sc,
+                  c->red2,   c->slab_syrk, c->slab_con, c->slab_small, c->slab_aux, c->sc,
                   c->Xt22,   c->T22,    c->dinv22, c->omega, c->pvec, c->rowq, c->red2f,
                   c->y,      c->mu,     c->lv,     c->lm,    c->lslab, c->lred[0], c->lred[1],
                   c->Cprev,  c->knot_slab, c->knot_part, c->knot_kmm, c->tslab};
@@ -282,6 +286,8 @@ void ctx_free(sgp_ctx* c) {
   if (c->ev_pin) hipEventDestroy(c->ev_pin);
   if (c->pin) hipHostFree(c->pin);
   if (c->ev_k22) hipEventDestroy(c->ev_k22);
+  if (c->ev_s) hipEventDestroy(c->ev_s);
+  if (c->ev_m3) hipEventDestroy(c->ev_m3);
   if (c->aux) hipStreamDestroy(c->aux);
   for (hipEvent_t e : c->pool) hipEventDestroy(e);
   if (c->own) hipStreamDestroy(c->own);
@@ -527,9 +533,16 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
     return SGP_EHIP;
   }
   c->stream = c->own;
-  if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+  // aux at the highest priority: its K22 chain (a few hundred short workgroups per launch)
+  // would otherwise queue behind the builder's tens of thousands
+  int prio_least = 0, prio_greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess)
+    prio_greatest = 0;
+  if (hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, prio_greatest) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_knots, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_k22, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_k22, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_s, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_m3, hipEventDisableTiming) != hipSuccess) {
     set_err("hipStream/hipEvent creation failed");
     ctx_free(c);
     delete c;
@@ -570,6 +583,7 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->slab_syrk, c->slab_syrk_cap);
   st = st ? st : dalloc(&c->slab_con, c->slab_con_cap);
   st = st ? st : dalloc(&c->slab_small, SLAB_SMALL);
+  st = st ? st : dalloc(&c->slab_aux, 1024);
   st = st ? st : dalloc(&c->sc, SC_N);
   st = st ? st : dalloc(&c->y, np_);
   st = st ? st : dalloc(&c->mu, np_);
@@ -954,26 +968,38 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
   const double* t = red1 + mm;
   c->n_global = n_global;
   c->flags = flags;
+  {
+    // tr(K22inv S) and M3 = K22inv S K22inv need S and K22inv only: on `aux`, overlapping the
+    // Bm inversion (T22 is free once the K22 chain, earlier on `aux`, has finished)
+    HIPCHK(hipEventRecord(c->ev_s, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->aux, c->ev_s, 0));
+    Scope ta(c, "m3_aux", c->aux);
+    HIPCHK(launch_dot(c->K22inv, S, mm, c->slab_aux, c->sc + SC_TRKS, c->aux));
+    if (!(flags & SGP_FLAG_OBJ_ONLY)) {
+      HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->K22inv, mp, S, mp, 0.0,
+                           c->T22, mp, c->aux));
+      HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->T22, mp, c->K22inv, mp, 0.0,
+                           c->M3, mp, c->aux));
+    }
+    HIPCHK(hipEventRecord(c->ev_m3, c->aux));
+  }
   int st = bm_stage(c, S, 1.0 / z);
   if (st) return st;
   {
     Scope tm(c, "mm_vectors");
     HIPCHK(dense_gemv(c->Binv, mp, t, 1.0 / z, c->uvec, c->stream));         // u = Binv t / z
     HIPCHK(launch_dot(t, c->uvec, mp, c->slab_small, c->sc + SC_TU, c->stream));
-    HIPCHK(launch_dot(c->K22inv, S, mm, c->slab_small, c->sc + SC_TRKS, c->stream));
     HIPCHK(hipMemcpyAsync(c->sc + SC_RR, red1 + mm + mp, sizeof(double), hipMemcpyDeviceToDevice,
                           c->stream));
     if (flags & SGP_FLAG_OBJ_ONLY) {   // elbo_fun alone: no adjoint work
+      HIPCHK(hipStreamWaitEvent(c->stream, c->ev_m3, 0));
       c->phase = 2;
       return SGP_OK;
     }
     HIPCHK(launch_dot(c->Binv, S, mm, c->slab_small, c->sc + SC_TRBS, c->stream));
-    // P = tau^-2 K22inv - z^-1 Binv ; M3 = K22inv S K22inv
+    // P = tau^-2 K22inv - z^-1 Binv
     HIPCHK(dense_axpby(1.0 / kp.tau2, c->K22inv, -1.0 / z, c->Binv, c->Pm, mm, c->stream));
-    HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->K22inv, mp, S, mp, 0.0, c->T1,
-                         mp, c->stream));
-    HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->T1, mp, c->K22inv, mp, 0.0,
-                         c->M3, mp, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_m3, 0));
   }
   {
     Scope tm(c, "contract_kmm");

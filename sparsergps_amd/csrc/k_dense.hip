@@ -260,10 +260,20 @@ __device__ __forceinline__ void gj_mm64(const double* As, const double* Bs, d4 (
   }
 }
 
-__device__ __forceinline__ void gj_load_tile(double* S, const double* G, int64_t ldg) {
-  for (int e = threadIdx.x; e < 4096; e += 256) {
-    const int r = e >> 6, c = e & 63;
-    S[r * GJ_LS + c] = G[r * ldg + c];
+// Global loads of a 64x64 tile into registers (16 per thread, coalesced rows) and their LDS
+// stores, split so that every load of a step is in flight before the first one is waited on.
+__device__ __forceinline__ void gj_ld(double (&v)[16], const double* G, int64_t ldg) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = threadIdx.x + 256 * q;
+    v[q] = G[(int64_t)(e >> 6) * ldg + (e & 63)];
+  }
+}
+__device__ __forceinline__ void gj_st(double* S, const double (&v)[16]) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = threadIdx.x + 256 * q;
+    S[(e >> 6) * GJ_LS + (e & 63)] = v[q];
   }
 }
 
@@ -281,14 +291,17 @@ __global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   d4 acc[2][2];
+  double v0[16], v1[16];
   if (i == k) {
     if (j == k) {
       for (int e = threadIdx.x; e < 4096; e += 256)
         An[(oi + (e >> 6)) * lda + oj + (e & 63)] = Pk[e];
       return;
     }
-    gj_load_tile(S0, Pk, 64);
-    gj_load_tile(S1, Ao + ok * lda + oj, lda);
+    gj_ld(v0, Pk, 64);
+    gj_ld(v1, Ao + ok * lda + oj, lda);
+    gj_st(S0, v0);
+    gj_st(S1, v1);
     __syncthreads();
     gj_mm64(S0, S1, acc);
 #pragma unroll
@@ -303,11 +316,13 @@ __global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
         }
     return;
   }
-  gj_load_tile(S0, Ao + oi * lda + ok, lda);     // C_i = Ao_ik
-  gj_load_tile(S1, Pk, 64);
-  __syncthreads();
-  gj_mm64(S0, S1, acc);                          // C_i P_k
+  gj_ld(v0, Ao + oi * lda + ok, lda);            // C_i = Ao_ik
+  gj_ld(v1, Pk, 64);
   if (j == k) {
+    gj_st(S0, v0);
+    gj_st(S1, v1);
+    __syncthreads();
+    gj_mm64(S0, S1, acc);                        // C_i P_k
 #pragma unroll
     for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
@@ -320,6 +335,23 @@ __global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
         }
     return;
   }
+  // the remaining operands (Ao_kj, and Ao_ij in the accumulator layout) are loaded now as well
+  double v2[16], aij[2][2][4];
+  gj_ld(v2, Ao + ok * lda + oj, lda);
+#pragma unroll
+  for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
+        const int c = wc * 32 + fn * 16 + (lane & 15);
+        aij[fm][fn][q] = Ao[(oi + r) * lda + oj + c];
+      }
+  gj_st(S0, v0);
+  gj_st(S1, v1);
+  __syncthreads();
+  gj_mm64(S0, S1, acc);                          // C_i P_k
   __syncthreads();                               // everyone is done reading S0 / S1
 #pragma unroll
   for (int fm = 0; fm < 2; ++fm)
@@ -331,7 +363,7 @@ __global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
         const int c = wc * 32 + fn * 16 + (lane & 15);
         S0[r * GJ_LS + c] = acc[fm][fn][q];
       }
-  gj_load_tile(S1, Ao + ok * lda + oj, lda);     // Ao_kj
+  gj_st(S1, v2);                                 // Ao_kj
   __syncthreads();
   gj_mm64(S0, S1, acc);                          // (C_i P_k) Ao_kj
   const bool look_ahead = (i == k + 1) && (j == k + 1);
@@ -344,9 +376,8 @@ __global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
       for (int q = 0; q < 4; ++q) {
         const int r = wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
         const int c = wc * 32 + fn * 16 + (lane & 15);
-        const int64_t g = (oi + r) * lda + oj + c;
-        const double v = Ao[g] - acc[fm][fn][q];
-        An[g] = v;
+        const double v = aij[fm][fn][q] - acc[fm][fn][q];
+        An[(oi + r) * lda + oj + c] = v;
         if (look_ahead) S0[r * GJ_LS + c] = v;
       }
   if (look_ahead) {

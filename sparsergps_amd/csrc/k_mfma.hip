@@ -403,6 +403,9 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     ku = fma(va3.x, u_[6], ku); ku = fma(va3.y, u_[7], ku);                      \
   }
 
+#ifdef SGP_CON_TRACE
+  if (tid == 0) SGP_CON_TRACE(0);
+#endif
   CON_GLOAD(0);
   CON_SSTORE(0);
   __syncthreads();
@@ -433,7 +436,13 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
 #undef CON_GLOAD
 #undef CON_SSTORE
 #undef CON_KU
+  // the epilogue's MFMAs and VALU win arbitration over the co-resident workgroup's k-loop (same
+  // total matrix-pipe work, but this tile finishes sooner and its successor starts sooner)
+  __builtin_amdgcn_s_setprio(1);
 
+#ifdef SGP_CON_TRACE
+  if (tid == 0) SGP_CON_TRACE(1);
+#endif
   // ---------------- alpha (per row), shared by both epilogues ----------------
   double* s_alpha = lds;                    // 128
   double* s_rs = s_alpha + T128;            // 128
@@ -521,6 +530,22 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
       // The C fragment of K P is read directly as the A operand of v_mfma_f64_16x16x4 (its lane
       // map is that of W^T), so D costs 4 MFMAs per 16x16 fragment instead of ~3 d VALU ops
       // per pair.
+      // K_ij is read back through LDS: per 16-row fragment fm, the 32 tile rows the four waves
+      // need (fm-th 16 rows of each 64-row half) are copied global -> LDS by LDS-DMA (one
+      // 1 KiB row per wave-instruction, no VGPRs held), the first stage before the coordinate
+      // staging so its latency hides behind it.  (Fragment-shaped loads straight to VGPRs
+      // serialised on one HBM round trip per fragment at this register pressure.)
+      constexpr int KST = 136;                  // stage row stride (doubles)
+      double* kst = s_us + ((T128 * sus + 1) & ~1);   // 32 x KST, 16-byte aligned
+#define CON_KSTAGE(fm_)                                                                  \
+      _Pragma("unroll") for (int q_ = 0; q_ < 8; ++q_) {                                 \
+        const int rho_ = wv * 8 + q_;                                                    \
+        const int64_t row_ = i0 + (rho_ >> 4) * 64 + (fm_) * 16 + (rho_ & 15);           \
+        __builtin_amdgcn_global_load_lds(                                                \
+            (const __attribute__((address_space(1))) void*)(K + row_ * mp + j0 + 2 * lane), \
+            (__attribute__((address_space(3))) void*)(kst + rho_ * KST), 16, 0, 0);       \
+      }
+      CON_KSTAGE(0);
       for (int e = tid; e < T128 * 8; e += 256) {
         const int rr = e % T128, c = e / T128;
         const int64_t i = i0 + rr, j = j0 + rr;
@@ -533,8 +558,13 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
         s_xs[rr * 16 + c] = xv;
         s_xs[rr * 16 + 8 + c] = xv * xv;
       }
+      __builtin_amdgcn_s_waitcnt(0);            // K stage 0 (LDS-DMA) landed
       __syncthreads();
-      s_kn = s_us + T128 * sus;                // KNOT: [2 (wr)][128 cols][d]
+      s_kn = s_us + ((T128 * sus + 1) & ~1);   // KNOT: [2 (wr)][128 cols][d] (aliases the K
+                                               // stage below; written after its last use)
+#ifdef SGP_CON_TRACE
+      if (tid == 0) SGP_CON_TRACE(4);
+#endif
 
       d4 P[4];
       double Cc[4], ucol[4], vcol[4];
@@ -550,6 +580,10 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
       }
 #pragma unroll
       for (int fm = 0; fm < 4; ++fm) {
+        if (fm > 0) {                           // stage fm landed (and is visible to all)
+          __builtin_amdgcn_s_waitcnt(0);
+          __syncthreads();
+        }
         double xb[4];
 #pragma unroll
         for (int r4 = 0; r4 < 4; ++r4)
@@ -559,8 +593,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
           const int col = wc * 64 + fn * 16 + (lane & 15);
           double kv[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            kv[q] = Kt[(int64_t)(wr * 64 + fm * 16 + (lane >> 4) + 4 * q) * mp + col];
+          for (int q = 0; q < 4; ++q) kv[q] = kst[(wr * 16 + (lane >> 4) + 4 * q) * KST + col];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
@@ -576,7 +609,16 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
           for (int r4 = 0; r4 < 4; ++r4)
             P[fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[fm][fn][r4], xb[r4], P[fn], 0, 0, 0);
         }
+#ifdef SGP_CON_TRACE
+        if (fm == 0 && tid == 0) SGP_CON_TRACE(3);
+#endif
+        __syncthreads();                        // everyone is done reading the stage
+        if (fm < 3) { CON_KSTAGE(fm + 1); }
       }
+#undef CON_KSTAGE
+#ifdef SGP_CON_TRACE
+      if (tid == 0) SGP_CON_TRACE(5);
+#endif
       // D fragment fn: lane l, register q -> column wc*64 + fn*16 + (l>>4) + 4q, c' = l & 15
       const int cp = lane & 15, cc = cp & 7;
       double E = 0.0;
@@ -694,6 +736,9 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
       }
     }
 
+#ifdef SGP_CON_TRACE
+    if (tid == 0) SGP_CON_TRACE(6);
+#endif
     // record = [e_sig, e_l[0..L-1], c_sum, c_cnt, c_dg, alpha^T alpha]
     // (the coincidence fields stay zero here; k_coinc adds them)
     double v;
@@ -716,6 +761,9 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     __syncthreads();
     if (tid < nrec)   // field-major [nrec][nwg]: coalesced for the reduction (launch_rowsum)
       slab[tid * nwg + wgid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+#ifdef SGP_CON_TRACE
+    if (tid == 0) SGP_CON_TRACE(2);
+#endif
   }
 }
 
