@@ -96,10 +96,18 @@ def main():
     import sparsergps_amd as S
     from sparsergps_amd.dist import HipRowBackend, RowShardedLaplace, RowShardedVI, shard_rows
 
+    # SGP_BENCH_REHEARSE=1: every rank on device 0 with gloo collectives -- exercises the N > 1
+    # control flow (sharding, barriers, max-over-ranks timing) on a one-GPU box; never used for
+    # a reported number (RCCL is the product path)
+    rehearse = os.environ.get("SGP_BENCH_REHEARSE") == "1"
+    dev_index = 0 if rehearse else local_rank
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev_index)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+    dev = torch.device("cuda", dev_index)
 
     P = make_problem(args.config, n=args.n, m=args.m)
     n, m, d = P["X"].shape[0], P["U"].shape[0], P["X"].shape[1]
@@ -109,7 +117,7 @@ def main():
     s0, s1 = shard_rows(n, world, rank)
     n_loc = s1 - s0
 
-    backend = HipRowBackend(P["X"][s0:s1], P["y"][s0:s1], P["mu"][s0:s1], m, local_rank, cov_fun,
+    backend = HipRowBackend(P["X"][s0:s1], P["y"][s0:s1], P["mu"][s0:s1], m, dev_index, cov_fun,
                             args.mode)
     ctx = backend.ctx
     nr_iters = []

@@ -1,0 +1,125 @@
+// k-loop anatomy of the f64 MFMA kernels (k_syrk / k_contract shape): 128x128 tile per
+// 256-thread workgroup (4 waves as 2x2 of 64x64, 4x4 v_mfma_f64_16x16x4 fragments per wave),
+// BK = 16 per step, register-staged double-buffered LDS, one barrier per step, 2 WGs per CU.
+// Variants switch off parts of the loop to locate the matrix-pipe bubbles:
+//   MODE 0  full loop (global loads -> regs -> LDS, barrier, LDS fragment reads, MFMA)
+//   MODE 1  no global loads (LDS stores of register constants)
+//   MODE 2  no global loads, no LDS stores (fragment reads + barrier + MFMA)
+//   MODE 3  no barrier (fragment reads + MFMA only)
+//   MODE 4  MFMA only (fragments in registers)
+//   build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -o kloop kloop.hip ; run: ./kloop
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+constexpr int BK = 16, SB = 144;
+
+template <int MODE>
+__global__ void __launch_bounds__(256, 2) k_loop(const double* __restrict__ K, int64_t mp,
+                                                 int nsteps, double* out) {
+  __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
+  __shared__ __attribute__((aligned(16))) double Kb[2][BK * SB];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int ta = blockIdx.x % 8, tb = (blockIdx.x / 8) % 8;
+  const int64_t rbeg = (int64_t)(blockIdx.x / 64) * nsteps * BK;
+  d4 acc[4][4];
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+  const int lrow = tid >> 4, lc = tid & 15;
+  const double2* gA = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + ta * 128) + lc;
+  const double2* gB = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + tb * 128) + lc;
+  const int64_t gstep = BK * mp / 2;
+  double2 va0, va1, va2, va3, vb0, vb1, vb2, vb3;
+  va0 = va1 = va2 = va3 = vb0 = vb1 = vb2 = vb3 = make_double2(1.0 + tid * 1e-9, 1.0);
+  auto gload = [&](int step) {
+    const int64_t o = (int64_t)step * gstep;
+    va0 = gA[o]; va1 = gA[o + 16]; va2 = gA[o + 32]; va3 = gA[o + 48];
+    vb0 = gB[o]; vb1 = gB[o + 16]; vb2 = gB[o + 32]; vb3 = gB[o + 48];
+  };
+  auto sstore = [&](int buf) {
+    double2* pa = reinterpret_cast<double2*>(&Ka[buf][lrow * SB]) + lc;
+    double2* pb = reinterpret_cast<double2*>(&Kb[buf][lrow * SB]) + lc;
+    pa[0] = va0; pa[16] = va1; pa[32] = va2; pa[48] = va3;
+    pb[0] = vb0; pb[16] = vb1; pb[32] = vb2; pb[48] = vb3;
+  };
+  if (MODE == 0) gload(0);
+  sstore(0);
+  sstore(1);
+  __syncthreads();
+  double rf[4] = {1.0 + lane * 1e-7, 1.0, 1.0, 1.0};
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
+    if (MODE == 0 && step + 1 < nsteps) gload(step + 1);
+    const double* As = Ka[cur];
+    const double* Bs = Kb[cur];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int krow = kk * 4 + (lane >> 4);
+      double af[4], bf[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        if (MODE <= 3) {
+          af[f] = As[krow * SB + wr * 64 + f * 16 + (lane & 15)];
+          bf[f] = Bs[krow * SB + wc * 64 + f * 16 + (lane & 15)];
+        } else {
+          af[f] = rf[f];
+          bf[f] = rf[(f + kk) & 3];
+        }
+      }
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
+    }
+    if (MODE <= 1 && step + 1 < nsteps) sstore(cur ^ 1);
+    if (MODE <= 2) __syncthreads();
+  }
+  double s = 0.0;
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b) s += acc[a][b][0] + acc[a][b][1] + acc[a][b][2] + acc[a][b][3];
+  if (s == 1234.5) out[tid] = s;
+}
+
+template <int MODE>
+void run(const double* K, int64_t mp, int nsteps, double* out) {
+  const int nwg = 512;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  hipLaunchKernelGGL(k_loop<MODE>, dim3(nwg), dim3(256), 0, 0, K, mp, nsteps / 4, out);
+  hipEventRecord(e0);
+  hipLaunchKernelGGL(k_loop<MODE>, dim3(nwg), dim3(256), 0, 0, K, mp, nsteps, out);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms; hipEventElapsedTime(&ms, e0, e1);
+  const double flops = 2.0 * 128 * 128 * 16 * (double)nsteps * nwg;
+  printf("MODE %d: %.3f ms  %.2f TF/s\n", MODE, ms, flops / (ms * 1e-3) / 1e12);
+}
+
+int main() {
+  const int64_t mp = 1024, rows = 8 * 16 * 4000;   // 8 row chunks x 4000 steps
+  double *K, *out;
+  hipMalloc(&K, rows * mp * 8);
+  hipMalloc(&out, 4096);
+  {
+    // random operands in (0, 1): switching activity like K12 (DVFS lowers the clock on it)
+    double* h = (double*)malloc(rows * mp * 8);
+    unsigned long long st = 88172645463325252ull;
+    for (int64_t i = 0; i < rows * mp; ++i) {
+      st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+      h[i] = (double)(st >> 11) * (1.0 / 9007199254740992.0);
+    }
+    (void)hipMemcpy(K, h, rows * mp * 8, hipMemcpyHostToDevice);
+    free(h);
+  }
+  const int nsteps = 4000;
+  run<0>(K, mp, nsteps, out);
+  run<1>(K, mp, nsteps, out);
+  run<2>(K, mp, nsteps, out);
+  run<3>(K, mp, nsteps, out);
+  run<4>(K, mp, nsteps, out);
+  run<0>(K, mp, nsteps, out);
+  return 0;
+}
