@@ -1137,7 +1137,7 @@ int sgp_fitc_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U
   {
     Scope t(c, "build_knm");
     HIPCHK(launch_build_knm(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp, m, mp, c->K,
-                            c->stream));
+                            c->stream, true));   // beside the K22 chain on aux
   }
   HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_fitc_red1_count(m), c->stream));
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
@@ -1421,7 +1421,7 @@ int sgp_lap_begin(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   {
     Scope t(c, "build_knm");
     HIPCHK(launch_build_knm(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp, m, mp, c->K,
-                            c->stream));
+                            c->stream, true));   // beside the K22 chain on aux
   }
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
   {

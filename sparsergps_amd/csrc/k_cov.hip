@@ -7,6 +7,8 @@
 // parameters up by name per pair; here one thread owns one (i, j) pair per iteration, rows
 // are staged in LDS, knots live in registers and stores are coalesced along the output's
 // contiguous dimension.  These kernels are HBM-write-bound (8 B stored per pair).
+#include <stdlib.h>
+
 #include "sgp_internal.h"
 
 namespace {
@@ -98,8 +100,9 @@ __global__ void __launch_bounds__(256) k_fill(KernParams kp, const double* __res
 }
 
 // K12 row-major (n_pad x mp).  Block: 64 knot columns (lanes) x 4 row groups; each block
-// owns 64 rows.  Row coordinates (pre-scaled by 1/l_c for ARD) are staged in LDS and read as
-// wave-wide broadcasts; the lane's knot stays in registers; one coalesced 512-B store per row.
+// walks 64-row blocks blockIdx.y, blockIdx.y + gridDim.y, ...  Row coordinates (pre-scaled by
+// 1/l_c for ARD) are staged in LDS and read as wave-wide broadcasts; the lane's knot stays in
+// registers; one coalesced 512-B store per row.  Row blocks [rb0, rb1).
 template <bool ARD, int DT>
 __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* __restrict__ X,
                                                    int64_t ldx, int64_t n,
@@ -107,23 +110,14 @@ __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* 
                                                    int64_t m, int64_t mp,
                                                    double* __restrict__ K,
                                                    const double* __restrict__ rvec,
-                                                   double* __restrict__ tslab) {
+                                                   double* __restrict__ tslab, int64_t rb0,
+                                                   int64_t rb1) {
   __shared__ __attribute__((aligned(16))) double xs[64 * DT];
   __shared__ double rsh[64];
   __shared__ double tsh[4][64];
   const int d = kp.d;
   const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  const int64_t i0 = (int64_t)blockIdx.y * 64;
   const int tid = threadIdx.y * 64 + threadIdx.x;
-  for (int e = tid; e < 64 * DT; e += 256) {
-    const int r = e / DT, c = e % DT;
-    const int64_t i = i0 + r;
-    double v = 0.0;
-    if (c < d && i < n) v = ARD ? X[i + c * ldx] * kp.rl[c] : X[i + c * ldx];
-    xs[e] = v;
-  }
-  if (rvec && tid < 64) rsh[tid] = (i0 + tid < n) ? rvec[i0 + tid] : 0.0;
-  double tpart = 0.0;
   double uj[DT];
   const bool jv = j < m;
 #pragma unroll
@@ -131,28 +125,41 @@ __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* 
     uj[c] = (jv && c < d) ? (ARD ? U[j + c * ldu] * kp.rl[c] : U[j + c * ldu]) : 0.0;
   const double sig2 = kp.sig2;
   const double scale = ARD ? -0.5 : kp.coef;
-  __syncthreads();
-  for (int r = threadIdx.y; r < 64; r += 4) {
-    const int64_t i = i0 + r;
-    const double2* xr = reinterpret_cast<const double2*>(&xs[r * DT]);
-    double s = 0.0;
-#pragma unroll
-    for (int c2 = 0; c2 < DT / 2; ++c2) {
-      const double2 xv = xr[c2];
-      const double t0 = xv.x - uj[2 * c2], t1 = xv.y - uj[2 * c2 + 1];
-      s = fma(t0, t0, s);
-      s = fma(t1, t1, s);
+  for (int64_t rb = rb0 + blockIdx.y; rb < rb1; rb += gridDim.y) {
+    const int64_t i0 = rb * 64;
+    __syncthreads();   // the previous row block's xs / rsh / tsh reads are done
+    for (int e = tid; e < 64 * DT; e += 256) {
+      const int r = e / DT, c = e % DT;
+      const int64_t i = i0 + r;
+      double v = 0.0;
+      if (c < d && i < n) v = ARD ? X[i + c * ldx] * kp.rl[c] : X[i + c * ldx];
+      xs[e] = v;
     }
-    const double v = (jv && i < n) ? sig2 * sgp_exp_nonpos(scale * s) : 0.0;
-    K[i * mp + j] = v;
-    if (rvec) tpart = fma(v, rsh[r], tpart);
-  }
-  if (rvec) {   // t_j partial of this block's 64 rows, fixed combination order
-    tsh[threadIdx.y][threadIdx.x] = tpart;
+    if (rvec && tid < 64) rsh[tid] = (i0 + tid < n) ? rvec[i0 + tid] : 0.0;
+    double tpart = 0.0;
     __syncthreads();
-    if (threadIdx.y == 0)
-      tslab[(int64_t)blockIdx.y * mp + j] =
-          ((tsh[0][threadIdx.x] + tsh[1][threadIdx.x]) + tsh[2][threadIdx.x]) + tsh[3][threadIdx.x];
+    for (int r = threadIdx.y; r < 64; r += 4) {
+      const int64_t i = i0 + r;
+      const double2* xr = reinterpret_cast<const double2*>(&xs[r * DT]);
+      double s = 0.0;
+#pragma unroll
+      for (int c2 = 0; c2 < DT / 2; ++c2) {
+        const double2 xv = xr[c2];
+        const double t0 = xv.x - uj[2 * c2], t1 = xv.y - uj[2 * c2 + 1];
+        s = fma(t0, t0, s);
+        s = fma(t1, t1, s);
+      }
+      const double v = (jv && i < n) ? sig2 * sgp_exp_nonpos(scale * s) : 0.0;
+      K[i * mp + j] = v;
+      if (rvec) tpart = fma(v, rsh[r], tpart);
+    }
+    if (rvec) {   // t_j partial of this block's 64 rows, fixed combination order
+      tsh[threadIdx.y][threadIdx.x] = tpart;
+      __syncthreads();
+      if (threadIdx.y == 0)
+        tslab[rb * mp + j] = ((tsh[0][threadIdx.x] + tsh[1][threadIdx.x]) + tsh[2][threadIdx.x]) +
+                             tsh[3][threadIdx.x];
+    }
   }
 }
 
@@ -308,33 +315,76 @@ hipError_t launch_fill_dcov(const KernParams& kp, const double* x, int64_t n, in
   return hipGetLastError();
 }
 
-static hipError_t build_knm_impl(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
-                                 int64_t n_pad, const double* U, int64_t ldu, int64_t m,
-                                 int64_t mp, double* K, const double* r, double* tslab,
-                                 hipStream_t s) {
-  dim3 grid((unsigned)(mp / 64), (unsigned)(n_pad / 64));
+// One builder launch over row blocks [rb0, rb1) with at most wpc workgroups per CU.
+static hipError_t build_knm_range(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
+                                  const double* U, int64_t ldu, int64_t m, int64_t mp, double* K,
+                                  const double* r, double* tslab, int64_t rb0, int64_t rb1,
+                                  int wpc, hipStream_t s) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+              ? prop.multiProcessorCount : 256;
+  }
+  if (rb1 <= rb0) return hipSuccess;
+  const int64_t ncb = mp / 64;
+  int64_t gy = ((int64_t)cus * wpc) / (ncb > 0 ? ncb : 1);
+  gy = gy < 1 ? 1 : (gy > rb1 - rb0 ? rb1 - rb0 : gy);
+  dim3 grid((unsigned)ncb, (unsigned)gy);
   const bool ard = kp.kernel == 1;
   if (kp.kernel == 2) return hipErrorInvalidValue;
   if (kp.d <= 8) {
-    if (ard) hipLaunchKernelGGL((k_build_knm<true, 8>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab);
-    else hipLaunchKernelGGL((k_build_knm<false, 8>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab);
+    if (ard) hipLaunchKernelGGL((k_build_knm<true, 8>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, rb0, rb1);
+    else hipLaunchKernelGGL((k_build_knm<false, 8>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, rb0, rb1);
   } else {
-    if (ard) hipLaunchKernelGGL((k_build_knm<true, SGP_MAXD>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab);
-    else hipLaunchKernelGGL((k_build_knm<false, SGP_MAXD>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab);
+    if (ard) hipLaunchKernelGGL((k_build_knm<true, SGP_MAXD>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, rb0, rb1);
+    else hipLaunchKernelGGL((k_build_knm<false, SGP_MAXD>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, rb0, rb1);
   }
   return hipGetLastError();
 }
 
+// Full-occupancy builder (64 workgroups per CU is more than fit: the hardware limit applies).
+constexpr int BUILD_WPC_FULL = 64;
+// While the K22 Gauss-Jordan chain runs on the high-priority aux stream (VI/FITC phase 1), a
+// builder at full occupancy leaves no CU room for the chain's workgroups (they queue behind
+// the builder's and the SYRK then waits for the chain).  The first row blocks are therefore
+// built at BUILD_WPC_SHARED workgroups per CU, sized to last about as long as the chain, and
+// the rest at full occupancy.
+constexpr int BUILD_WPC_SHARED = 2;
+
+static hipError_t build_knm_impl(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
+                                 int64_t n_pad, const double* U, int64_t ldu, int64_t m,
+                                 int64_t mp, double* K, const double* r, double* tslab,
+                                 int64_t shared_rb, hipStream_t s) {
+  const int64_t nrb = n_pad / 64;
+  if (shared_rb > nrb) shared_rb = nrb;
+  if (shared_rb < 0) shared_rb = 0;
+  hipError_t e = build_knm_range(kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, 0, shared_rb,
+                                 BUILD_WPC_SHARED, s);
+  if (e != hipSuccess) return e;
+  return build_knm_range(kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, shared_rb, nrb,
+                         BUILD_WPC_FULL, s);
+}
+
+// Row blocks built at shared occupancy beside the K22 chain: ~40 us per 64-wide Gauss-Jordan
+// step (+ build and pivot) at ~2.3 GB/ms for the shared-occupancy builder.
+static int64_t chain_shared_rb(int64_t mp) {
+  const double chain_us = 40.0 * (double)(mp / 64) + 100.0;
+  return (int64_t)(chain_us * 2.3e6 / (64.0 * (double)mp * 8.0)) + 1;   // 2.3 GB/ms = 2.3e6 B/us
+}
+
 hipError_t launch_build_knm(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
                             int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
-                            double* K, hipStream_t s) {
-  return build_knm_impl(kp, X, ldx, n, n_pad, U, ldu, m, mp, K, nullptr, nullptr, s);
+                            double* K, hipStream_t s, bool beside_chain) {
+  return build_knm_impl(kp, X, ldx, n, n_pad, U, ldu, m, mp, K, nullptr, nullptr,
+                        beside_chain ? chain_shared_rb(mp) : 0, s);
 }
 
 hipError_t launch_build_knm_t(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
                               int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
                               double* K, const double* r, double* tslab, hipStream_t s) {
-  return build_knm_impl(kp, X, ldx, n, n_pad, U, ldu, m, mp, K, r, tslab, s);
+  return build_knm_impl(kp, X, ldx, n, n_pad, U, ldu, m, mp, K, r, tslab, chain_shared_rb(mp), s);
 }
 
 hipError_t launch_build_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,

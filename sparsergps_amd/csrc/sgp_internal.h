@@ -69,9 +69,11 @@ hipError_t launch_build_knm_t(const KernParams& kp, const double* X, int64_t ldx
                               int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
                               double* K, const double* r, double* tslab, hipStream_t s);
 // K12 (n_pad x mp, row-major, ld = mp).  Rows >= n and columns >= m are written as 0.
+// beside_chain: the K22 chain runs concurrently on the aux stream (phase 1), so the first row
+// blocks are built at reduced occupancy to leave it room (launch_build_knm_t always does).
 hipError_t launch_build_knm(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
                             int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
-                            double* K, hipStream_t s);
+                            double* K, hipStream_t s, bool beside_chain = false);
 // K22 = Kuu + diag_add on the diagonal, padded with identity (mp x mp, row-major).
 // diag value = ((sig2 + tau2 + delta) - diag_sub) exactly like R's make_cov(...) - tau^2 I.
 hipError_t launch_build_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,
