@@ -122,7 +122,7 @@ struct sgp_ctx {
   double *red1 = nullptr, *red2 = nullptr;
   double *slab_syrk = nullptr, *slab_con = nullptr, *slab_small = nullptr, *sc = nullptr;
   double* tslab = nullptr;                // builder t = K^T r partials (VI), n_pad/64 x mp
-  int64_t slab_syrk_cap = 0, slab_con_cap = 0;
+  int64_t slab_syrk_cap = 0, slab_con_cap = 0, slab_small_cap = 0;
   // state carried between phases
   KernParams kp;
   int64_t m = 0, mp = 0, n_global = 0;
@@ -147,7 +147,8 @@ struct sgp_ctx {
   hipEvent_t ev_knots = nullptr, ev_k22 = nullptr;
   // phase 2's Bm-independent m x m work (K22inv S K22inv, tr(K22inv S)) also runs on `aux`,
   // concurrently with the latency-bound Bm inversion on the main stream
-  hipEvent_t ev_s = nullptr, ev_m3 = nullptr;
+  hipEvent_t ev_s = nullptr, ev_m3 = nullptr, ev_bm = nullptr;
+  hipStream_t aux_lo = nullptr;           // ... at normal priority (the Bm chain keeps its CUs)
   double* slab_aux = nullptr;             // partials of the aux stream's small reductions
   // launch-bound Bm factorisation captured once per (mp, S pointer) and replayed
   hipGraphExec_t g_bm = nullptr, g_k22 = nullptr;
@@ -288,7 +289,9 @@ void ctx_free(sgp_ctx* c) {
   if (c->ev_k22) hipEventDestroy(c->ev_k22);
   if (c->ev_s) hipEventDestroy(c->ev_s);
   if (c->ev_m3) hipEventDestroy(c->ev_m3);
+  if (c->ev_bm) hipEventDestroy(c->ev_bm);
   if (c->aux) hipStreamDestroy(c->aux);
+  if (c->aux_lo) hipStreamDestroy(c->aux_lo);
   for (hipEvent_t e : c->pool) hipEventDestroy(e);
   if (c->own) hipStreamDestroy(c->own);
 }
@@ -539,10 +542,12 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess)
     prio_greatest = 0;
   if (hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, prio_greatest) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->aux_lo, hipStreamNonBlocking, prio_least) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_knots, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_k22, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_s, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_m3, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_m3, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_bm, hipEventDisableTiming) != hipSuccess) {
     set_err("hipStream/hipEvent creation failed");
     ctx_free(c);
     delete c;
@@ -582,8 +587,10 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->red2f, sgp_fitc_red2_count(SGP_KERNEL_ARD, SGP_MAXD, m_max) + mp * 8);
   st = st ? st : dalloc(&c->slab_syrk, c->slab_syrk_cap);
   st = st ? st : dalloc(&c->slab_con, c->slab_con_cap);
-  st = st ? st : dalloc(&c->slab_small, SLAB_SMALL);
-  st = st ? st : dalloc(&c->slab_aux, 1024);
+  // small-reduction partials: the dot/colsum helpers, and k_contract_kmm's one record per knot
+  c->slab_small_cap = std::max<int64_t>(SLAB_SMALL, mp * (SGP_MAXD + 2));
+  st = st ? st : dalloc(&c->slab_small, c->slab_small_cap);
+  st = st ? st : dalloc(&c->slab_aux, c->slab_small_cap);
   st = st ? st : dalloc(&c->sc, SC_N);
   st = st ? st : dalloc(&c->y, np_);
   st = st ? st : dalloc(&c->mu, np_);
@@ -640,6 +647,7 @@ int sgp_ctx_destroy(sgp_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->aux) (void)hipStreamSynchronize(c->aux);
+  if (c->aux_lo) (void)hipStreamSynchronize(c->aux_lo);
   ctx_free(c);
   delete c;
   return SGP_OK;
@@ -685,6 +693,7 @@ int sgp_ctx_timings(sgp_ctx* c, char* names, int64_t names_len, double* ms, int 
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipStreamSynchronize(c->aux));
+  HIPCHK(hipStreamSynchronize(c->aux_lo));
   // per-phase totals over the recorded evaluations, in first-seen order
   std::vector<std::string> nm;
   std::vector<double> tot;
@@ -734,7 +743,7 @@ static int contract_pass(sgp_ctx* c, const double* M, ConArgs ca, double* rec_ou
   if (fused) ca.alpha_out = c->alpha;   // k_coinc needs the fused alpha_i
   HIPCHK(launch_contract_args(c->kp, c->K, M, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp, c->m,
                               c->mp, ca, c->slab_con, &nrec, &nwg, c->stream));
-  HIPCHK(launch_rowsum(c->slab_con, nrec, nwg, c->slab_small, SLAB_SMALL, rec_out, c->stream));
+  HIPCHK(launch_rowsum(c->slab_con, nrec, nwg, c->slab_small, c->slab_small_cap, rec_out, c->stream));
   // tau's coincidence sums -> record fields 1+L .. 3+L
   HIPCHK(launch_coinc(c->X, c->n_pad, c->n, c->kp.d, c->U, c->mp, c->m, c->khash, c->kidx, c->K,
                       c->mp, M, ca, fused ? c->alpha : ca.alpha_in, c->slab_small,
@@ -969,19 +978,22 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
   c->n_global = n_global;
   c->flags = flags;
   {
-    // tr(K22inv S) and M3 = K22inv S K22inv need S and K22inv only: on `aux`, overlapping the
-    // Bm inversion (T22 is free once the K22 chain, earlier on `aux`, has finished)
+    // tr(K22inv S) and M3 = K22inv S K22inv need S and K22inv only: on aux_lo beside the Bm
+    // inversion (T22 and K22inv are final once the K22 chain on `aux` has finished).  Beside
+    // the K12 contraction instead, the GEMMs' workgroups starved and slowed it more.
     HIPCHK(hipEventRecord(c->ev_s, c->stream));
-    HIPCHK(hipStreamWaitEvent(c->aux, c->ev_s, 0));
-    Scope ta(c, "m3_aux", c->aux);
-    HIPCHK(launch_dot(c->K22inv, S, mm, c->slab_aux, c->sc + SC_TRKS, c->aux));
+    HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_s, 0));
+    HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_k22, 0));
+    Scope ta(c, "m3_aux", c->aux_lo);
+    HIPCHK(launch_dot(c->K22inv, S, mm, c->slab_aux, c->sc + SC_TRKS, c->aux_lo));
     if (!(flags & SGP_FLAG_OBJ_ONLY)) {
       HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->K22inv, mp, S, mp, 0.0,
-                           c->T22, mp, c->aux));
+                           c->T22, mp, c->aux_lo));
       HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, c->T22, mp, c->K22inv, mp, 0.0,
-                           c->M3, mp, c->aux));
+                           c->M3, mp, c->aux_lo));
+    } else {
+      HIPCHK(hipEventRecord(c->ev_m3, c->aux_lo));
     }
-    HIPCHK(hipEventRecord(c->ev_m3, c->aux));
   }
   int st = bm_stage(c, S, 1.0 / z);
   if (st) return st;
@@ -999,16 +1011,19 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
     HIPCHK(launch_dot(c->Binv, S, mm, c->slab_small, c->sc + SC_TRBS, c->stream));
     // P = tau^-2 K22inv - z^-1 Binv
     HIPCHK(dense_axpby(1.0 / kp.tau2, c->K22inv, -1.0 / z, c->Binv, c->Pm, mm, c->stream));
-    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_m3, 0));
+    HIPCHK(hipEventRecord(c->ev_bm, c->stream));
   }
   {
-    Scope tm(c, "contract_kmm");
+    // sum G22 o dK22/dtheta needs only m x m operands: on aux_lo beside the K12 contraction
+    // (off the critical path; joined before the phase ends)
+    HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_bm, 0));
+    Scope tm(c, "contract_kmm", c->aux_lo);
     int nb = 0;
     HIPCHK(launch_contract_kmm(kp, c->U, c->mp, c->m, mp, c->uvec, c->K22inv, c->Binv, c->M3,
                                -0.5, 0.5, -1.0 / (2.0 * kp.tau2), nullptr, nullptr, 0.0,
-                               c->slab_small, SLAB_SMALL, &nb,
-                               c->stream));
-    HIPCHK(launch_colsum(c->slab_small, nb, kp.P, c->sc + SC_G22, c->stream));
+                               c->slab_aux, c->slab_small_cap, &nb, c->aux_lo));
+    HIPCHK(launch_colsum(c->slab_aux, nb, kp.P, c->sc + SC_G22, c->aux_lo));
+    HIPCHK(hipEventRecord(c->ev_m3, c->aux_lo));
   }
   {
     Scope tm(c, "contract_knm");
@@ -1021,6 +1036,7 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
     int st2 = contract_pass(c, c->Pm, ca, red2, red2 + sgp_vi_red2_count(kp.kernel, kp.d), false);
     if (st2) return st2;
   }
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_m3, 0));   // G22 records (aux_lo)
   c->phase = 2;
   return SGP_OK;
 }
@@ -1251,7 +1267,7 @@ int sgp_fitc_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
     int nb = 0;
     HIPCHK(launch_contract_kmm(kp, c->U, c->mp, c->m, mp, c->uvec, c->K22inv, c->Binv, c->M3,
                                -0.5, 0.5, 0.5, nullptr, nullptr, 0.0, c->slab_small,
-                               SLAB_SMALL, &nb, c->stream));
+                               c->slab_small_cap, &nb, c->stream));
     HIPCHK(launch_colsum(c->slab_small, nb, kp.P, c->sc + SC_G22, c->stream));
   }
   double sc[SC_N], r2[2 * (SGP_MAXD + 5) + 2];
@@ -1624,7 +1640,7 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
       int nb = 0;
       HIPCHK(launch_contract_kmm(kp, c->U, c->mp, c->m, mp, lmv(c, LM_S), c->K22inv, c->Binv,
                                  c->M3, -0.5, 0.5, 1.0, lmv(c, LM_CW), lmv(c, LM_GG), 0.25,
-                                 c->slab_small, SLAB_SMALL, &nb, c->stream));
+                                 c->slab_small, c->slab_small_cap, &nb, c->stream));
       HIPCHK(launch_colsum(c->slab_small, nb, kp.P, c->sc + SC_G22, c->stream));
     }
     const int64_t off = lap_rec_off(mp);
@@ -1770,7 +1786,7 @@ int sgp_eval_full(sgp_ctx* c, int kernel, const double* theta, double delta, uns
     HIPCHK(hipMemsetAsync(c->T1, 0, sizeof(double) * mm, c->stream));
     int nb = 0;
     HIPCHK(launch_contract_kmm(kp, c->U, mp, c->m, mp, c->uvec, c->T1, c->K22inv, c->T1, 0.5,
-                               0.5, 0.0, nullptr, nullptr, 0.0, c->slab_small, SLAB_SMALL, &nb,
+                               0.5, 0.0, nullptr, nullptr, 0.0, c->slab_small, c->slab_small_cap, &nb,
                                c->stream));
     HIPCHK(launch_colsum(c->slab_small, nb, kp.P, c->sc + SC_G22, c->stream));
   }

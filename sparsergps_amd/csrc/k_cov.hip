@@ -187,6 +187,7 @@ __global__ void __launch_bounds__(256) k_build_kmm(KernParams kp, const double* 
 // Per block partial sums of P records: sigma, the length scales, and the tau-coincidence sum
 // sum_{u_j == u_k} G22_jk (dK22/dlog tau = 2 tau^2 there; used by the Laplace path, whose
 // K22 keeps tau^2 -- the Gaussian paths zero dK22/dtau, vi_functions.R:313-316).
+template <int DT>
 __global__ void __launch_bounds__(256) k_contract_kmm(KernParams kp, const double* __restrict__ U,
                                                       int64_t ldu, int64_t m, int64_t mp,
                                                       const double* __restrict__ uvec,
@@ -197,48 +198,61 @@ __global__ void __launch_bounds__(256) k_contract_kmm(KernParams kp, const doubl
                                                       const double* __restrict__ vvec,
                                                       const double* __restrict__ wvec, double e2,
                                                       double* __restrict__ slab) {
-  __shared__ double red[4][SGP_MAXD + 2];
-  const int np = kp.P;
-  double acc[SGP_MAXD + 2];
-  for (int p = 0; p < np; ++p) acc[p] = 0.0;
-  const int64_t total = m * m;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * 256) {
-    const int64_t j = e / m, k = e % m;
-    double uj[SGP_MAXD], uk[SGP_MAXD];
+  // one block per knot row j; compile-time coordinate loops keep everything in registers
+  __shared__ double red[4][DT + 2];
+  const int np = kp.P, d = kp.d;
+  const int64_t j = blockIdx.x;
+  double uj[DT], acc[DT + 2];
+#pragma unroll
+  for (int q = 0; q < DT; ++q) uj[q] = (q < d) ? U[j + q * ldu] : 0.0;
+#pragma unroll
+  for (int p = 0; p < DT + 2; ++p) acc[p] = 0.0;
+  const double auj = a * uvec[j];
+  const double vj = vvec ? vvec[j] : 0.0, wj = vvec ? wvec[j] : 0.0;
+  for (int64_t k = threadIdx.x; k < m; k += 256) {
+    double uk[DT];
     bool same = true;
-    for (int q = 0; q < kp.d; ++q) {
-      uj[q] = U[j + q * ldu];
-      uk[q] = U[k + q * ldu];
+#pragma unroll
+    for (int q = 0; q < DT; ++q) {
+      uk[q] = (q < d) ? U[k + q * ldu] : 0.0;
       same = same && (uj[q] == uk[q]);
     }
     const int64_t o = j * mp + k;
-    double g = a * uvec[j] * uvec[k] + b * (Ainv[o] - Binv[o]) + c * M3[o];
-    if (vvec) g += e2 * (vvec[j] * wvec[k] + wvec[j] * vvec[k]);
+    double g = auj * uvec[k] + b * (Ainv[o] - Binv[o]) + c * M3[o];
+    if (vvec) g += e2 * (vj * wvec[k] + wj * vvec[k]);
     const double kv = kvalue(kp, uj, uk);
     const double gk = g * kv;
     acc[0] += 2.0 * gk;                                   // sigma: dK/dlog sigma = 2K
     if (kp.kernel == 0) {
       double s = 0.0;
-      for (int q = 0; q < kp.d; ++q) { double t = uj[q] - uk[q]; s = fma(t, t, s); }
+#pragma unroll
+      for (int q = 0; q < DT; ++q) {
+        if (q < d) { const double t = uj[q] - uk[q]; s = fma(t, t, s); }
+      }
       acc[1] += gk * s * kp.rl2[0];
     } else {
-      for (int q = 0; q < kp.d; ++q) {
-        double t = (uj[q] - uk[q]) * kp.rl[q];
-        acc[1 + q] += gk * t * t;
+#pragma unroll
+      for (int q = 0; q < DT; ++q) {
+        if (q < d) {
+          const double t = (uj[q] - uk[q]) * kp.rl[q];
+          acc[1 + q] += gk * t * t;
+        }
       }
     }
-    if (same) acc[np - 1] += g;
+    if (same) acc[DT + 1] += g;                           // tau coincidence sum
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int p = 0; p < np; ++p) {
-    double v = wave_sum(acc[p]);
+#pragma unroll
+  for (int p = 0; p < DT + 2; ++p) {
+    const double v = wave_sum(acc[p]);
     if (lane == 0) red[w][p] = v;
   }
   __syncthreads();
-  if (threadIdx.x < np)
-    slab[(int64_t)blockIdx.x * np + threadIdx.x] =
-        red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+  // record layout: [sigma, length scales (L), tau-coincidence] -> P fields
+  if (threadIdx.x < np) {
+    const int src = (threadIdx.x == np - 1) ? DT + 1 : threadIdx.x;
+    slab[j * np + threadIdx.x] = red[0][src] + red[1][src] + red[2][src] + red[3][src];
+  }
 }
 
 // Knot part of the m x m contraction for d K22 / d u_kc = e_k v^T + v e_k^T,
@@ -399,13 +413,15 @@ hipError_t launch_contract_kmm(const KernParams& kp, const double* U, int64_t ld
                                const double* Binv, const double* M3, double a, double b,
                                double c, const double* vvec, const double* wvec, double e2,
                                double* slab, int64_t slab_cap, int* nblocks, hipStream_t s) {
-  int64_t total = m * m;
-  int nb = (int)((total + 255) / 256);
-  if (nb > 1024) nb = 1024;
-  if (nb < 1) nb = 1;
+  const int nb = (int)(m > 0 ? m : 1);   // one block (and one record) per knot row
   *nblocks = nb;
   if ((int64_t)nb * kp.P > slab_cap) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_contract_kmm, dim3(nb), dim3(256), 0, s, kp, U, ldu, m, mp, uvec, Ainv,
-                     Binv, M3, a, b, c, vvec, wvec, e2, slab);
+  if (m <= 0) return hipSuccess;
+  if (kp.d <= 8)
+    hipLaunchKernelGGL(k_contract_kmm<8>, dim3(nb), dim3(256), 0, s, kp, U, ldu, m, mp, uvec,
+                       Ainv, Binv, M3, a, b, c, vvec, wvec, e2, slab);
+  else
+    hipLaunchKernelGGL(k_contract_kmm<SGP_MAXD>, dim3(nb), dim3(256), 0, s, kp, U, ldu, m, mp,
+                       uvec, Ainv, Binv, M3, a, b, c, vvec, wvec, e2, slab);
   return hipGetLastError();
 }
