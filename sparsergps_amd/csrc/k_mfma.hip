@@ -895,8 +895,10 @@ __global__ void __launch_bounds__(256)
 k_gemm64(int64_t M, int64_t N, int64_t Kd, double alpha, const double* __restrict__ A,
          int64_t lda, const double* __restrict__ B, int64_t ldb, double beta,
          double* C, int64_t ldc, int lower_only) {
-  __shared__ double As[64 * GA];
-  __shared__ double Bs[16 * GB];
+  // double-buffered LDS with the next k-step's operands prefetched into registers while the
+  // current step's MFMAs run (Kd is a multiple of 16 at every call site: padded m x m blocks)
+  __shared__ double As[2][64 * GA];
+  __shared__ double Bs[2][16 * GB];
   const int64_t tn = blockIdx.x, tm = blockIdx.y;
   if (lower_only && tm < tn) return;
   const int64_t i0 = tm * 64, j0 = tn * 64;
@@ -907,28 +909,48 @@ k_gemm64(int64_t M, int64_t N, int64_t Kd, double alpha, const double* __restric
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-  for (int64_t k0 = 0; k0 < Kd; k0 += 16) {
+  double ra[4], rb[4];
+  auto gload = [&](int64_t k0) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int e = tid + q * 256;
       int row, kk;
       if (!TA) { row = e >> 4; kk = e & 15; } else { kk = e >> 6; row = e & 63; }
-      const double av = TA ? A[(k0 + kk) * lda + i0 + row] : A[(i0 + row) * lda + k0 + kk];
-      As[row * GA + kk] = av;
+      ra[q] = TA ? A[(k0 + kk) * lda + i0 + row] : A[(i0 + row) * lda + k0 + kk];
       int col, kb;
       if (!TB) { kb = e >> 6; col = e & 63; } else { col = e >> 4; kb = e & 15; }
-      const double bv = TB ? B[(j0 + col) * ldb + k0 + kb] : B[(k0 + kb) * ldb + j0 + col];
-      Bs[kb * GB + col] = bv;
+      rb[q] = TB ? B[(j0 + col) * ldb + k0 + kb] : B[(k0 + kb) * ldb + j0 + col];
     }
-    __syncthreads();
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + q * 256;
+      int row, kk;
+      if (!TA) { row = e >> 4; kk = e & 15; } else { kk = e >> 6; row = e & 63; }
+      As[buf][row * GA + kk] = ra[q];
+      int col, kb;
+      if (!TB) { kb = e >> 6; col = e & 63; } else { col = e >> 4; kb = e & 15; }
+      Bs[buf][kb * GB + col] = rb[q];
+    }
+  };
+  if (Kd > 0) {
+    gload(0);
+    sstore(0);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int64_t k0 = 0; k0 < Kd; k0 += 16) {
+    const bool more = k0 + 16 < Kd;
+    if (more) gload(k0 + 16);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int kx = kk * 4 + (lane >> 4);
       double af[2], bf[2];
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
-        af[f] = As[(wr * 32 + f * 16 + (lane & 15)) * GA + kx];
-        bf[f] = Bs[kx * GB + wc * 32 + f * 16 + (lane & 15)];
+        af[f] = As[cur][(wr * 32 + f * 16 + (lane & 15)) * GA + kx];
+        bf[f] = Bs[cur][kx * GB + wc * 32 + f * 16 + (lane & 15)];
       }
 #pragma unroll
       for (int fm = 0; fm < 2; ++fm)
@@ -936,7 +958,9 @@ k_gemm64(int64_t M, int64_t N, int64_t Kd, double alpha, const double* __restric
         for (int fn = 0; fn < 2; ++fn)
           acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
     }
+    if (more) sstore(cur ^ 1);
     __syncthreads();
+    cur ^= 1;
   }
 #pragma unroll
   for (int fm = 0; fm < 2; ++fm)
@@ -1184,6 +1208,7 @@ hipError_t launch_gemm64(bool transA, bool transB, bool lower_only, int64_t M, i
                          const double* B, int64_t ldb, double beta, double* C, int64_t ldc,
                          hipStream_t s) {
   if (M <= 0 || N <= 0) return hipSuccess;
+  if (M % 64 || N % 64 || K % 16 || K < 0) return hipErrorInvalidValue;   // tile-padded shapes only
   dim3 grid((unsigned)(N / 64), (unsigned)(M / 64));
   const int lo = lower_only ? 1 : 0;
   if (!transA && !transB)
