@@ -166,12 +166,12 @@ def main():
         elapsed = float(tt.item())
     timed_iters = nr_iters[args.warmup:]
 
-    # roofline of the dominant kernel: fused GEMM + gradient contraction (2 n_loc m^2 MFMA flops
-    # per pass; FITC's second pass is timed separately as "contract_knm_b"; Laplace runs two
-    # passes inside "lap_grad_b" together with other work, so its figure is a lower bound)
-    con_key = {"vi": "contract_knm", "fitc": "contract_knm", "laplace": "lap_grad_b"}[args.mode]
+    # roofline of the dominant MFMA kernel, 2 n_loc m^2 flops per launch: VI's fused GEMM +
+    # gradient contraction; FITC / Laplace's row-quadratic GEMM pass diag(K12 K22^-1 K21) (their
+    # gradient passes read the products the row-quadratic passes stored, no GEMM of their own)
+    con_key = {"vi": "contract_knm", "fitc": "rowquad_q", "laplace": "rowquad_q"}[args.mode]
     t_con = phase_avg.get(con_key, float("nan")) * 1e-3
-    flops = 2.0 * n_loc * m * m * (2 if args.mode == "laplace" else 1)
+    flops = 2.0 * n_loc * m * m
     achieved = flops / t_con / 1e12 if t_con > 0 else float("nan")
     traffic = None
     tp = os.path.join(ROOT, "profiles", "pmc_traffic_contract_knm.json")
@@ -209,7 +209,8 @@ def main():
                        "parallelism": f"rows{world}" if world > 1 else "single"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
-                         "traffic": traffic, "kernel": con_key + " (k_contract<8>)",
+                         "traffic": traffic if args.mode == "vi" else None,
+                         "kernel": con_key + " (k_contract<8>)",
                          "flops_per_launch": flops},
             "phases_ms": {k: round(v, 4) for k, v in phase_avg.items()},
             "objective": obj,

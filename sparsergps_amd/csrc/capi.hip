@@ -122,6 +122,11 @@ struct sgp_ctx {
   double *red1 = nullptr, *red2 = nullptr;
   double *slab_syrk = nullptr, *slab_con = nullptr, *slab_small = nullptr, *sc = nullptr;
   double* tslab = nullptr;                // builder t = K^T r partials (VI), n_pad/64 x mp
+  // stored products of the FITC / Laplace row-quadratic passes (n_pad x mp each, allocated on
+  // first use; d <= 8): tq = K K22^-1, tp = K Bm^-1 (FITC) or K C (Laplace).  The gradient
+  // contraction passes read them instead of recomputing the same 2 n m^2 GEMMs.
+  double *tq = nullptr, *tp = nullptr;
+  int tstore_state = 0;                   // 0 untried, 1 allocated, -1 unavailable
   int64_t slab_syrk_cap = 0, slab_con_cap = 0, slab_small_cap = 0;
   // state carried between phases
   KernParams kp;
@@ -267,6 +272,26 @@ int dalloc(T** p, int64_t count) {
   return SGP_OK;
 }
 
+// Stored-product buffers for the FITC / Laplace passes; false (GEMM path) when d > 8 or HBM is
+// short -- the evaluation is the same either way.
+bool tstore_ready(sgp_ctx* c) {
+  if (c->kp.d > 8) return false;
+  if (c->tstore_state == 0) {
+    const int64_t cnt = c->n_pad * c->mp_max;
+    if (hipMalloc(reinterpret_cast<void**>(&c->tq), sizeof(double) * cnt) == hipSuccess &&
+        hipMalloc(reinterpret_cast<void**>(&c->tp), sizeof(double) * cnt) == hipSuccess) {
+      c->tstore_state = 1;
+    } else {
+      (void)hipGetLastError();
+      if (c->tq) (void)hipFree(c->tq);
+      if (c->tp) (void)hipFree(c->tp);
+      c->tq = c->tp = nullptr;
+      c->tstore_state = -1;
+    }
+  }
+  return c->tstore_state == 1;
+}
+
 void ctx_free(sgp_ctx* c) {
   void* ptrs[] = {c->X,      c->r,     c->K,      c->alpha,   c->zinv,  c->U,    c->K22,
                   c->K22inv, c->Bm,    c->Binv,   c->Pm,      c->Xt,    c->T1,   c->M3,
@@ -274,7 +299,7 @@ void ctx_free(sgp_ctx* c) {
                   c->red2,   c->slab_syrk, c->slab_con, c->slab_small, c->slab_aux, c->sc,
                   c->Xt22,   c->T22,    c->dinv22, c->omega, c->pvec, c->rowq, c->red2f,
                   c->y,      c->mu,     c->lv,     c->lm,    c->lslab, c->lred[0], c->lred[1],
-                  c->Cprev,  c->knot_slab, c->knot_part, c->knot_kmm, c->tslab};
+                  c->Cprev,  c->knot_slab, c->knot_part, c->knot_kmm, c->tslab, c->tq, c->tp};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->khash) hipFree(c->khash);
@@ -1160,7 +1185,8 @@ int sgp_fitc_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U
   {
     Scope t(c, "rowquad_q");
     HIPCHK(launch_rowquad_knm(kp, c->K, c->K22inv, c->n, c->n_pad, m, mp, c->r, 0.0, nullptr,
-                              nullptr, nullptr, c->rowq, c->pvec, c->stream));
+                              nullptr, nullptr, c->rowq, c->pvec, c->stream,
+                              tstore_ready(c) ? c->tq : nullptr));
     int nb = 0;
     HIPCHK(launch_fitc_z(c->pvec, c->n, c->n_pad, kp.sig2 + kp.tau2 + delta, c->zinv,
                          c->slab_small, &nb, c->stream));
@@ -1206,7 +1232,8 @@ int sgp_fitc_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned f
   {
     Scope tm(c, "rowquad_p");
     HIPCHK(launch_rowquad_knm(kp, c->K, c->Binv, c->n, c->n_pad, c->m, mp, c->r, 0.0, c->zinv,
-                              c->uvec, c->alpha, c->rowq, c->pvec, c->stream));
+                              c->uvec, c->alpha, c->rowq, c->pvec, c->stream,
+                              tstore_ready(c) ? c->tp : nullptr));
     int nb = 0;
     HIPCHK(launch_fitc_omega(c->alpha, c->zinv, c->pvec, c->n, c->n_pad, c->omega,
                              c->slab_small, &nb, c->stream));
@@ -1230,6 +1257,10 @@ int sgp_fitc_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned f
     a1.uvec = c->uvec;
     a1.rs_vec = c->zinv;
     a1.rs = -1.0;
+    if (tstore_ready(c)) {   // K Bm^-1 and alpha were produced by rowquad_p
+      a1.tin = c->tp;
+      a1.alpha_in = c->alpha;
+    }
     st = contract_pass(c, c->Binv, a1, red2 + off, kout, false);
     if (st) return st;
   }
@@ -1239,6 +1270,7 @@ int sgp_fitc_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned f
     ConArgs a2;
     a2.rs_vec = c->omega;
     a2.rs = -1.0;
+    if (tstore_ready(c)) a2.tin = c->tq;   // K K22^-1 from phase 1's rowquad_q
     st = contract_pass(c, c->K22inv, a2, red2 + off + nrec, kout, true);
     if (st) return st;
   }
@@ -1443,7 +1475,8 @@ int sgp_lap_begin(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   {
     Scope t(c, "rowquad_q");
     HIPCHK(launch_rowquad_knm(kp, c->K, c->K22inv, c->n, c->n_pad, m, mp, c->r, 0.0, nullptr,
-                              nullptr, nullptr, c->rowq, lvec(c, LV_P), c->stream));
+                              nullptr, nullptr, c->rowq, lvec(c, LV_P), c->stream,
+                              tstore_ready(c) ? c->tq : nullptr));
     HIPCHK(launch_lap_z(lvec(c, LV_P), c->n, c->n_pad, kp.sig2 + kp.tau2 + delta, lvec(c, LV_Z),
                         lvec(c, LV_ZI), c->stream));
   }
@@ -1554,7 +1587,8 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
     HIPCHK(launch_gemv_rows(c->K, n_pad, mp, lmv(c, LM_X1), nullptr, lvec(c, LV_Y1), nullptr,
                             c->stream));
     HIPCHK(launch_rowquad_knm(kp, c->K, c->Binv, n, n_pad, c->m, mp, c->r, 0.0, nullptr, nullptr,
-                              nullptr, c->rowq, lvec(c, LV_P), c->stream));
+                              nullptr, c->rowq, lvec(c, LV_P), c->stream,
+                              tstore_ready(c) ? c->tp : nullptr));
     HIPCHK(launch_lap_grad_a(n, n_pad, lvec(c, LV_F), c->y, c->mu, lvec(c, LV_Z), lvec(c, LV_ZI),
                              c->lap_expo, lvec(c, LV_Y1), lvec(c, LV_P), lvec(c, LV_C2),
                              lvec(c, LV_G), lvec(c, LV_B), lvec(c, LV_DMT), lvec(c, LV_SV),
@@ -1616,12 +1650,14 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
     a1.vvec = lmv(c, LM_NGG);
     a1.rs_vec = lvec(c, LV_B);
     a1.rs = -1.0;
+    if (tstore_ready(c)) a1.tin = c->tp;   // K C from lap_grad_a's row-quadratic pass
     int st = contract_pass(c, c->Binv, a1, red_out + off, kout, false);
     if (st) return st;
     // G2 = -diag(2a) K K22^-1
     ConArgs a2;
     a2.rs_vec = lvec(c, LV_A);
     a2.rs = -2.0;
+    if (tstore_ready(c)) a2.tin = c->tq;   // K K22^-1 from lap_begin's rowquad_q
     st = contract_pass(c, c->K22inv, a2, red_out + off + nrec, kout, true);
     if (st) return st;
     *count = off + 2 * nrec + (c->knot_on ? mp * kp.d : 0);

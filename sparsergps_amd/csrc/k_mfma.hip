@@ -329,7 +329,7 @@ k_syrk_reduce_t(const double* __restrict__ slab_t, const double* __restrict__ sl
 // staged K values (iz_i = invz_vec ? invz_vec[i] : invz), optionally written to alpha_out.
 enum { EPI_GRAD = 0, EPI_ROWQUAD = 1 };
 
-template <int DT, int EPI, bool V2 = false, bool KNOT = false>
+template <int DT, int EPI, bool V2 = false, bool KNOT = false, bool FROM_T = false>
 __global__ void __launch_bounds__(256, 2)
 k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict__ M,
            const double* __restrict__ X, int64_t ldx, int64_t n, int64_t n_pad,
@@ -406,6 +406,18 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
 #ifdef SGP_CON_TRACE
   if (tid == 0) SGP_CON_TRACE(0);
 #endif
+  if constexpr (FROM_T) {
+    // the product tile T = K M was stored by an earlier row-quadratic pass over the same K and
+    // M (launch_rowquad_knm with tstore): read it instead of recomputing 2 n m^2 flops
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          acc[fm][fn][q] = ca.tin[(i0 + wr * 64 + fm * 16 + (lane >> 4) + 4 * q) * mp + j0 +
+                                  wc * 64 + fn * 16 + (lane & 15)];
+  } else {
   CON_GLOAD(0);
   CON_SSTORE(0);
   __syncthreads();
@@ -433,12 +445,10 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     if (step + 1 < nsteps) CON_SSTORE(cur ^ 1);
     __syncthreads();
   }
+  }   // !FROM_T
 #undef CON_GLOAD
 #undef CON_SSTORE
 #undef CON_KU
-  // the epilogue's MFMAs and VALU win arbitration over the co-resident workgroup's k-loop (same
-  // total matrix-pipe work, but this tile finishes sooner and its successor starts sooner)
-  __builtin_amdgcn_s_setprio(1);
 
 #ifdef SGP_CON_TRACE
   if (tid == 0) SGP_CON_TRACE(1);
@@ -472,6 +482,16 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   const double* Kt = K + i0 * mp + j0;
 
   if constexpr (EPI == EPI_ROWQUAD) {
+    if (ca.tstore != nullptr) {   // keep T = K M for a later FROM_T gradient pass
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            ca.tstore[(i0 + wr * 64 + fm * 16 + (lane >> 4) + 4 * q) * mp + j0 + wc * 64 +
+                      fn * 16 + (lane & 15)] = acc[fm][fn][q];
+    }
     __syncthreads();
     double* s_q = s_cd;                       // [2][128] (reuses s_cd / s_xs space)
     // per lane: 16 rows (fm, q) x 4 cols (fn) -> row sums over this wave's 64 columns
@@ -1139,6 +1159,27 @@ hipError_t launch_contract_args(const KernParams& kp, const double* K, const dou
   const int nrec = kp.L + 5;
   *nrec_out = nrec;
   *nwg_out = nwg;
+  if (ca.tin != nullptr) {   // stored product: no k-loop (d <= 8, alpha from alpha_in)
+    if (kp.d > 8 || (ca.uvec != nullptr && ca.alpha_in == nullptr)) return hipErrorInvalidValue;
+    const bool v2 = ca.beta_in != nullptr, kn = ca.knot_slab != nullptr;
+    if (v2 && kn)
+      hipLaunchKernelGGL((k_contract<8, EPI_GRAD, true, true, true>), dim3((unsigned)nwg),
+                         dim3(256), 0, s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab,
+                         nrec, (double*)nullptr);
+    else if (v2)
+      hipLaunchKernelGGL((k_contract<8, EPI_GRAD, true, false, true>), dim3((unsigned)nwg),
+                         dim3(256), 0, s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab,
+                         nrec, (double*)nullptr);
+    else if (kn)
+      hipLaunchKernelGGL((k_contract<8, EPI_GRAD, false, true, true>), dim3((unsigned)nwg),
+                         dim3(256), 0, s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab,
+                         nrec, (double*)nullptr);
+    else
+      hipLaunchKernelGGL((k_contract<8, EPI_GRAD, false, false, true>), dim3((unsigned)nwg),
+                         dim3(256), 0, s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab,
+                         nrec, (double*)nullptr);
+    return hipGetLastError();
+  }
   if (ca.knot_slab != nullptr) {
     if (kp.d > 8) return hipErrorInvalidValue;   // knot epilogue is instantiated for d <= 8
     if (ca.beta_in != nullptr)
@@ -1187,7 +1228,7 @@ hipError_t launch_rowquad_knm(const KernParams& kp, const double* K, const doubl
                               int64_t n_pad, int64_t m, int64_t mp, const double* r,
                               double invz, const double* invz_vec, const double* uvec,
                               double* alpha_out, double* rowq_slab, double* out,
-                              hipStream_t s) {
+                              hipStream_t s, double* tstore) {
   const int64_t nwg = (n_pad / T128) * (mp / T128);
   ConArgs ca;
   ca.r = r;
@@ -1195,6 +1236,7 @@ hipError_t launch_rowquad_knm(const KernParams& kp, const double* K, const doubl
   ca.invz_vec = invz_vec;
   ca.uvec = uvec;
   ca.alpha_out = alpha_out;
+  ca.tstore = tstore;
   hipLaunchKernelGGL((k_contract<8, EPI_ROWQUAD>), dim3((unsigned)nwg), dim3(256), 0, s, kp, K, M,
                      (const double*)nullptr, (int64_t)0, n, n_pad, (const double*)nullptr,
                      (int64_t)0, m, mp, ca, (double*)nullptr, 0, rowq_slab);

@@ -125,6 +125,11 @@ struct ConArgs {
   // with t = scaled coordinate difference (ARD: (x_c - u_c)/l_c; sqexp/exp: x_c - u_c),
   // written to knot_slab[(ti * mp + j) * d + c]
   double* knot_slab = nullptr;
+  // stored products T = K M (row-major n_pad x mp): a row-quadratic pass writes T to tstore; a
+  // gradient pass with tin set reads T instead of running the MFMA k-loop (alpha must then come
+  // from alpha_in; d <= 8)
+  double* tstore = nullptr;
+  const double* tin = nullptr;
 };
 hipError_t launch_contract_args(const KernParams& kp, const double* K, const double* M,
                                 const double* X, int64_t ldx, int64_t n, int64_t n_pad,
@@ -139,12 +144,13 @@ hipError_t launch_contract_knm(const KernParams& kp, const double* K, const doub
                                const double* coinc_diag, int count_a2, double* slab,
                                int64_t* nrec_out, int64_t* nwg_out, hipStream_t s);
 // out_i = sum_j K_ij (K M)_ij = diag(K M K^T) (n_pad); optional fused alpha as above.
-// rowq_slab: (mp/128) x n_pad work.
+// rowq_slab: (mp/128) x n_pad work.  tstore (optional, n_pad x mp row-major): keeps T = K M for a
+// later gradient pass with ConArgs::tin = tstore.
 hipError_t launch_rowquad_knm(const KernParams& kp, const double* K, const double* M, int64_t n,
                               int64_t n_pad, int64_t m, int64_t mp, const double* r,
                               double invz, const double* invz_vec, const double* uvec,
                               double* alpha_out, double* rowq_slab, double* out,
-                              hipStream_t s);
+                              hipStream_t s, double* tstore = nullptr);
 // generic m x m GEMM on f64 MFMA: C = alpha*op(A)*op(B) + beta*C, sizes multiples of 64.
 hipError_t launch_gemm64(bool transA, bool transB, bool lower_only, int64_t M, int64_t N,
                          int64_t K, double alpha, const double* A, int64_t lda,

@@ -14,7 +14,7 @@ import argparse
 import csv
 import json
 
-KERNEL_MATCH = "k_contract<8, 0,"   # EPI_GRAD instantiation (the VI "contract_knm" launch)
+KERNEL_MATCH = "k_contract<8, 0, false, false, false>"   # VI "contract_knm" (EPI_GRAD, GEMM k-loop)
 
 
 def per_launch(path, counter, match):

@@ -10,7 +10,7 @@ import sys
 
 def main():
     path = sys.argv[1]
-    anchor = sys.argv[2] if len(sys.argv) > 2 else "k_contract<8, 0, false, false>"
+    anchor = sys.argv[2] if len(sys.argv) > 2 else "k_contract<8, 0, false, false, false>"
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]
     if len(idx) < 2:
