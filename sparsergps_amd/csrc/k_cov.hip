@@ -112,17 +112,22 @@ __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* 
                                                    const double* __restrict__ rvec,
                                                    double* __restrict__ tslab, int64_t rb0,
                                                    int64_t rb1) {
+  // block: 128 knot columns (two adjacent per lane, one 16-byte store per lane and row: 1 KiB
+  // per wave-instruction) x 4 row groups
   __shared__ __attribute__((aligned(16))) double xs[64 * DT];
   __shared__ double rsh[64];
-  __shared__ double tsh[4][64];
+  __shared__ double tsh[4][128];
   const int d = kp.d;
-  const int64_t j = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  const int64_t j = (int64_t)blockIdx.x * 128 + 2 * threadIdx.x;
   const int tid = threadIdx.y * 64 + threadIdx.x;
-  double uj[DT];
-  const bool jv = j < m;
+  double u0[DT], u1[DT];
+  const bool jv0 = j < m, jv1 = j + 1 < m;
 #pragma unroll
-  for (int c = 0; c < DT; ++c)
-    uj[c] = (jv && c < d) ? (ARD ? U[j + c * ldu] * kp.rl[c] : U[j + c * ldu]) : 0.0;
+  for (int c = 0; c < DT; ++c) {
+    const double sc = ARD ? kp.rl[c] : 1.0;
+    u0[c] = (jv0 && c < d) ? (ARD ? U[j + c * ldu] * sc : U[j + c * ldu]) : 0.0;
+    u1[c] = (jv1 && c < d) ? (ARD ? U[j + 1 + c * ldu] * sc : U[j + 1 + c * ldu]) : 0.0;
+  }
   const double sig2 = kp.sig2;
   const double scale = ARD ? -0.5 : kp.coef;
   for (int64_t rb = rb0 + blockIdx.y; rb < rb1; rb += gridDim.y) {
@@ -136,29 +141,40 @@ __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* 
       xs[e] = v;
     }
     if (rvec && tid < 64) rsh[tid] = (i0 + tid < n) ? rvec[i0 + tid] : 0.0;
-    double tpart = 0.0;
+    double tp0 = 0.0, tp1 = 0.0;
     __syncthreads();
     for (int r = threadIdx.y; r < 64; r += 4) {
       const int64_t i = i0 + r;
       const double2* xr = reinterpret_cast<const double2*>(&xs[r * DT]);
-      double s = 0.0;
+      double s0 = 0.0, s1 = 0.0;
 #pragma unroll
       for (int c2 = 0; c2 < DT / 2; ++c2) {
         const double2 xv = xr[c2];
-        const double t0 = xv.x - uj[2 * c2], t1 = xv.y - uj[2 * c2 + 1];
-        s = fma(t0, t0, s);
-        s = fma(t1, t1, s);
+        const double a0 = xv.x - u0[2 * c2], a1 = xv.y - u0[2 * c2 + 1];
+        const double b0 = xv.x - u1[2 * c2], b1 = xv.y - u1[2 * c2 + 1];
+        s0 = fma(a0, a0, s0);
+        s0 = fma(a1, a1, s0);
+        s1 = fma(b0, b0, s1);
+        s1 = fma(b1, b1, s1);
       }
-      const double v = (jv && i < n) ? sig2 * sgp_exp_nonpos(scale * s) : 0.0;
-      K[i * mp + j] = v;
-      if (rvec) tpart = fma(v, rsh[r], tpart);
+      const bool iv = i < n;
+      const double v0 = (jv0 && iv) ? sig2 * sgp_exp_nonpos(scale * s0) : 0.0;
+      const double v1 = (jv1 && iv) ? sig2 * sgp_exp_nonpos(scale * s1) : 0.0;
+      *reinterpret_cast<double2*>(&K[i * mp + j]) = make_double2(v0, v1);
+      if (rvec) {
+        tp0 = fma(v0, rsh[r], tp0);
+        tp1 = fma(v1, rsh[r], tp1);
+      }
     }
     if (rvec) {   // t_j partial of this block's 64 rows, fixed combination order
-      tsh[threadIdx.y][threadIdx.x] = tpart;
+      tsh[threadIdx.y][2 * threadIdx.x] = tp0;
+      tsh[threadIdx.y][2 * threadIdx.x + 1] = tp1;
       __syncthreads();
-      if (threadIdx.y == 0)
-        tslab[rb * mp + j] = ((tsh[0][threadIdx.x] + tsh[1][threadIdx.x]) + tsh[2][threadIdx.x]) +
-                             tsh[3][threadIdx.x];
+      if (threadIdx.y < 2) {
+        const int cc = threadIdx.y * 64 + threadIdx.x;
+        tslab[rb * mp + (int64_t)blockIdx.x * 128 + cc] =
+            ((tsh[0][cc] + tsh[1][cc]) + tsh[2][cc]) + tsh[3][cc];
+      }
     }
   }
 }
@@ -342,7 +358,7 @@ static hipError_t build_knm_range(const KernParams& kp, const double* X, int64_t
               ? prop.multiProcessorCount : 256;
   }
   if (rb1 <= rb0) return hipSuccess;
-  const int64_t ncb = mp / 64;
+  const int64_t ncb = mp / 128;   // 128 knot columns per block
   int64_t gy = ((int64_t)cus * wpc) / (ncb > 0 ? ncb : 1);
   gy = gy < 1 ? 1 : (gy > rb1 - rb0 ? rb1 - rb0 : gy);
   dim3 grid((unsigned)ncb, (unsigned)gy);
@@ -381,11 +397,12 @@ static hipError_t build_knm_impl(const KernParams& kp, const double* X, int64_t 
                          BUILD_WPC_FULL, s);
 }
 
-// Row blocks built at shared occupancy beside the K22 chain: ~40 us per 64-wide Gauss-Jordan
-// step (+ build and pivot) at ~2.3 GB/ms for the shared-occupancy builder.
+// Row blocks built at shared occupancy beside the K22 chain: ~50 us per 64-wide Gauss-Jordan
+// step beside the builder (+ build and first pivot) at ~2.8 GB/ms for the shared-occupancy
+// builder (measured, m = 1024).
 static int64_t chain_shared_rb(int64_t mp) {
-  const double chain_us = 40.0 * (double)(mp / 64) + 100.0;
-  return (int64_t)(chain_us * 2.3e6 / (64.0 * (double)mp * 8.0)) + 1;   // 2.3 GB/ms = 2.3e6 B/us
+  const double chain_us = 50.0 * (double)(mp / 64) + 150.0;
+  return (int64_t)(chain_us * 2.8e6 / (64.0 * (double)mp * 8.0)) + 1;   // 2.8 GB/ms = 2.8e6 B/us
 }
 
 hipError_t launch_build_knm(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
