@@ -865,7 +865,12 @@ int sgp_knot_gradient(sgp_ctx* c, const double* bounds, double* grad_knot) {
   return SGP_OK;
 }
 
-static int k22_stage(sgp_ctx* c, double diag_sub);
+static int k22_sync(sgp_ctx* c);
+static int k22_launch(sgp_ctx* c, double diag_sub);
+static int k22_stage(sgp_ctx* c, double diag_sub) {
+  int st = k22_sync(c);
+  return st ? st : k22_launch(c, diag_sub);
+}
 
 int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
                   int64_t ldu, double delta, double* red1) {
@@ -883,7 +888,7 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   if (st) return st;
   HIPCHK(hipMemsetAsync(c->status, 0, sizeof(int) * 4, c->stream));
   HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->stream));
-  st = k22_stage(c, kp.tau2);   // aux stream, overlaps the builder and the SYRK below
+  st = k22_sync(c);
   if (st) return st;
   const int64_t mpv = c->mp, mmv = mpv * mpv;
   {
@@ -893,6 +898,8 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
     HIPCHK(launch_build_knm_t(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, mpv, m, mpv, c->K, c->r,
                               c->tslab, c->stream));
   }
+  st = k22_launch(c, kp.tau2);   // aux stream, beside the builder's shared-occupancy head
+  if (st) return st;
   HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_vi_red1_count(m), c->stream));
   HIPCHK(launch_knot_reduce(c->tslab, c->n_pad / 64, mpv, 1, c->T1, c->mp_max * c->mp_max,
                             red1 + mmv, false,
@@ -959,10 +966,18 @@ static int k22_factor_launches(sgp_ctx* c, hipStream_t s) {
 // depends only on (U, theta), so it runs concurrently with phase 1's memory-bound builder; the
 // SYRK (whose grid fills exactly one residency round) waits for it.  A pristine copy of K22
 // goes to Bm for phase 2.
-static int k22_stage(sgp_ctx* c, double diag_sub) {
-  const int64_t mp = c->mp;
+// The aux stream's K22 work may start once the knots (and the status/scalar resets) are on
+// the main stream.  Split from the launches so that callers can enqueue the K12 builder on the
+// main stream first: the chain's ~20 launches cost the host ~0.2 ms, which otherwise delayed
+// the builder's start by as much.
+static int k22_sync(sgp_ctx* c) {
   HIPCHK(hipEventRecord(c->ev_knots, c->stream));
   HIPCHK(hipStreamWaitEvent(c->aux, c->ev_knots, 0));
+  return SGP_OK;
+}
+
+static int k22_launch(sgp_ctx* c, double diag_sub) {
+  const int64_t mp = c->mp;
   Scope t(c, "k22_aux", c->aux);
   HIPCHK(launch_build_kmm(c->kp, c->U, c->mp, c->m, mp, diag_sub, c->K22, c->aux));
   int st = run_graph(c, c->aux, k22_factor_launches, &c->g_k22, &c->g_k22_graph, &c->g_k22_mp);
@@ -1173,13 +1188,15 @@ int sgp_fitc_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U
   if (st) return st;
   HIPCHK(hipMemsetAsync(c->status, 0, sizeof(int) * 4, c->stream));
   HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->stream));
-  st = k22_stage(c, kp.tau2);   // K22 = Kuu + delta I, same as the VI path (laplace_gradient_ascent.R:1238-1257)
+  st = k22_sync(c);
   if (st) return st;
   {
     Scope t(c, "build_knm");
     HIPCHK(launch_build_knm(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp, m, mp, c->K,
                             c->stream, true));   // beside the K22 chain on aux
   }
+  st = k22_launch(c, kp.tau2);   // K22 = Kuu + delta I, same as the VI path (laplace_gradient_ascent.R:1238-1257)
+  if (st) return st;
   HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_fitc_red1_count(m), c->stream));
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
   {
@@ -1464,13 +1481,15 @@ int sgp_lap_begin(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   if (st) return st;
   HIPCHK(hipMemsetAsync(c->status, 0, sizeof(int) * 4, c->stream));
   HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->stream));
-  st = k22_stage(c, 0.0);   // K22 = Kuu + (tau^2 + delta) I (newtrap_sparseGP.R:51-59)
+  st = k22_sync(c);
   if (st) return st;
   {
     Scope t(c, "build_knm");
     HIPCHK(launch_build_knm(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp, m, mp, c->K,
                             c->stream, true));   // beside the K22 chain on aux
   }
+  st = k22_launch(c, 0.0);   // K22 = Kuu + (tau^2 + delta) I (newtrap_sparseGP.R:51-59)
+  if (st) return st;
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
   {
     Scope t(c, "rowquad_q");

@@ -397,11 +397,11 @@ static hipError_t build_knm_impl(const KernParams& kp, const double* X, int64_t 
                          BUILD_WPC_FULL, s);
 }
 
-// Row blocks built at shared occupancy beside the K22 chain: ~50 us per 64-wide Gauss-Jordan
+// Row blocks built at shared occupancy beside the K22 chain: ~60 us per 64-wide Gauss-Jordan
 // step beside the builder (+ build and first pivot) at ~2.8 GB/ms for the shared-occupancy
 // builder (measured, m = 1024).
 static int64_t chain_shared_rb(int64_t mp) {
-  const double chain_us = 50.0 * (double)(mp / 64) + 150.0;
+  const double chain_us = 60.0 * (double)(mp / 64) + 250.0;
   return (int64_t)(chain_us * 2.8e6 / (64.0 * (double)mp * 8.0)) + 1;   // 2.8 GB/ms = 2.8e6 B/us
 }
 
