@@ -181,6 +181,167 @@ k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __
   if (diag && ta == 0 && tid == 255) slab_rr[split] = rr_acc;
 }
 
+// ============================================================================ SYRK, 64-blocks
+// S = K^T diag(w) K without the diagonal tiles' redundant upper halves.  The lower triangle of
+// 64 x 64 blocks (nb64 = mp/64 block rows) is covered by workgroups of 4 blocks (one per wave):
+//   * every strictly-lower 128-tile (a > b): its 4 blocks (2a+r, 2b+c), operands = the 128-col
+//     K blocks a (image A) and b (image B) -- as k_syrk;
+//   * the diagonal 128-tiles' 3 lower blocks D0 = (2t,2t), L = (2t+1,2t), D1 = (2t+1,2t+1) are
+//     packed: group g (g < G = ceil(3 nb / 4)) takes tile g's three blocks from image A = K block
+//     g, plus one block of tile G + k/3 (k = g; block kind k % 3) from image B = that K block,
+//     so G groups cover all 3 nb diagonal blocks.
+// At m = 1024 that is 28 + 6 = 34 workgroups per row chunk instead of 36 (5.6% fewer flops).
+// Weights scale the A-side fragment in registers (a wave may take both operands from one
+// image).  The per-(split, block) slabs are reduced in fixed order by k_syrk_reduce_blk.
+__device__ __forceinline__ void syrk_group(int64_t gi, int nb, int wv, int& ta, int& tb, int& rs,
+                                           int& cs, int& rp, int& cp) {
+  const int64_t noff = (int64_t)nb * (nb - 1) / 2;
+  if (gi < noff) {
+    int a = (int)((sqrtf(8.0f * (float)gi + 1.0f) + 1.0f) * 0.5f);
+    while ((int64_t)a * (a - 1) / 2 > gi) --a;
+    while ((int64_t)(a + 1) * a / 2 <= gi) ++a;
+    const int b = (int)(gi - (int64_t)a * (a - 1) / 2);
+    ta = a; tb = b;
+    const int wr = wv >> 1, wc = wv & 1;
+    rs = wr; cs = 2 + wc;
+    rp = 2 * a + wr; cp = 2 * b + wc;
+    return;
+  }
+  const int g = (int)(gi - noff), G = (3 * nb + 3) / 4;
+  const int te = G + g / 3, kind = g % 3;
+  ta = g;
+  tb = (te < nb) ? te : g;
+  if (wv == 0) { rs = 0; cs = 0; rp = 2 * g; cp = 2 * g; }
+  else if (wv == 1) { rs = 1; cs = 0; rp = 2 * g + 1; cp = 2 * g; }
+  else if (wv == 2) { rs = 1; cs = 1; rp = 2 * g + 1; cp = 2 * g + 1; }
+  else if (te < nb) {
+    if (kind == 0) { rs = 2; cs = 2; rp = 2 * te; cp = 2 * te; }
+    else if (kind == 1) { rs = 3; cs = 2; rp = 2 * te + 1; cp = 2 * te; }
+    else { rs = 3; cs = 3; rp = 2 * te + 1; cp = 2 * te + 1; }
+  } else {
+    rs = cs = rp = cp = -1;   // idle wave (nb too small to pack)
+  }
+}
+
+__global__ void __launch_bounds__(256, 2)
+k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __restrict__ w,
+           int64_t chunk, int ngroups, int nb, double* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
+  __shared__ __attribute__((aligned(16))) double Kb[2][BK * SB];
+  __shared__ double ws[2][BK];
+
+  const int64_t nwg = (int64_t)gridDim.x;
+  const int64_t wgid = xcd_remap(blockIdx.x, nwg);
+  const int split = (int)(wgid / ngroups);
+  const int64_t gi = wgid % ngroups;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  int ta, tb, rs, cs, rp, cp;
+  syrk_group(gi, nb, wv, ta, tb, rs, cs, rp, cp);
+  const bool active = rs >= 0;
+  const int64_t rbeg = (int64_t)split * chunk;
+  int64_t rend = rbeg + chunk;
+  if (rend > n_pad) rend = n_pad;
+  const int nsteps = (int)((rend - rbeg) / BK);
+
+  d4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+
+  const int lrow = tid >> 4, lc = tid & 15;
+  const double2* gA = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + ta * (int64_t)T128) + lc;
+  const double2* gB = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + tb * (int64_t)T128) + lc;
+  const int64_t gstep = BK * mp / 2;
+  double2 va0, va1, va2, va3, vb0, vb1, vb2, vb3;
+  double vw = 1.0;
+  // operand images and column offsets of this wave's row / column panels
+  const int ra = (rs >> 1) & 1, ro = (rs & 1) * 64;
+  const int ca_ = (cs >> 1) & 1, co = (cs & 1) * 64;
+
+#define SYRKB_GLOAD(step)                                                       \
+  {                                                                             \
+    const int64_t o_ = (int64_t)(step) * gstep;                                 \
+    va0 = gA[o_]; va1 = gA[o_ + 16]; va2 = gA[o_ + 32]; va3 = gA[o_ + 48];      \
+    vb0 = gB[o_]; vb1 = gB[o_ + 16]; vb2 = gB[o_ + 32]; vb3 = gB[o_ + 48];      \
+    if (w != nullptr && tid < BK) vw = w[rbeg + (int64_t)(step) * BK + tid];    \
+  }
+#define SYRKB_SSTORE(buf)                                                       \
+  {                                                                             \
+    double2* pa_ = reinterpret_cast<double2*>(&Ka[buf][lrow * SB]) + lc;        \
+    double2* pb_ = reinterpret_cast<double2*>(&Kb[buf][lrow * SB]) + lc;        \
+    pa_[0] = va0; pa_[16] = va1; pa_[32] = va2; pa_[48] = va3;                  \
+    pb_[0] = vb0; pb_[16] = vb1; pb_[32] = vb2; pb_[48] = vb3;                  \
+    if (tid < BK) ws[buf][tid] = vw;                                            \
+  }
+
+  if (nsteps > 0) {
+    SYRKB_GLOAD(0);
+    SYRKB_SSTORE(0);
+  }
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
+    if (step + 1 < nsteps) SYRKB_GLOAD(step + 1);
+    const double* As = (ra ? Kb[cur] : Ka[cur]) + ro;
+    const double* Bs = (ca_ ? Kb[cur] : Ka[cur]) + co;
+    if (active) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int krow = kk * 4 + (lane >> 4);
+        const double wk = (w != nullptr) ? ws[cur][krow] : 1.0;
+        double af[4], bf[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          af[f] = As[krow * SB + f * 16 + (lane & 15)] * wk;
+          bf[f] = Bs[krow * SB + f * 16 + (lane & 15)];
+        }
+#pragma unroll
+        for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < 4; ++fn)
+            acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
+      }
+    }
+    if (step + 1 < nsteps) SYRKB_SSTORE(cur ^ 1);
+    __syncthreads();
+  }
+#undef SYRKB_GLOAD
+#undef SYRKB_SSTORE
+
+  if (!active) return;
+  const int64_t bid = (int64_t)rp * (rp + 1) / 2 + cp;
+  const int64_t nblk = (int64_t)(2 * nb) * (2 * nb + 1) / 2;
+  double* out = slab + ((int64_t)split * nblk + bid) * 4096;
+#pragma unroll
+  for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = fm * 16 + (lane >> 4) + 4 * q;
+        const int col = fn * 16 + (lane & 15);
+        out[row * 64 + col] = acc[fm][fn][q];
+      }
+}
+
+// S (mp x mp full symmetric) from the per-split lower 64-blocks, fixed split order
+__global__ void __launch_bounds__(256)
+k_syrk_reduce_blk(const double* __restrict__ slab, int splits, int64_t nblk, int64_t mp,
+                  double* __restrict__ red) {
+  const int64_t bid = blockIdx.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;   // element of the 64 x 64 block
+  int rp = (int)((sqrtf(8.0f * (float)bid + 1.0f) - 1.0f) * 0.5f);
+  while ((int64_t)(rp + 1) * (rp + 2) / 2 <= bid) ++rp;
+  while ((int64_t)rp * (rp + 1) / 2 > bid) --rp;
+  const int cp = (int)(bid - (int64_t)rp * (rp + 1) / 2);
+  double v = 0.0;
+  for (int sp = 0; sp < splits; ++sp) v += slab[((int64_t)sp * nblk + bid) * 4096 + e];
+  const int64_t a = (int64_t)rp * 64 + e / 64, b = (int64_t)cp * 64 + e % 64;
+  red[a * mp + b] = v;
+  red[b * mp + a] = v;
+}
+
 // ============================================================================ TN GEMM
 // C = A^T B over n rows (A: n_pad x ma, B: n_pad x mb, both row-major; ma, mb multiples of
 // 128): split-K over row chunks like k_syrk, one 128x128 tile per workgroup, deterministic
@@ -1026,16 +1187,59 @@ SyrkPlan syrk_plan(int64_t n_pad, int64_t mp) {
   return p;
 }
 
+// k_syrk_blk: the same split rule over its packed groups (T = workgroups per row chunk)
+SyrkPlan syrk_plan_blk(int64_t n_pad, int64_t mp) {
+  SyrkPlan p = syrk_plan(n_pad, mp);   // nb, and a starting point
+  const int nb = p.nb;
+  const int groups = nb * (nb - 1) / 2 + (3 * nb + 3) / 4;
+  constexpr int64_t kSlots = 512;
+  const int64_t max_splits = n_pad / BK > 0 ? n_pad / BK : 1;
+  int64_t best = 1;
+  double best_fill = 0.0;
+  for (int64_t rounds = 1; rounds <= 4; ++rounds) {
+    int64_t sp = rounds * kSlots / groups;
+    if (sp < 1) sp = 1;
+    if (sp > max_splits) sp = max_splits;
+    const double fill = (double)(sp * groups) /
+                        (double)(((sp * groups + kSlots - 1) / kSlots) * kSlots);
+    if (fill > best_fill + 1e-9) { best_fill = fill; best = sp; }
+    if (best_fill >= 0.95) break;
+  }
+  int64_t chunk = (n_pad + best - 1) / best;
+  chunk = (chunk + BK - 1) / BK * BK;
+  p.T = groups;
+  p.chunk = chunk;
+  p.splits = (int)((n_pad + chunk - 1) / chunk);
+  return p;
+}
+
 }  // namespace
 
 int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp) {
   SyrkPlan p = syrk_plan(n_pad, mp);
-  return (int64_t)p.splits * p.T * T128 * T128 + (int64_t)p.splits * p.nb * T128 + p.splits;
+  SyrkPlan q = syrk_plan_blk(n_pad, mp);
+  const int64_t nblk = (int64_t)(2 * q.nb) * (2 * q.nb + 1) / 2;
+  const int64_t old_ = (int64_t)p.splits * p.T * T128 * T128 + (int64_t)p.splits * p.nb * T128 +
+                       p.splits;
+  const int64_t blk_ = (int64_t)q.splits * nblk * 4096;
+  return old_ > blk_ ? old_ : blk_;
 }
 
 hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const double* r,
                            const double* w, double* slab, int64_t slab_cap, double* red,
                            hipStream_t s, int part, const double* tv, int with_t) {
+  if (!with_t) {   // S only: the packed 64-block kernel (no redundant diagonal-tile halves)
+    SyrkPlan q = syrk_plan_blk(n_pad, mp);
+    const int64_t nblk = (int64_t)(2 * q.nb) * (2 * q.nb + 1) / 2;
+    if ((int64_t)q.splits * nblk * 4096 > slab_cap) return hipErrorInvalidValue;
+    if (part & 1)
+      hipLaunchKernelGGL(k_syrk_blk, dim3((unsigned)(q.splits * q.T)), dim3(256), 0, s, K, n_pad,
+                         mp, w, q.chunk, q.T, q.nb, slab);
+    if (part & 2)
+      hipLaunchKernelGGL(k_syrk_reduce_blk, dim3(4096 / 256, (unsigned)nblk), dim3(256), 0, s,
+                         slab, q.splits, nblk, mp, red);
+    return hipGetLastError();
+  }
   SyrkPlan p = syrk_plan(n_pad, mp);
   double* slab_s = slab;
   double* slab_t = slab_s + (int64_t)p.splits * p.T * T128 * T128;
