@@ -1,8 +1,9 @@
 // fp64 matrix-core (v_mfma_f64_16x16x4_f64) kernels for gfx950.
 //
-//  k_syrk      S = K^T diag(w) K over n rows (split-K over row chunks, deterministic slabs),
-//              plus t = K^T diag(w) r and rr = r^T diag(w) r.  Replaces the reference's
-//              `t(Sigma12) %*% ((1/Z) * Sigma12)` (R/vi_functions.R:96, 231, 239).
+//  k_syrk_blk  S = K^T diag(w) K over n rows (split-K over row chunks, deterministic slabs, the
+//              lower 64-blocks packed 4 per workgroup), plus t = K^T diag(w) r and
+//              rr = r^T diag(w) r.  Replaces the reference's `t(Sigma12) %*% ((1/Z) * Sigma12)`
+//              (R/vi_functions.R:96, 231, 239).
 //  k_contract  G = alpha u^T + K P fused with the d K12/d log(theta) contraction: the GEMM
 //              result never leaves registers; the epilogue recomputes K_ij and the pairwise
 //              distances and reduces sum_ij G_ij dK_ij/dtheta_p for every p at once.  Replaces
@@ -50,142 +51,11 @@ __device__ __forceinline__ void store8(double* s, const double2 (&v)[4]) {
   for (int q = 0; q < 4; ++q) p[q] = v[q];
 }
 
-// ============================================================================ SYRK
-// grid = splits * T (T = lower 128-tiles); block 256 = 4 waves as 2x2 of 64x64.
-__global__ void __launch_bounds__(256, 2)
-k_syrk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __restrict__ r,
-       const double* __restrict__ w, const double* __restrict__ tv, int with_t, int64_t chunk,
-       int T, int nb,
-       double* __restrict__ slab_s, double* __restrict__ slab_t, double* __restrict__ slab_rr) {
-  __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
-  __shared__ __attribute__((aligned(16))) double Kb[2][BK * SB];
-  __shared__ double rw[2][BK];
-  __shared__ double rv[2][BK];
-  __shared__ double rr_acc;
-
-  const int64_t nwg = (int64_t)gridDim.x;
-  const int64_t wgid = xcd_remap(blockIdx.x, nwg);
-  const int split = (int)(wgid / T);
-  const int tile = (int)(wgid % T);
-  int ta = (int)((sqrtf(8.0f * tile + 1.0f) - 1.0f) * 0.5f);
-  while ((ta + 1) * (ta + 2) / 2 <= tile) ++ta;
-  while (ta * (ta + 1) / 2 > tile) --ta;
-  const int tb = tile - ta * (ta + 1) / 2;
-  const bool diag = (ta == tb);
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wr = wv >> 1, wc = wv & 1;
-  const int64_t rbeg = (int64_t)split * chunk;
-  int64_t rend = rbeg + chunk;
-  if (rend > n_pad) rend = n_pad;
-  const int nsteps = (int)((rend - rbeg) / BK);
-
-  d4 acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-
-  // loader mapping: 16 rows x 128 cols, 4 double2 per thread at double2 columns lc + 16 q, so
-  // 8 consecutive lanes store 128 contiguous bytes (conflict-free ds_write_b128; 8 doubles per
-  // thread contiguous gave 4-way bank conflicts on every store)
-  const int lrow = tid >> 4, lc = tid & 15;
-  const double2* gA = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + ta * (int64_t)T128) + lc;
-  const double2* gB = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + tb * (int64_t)T128) + lc;
-  const int64_t gstep = BK * mp / 2;   // double2 stride of one k-step
-  double2 va0, va1, va2, va3, vb0, vb1, vb2, vb3;
-  double vr = 0.0, wi = 1.0, vrr = 0.0;
-  double tacc = 0.0;  // t partial for column (tid) when diag
-  if (tid == 0) rr_acc = 0.0;
-
-#define SYRK_GLOAD(step)                                                        \
-  {                                                                             \
-    const int64_t o_ = (int64_t)(step) * gstep;                                 \
-    va0 = gA[o_]; va1 = gA[o_ + 16]; va2 = gA[o_ + 32]; va3 = gA[o_ + 48];      \
-    vb0 = gB[o_]; vb1 = gB[o_ + 16]; vb2 = gB[o_ + 32]; vb3 = gB[o_ + 48];      \
-    if (w != nullptr) wi = w[rbeg + (int64_t)(step) * BK + lrow];               \
-    if (tid < BK) {   /* raw loads only: arithmetic here would wait on every load above */ \
-      const int64_t rr_ = rbeg + (int64_t)(step) * BK + tid;                    \
-      vrr = r[rr_];                                                             \
-      vr = (tv != nullptr) ? tv[rr_] : ((w != nullptr) ? w[rr_] : 1.0);         \
-    }                                                                           \
-  }
-#define SYRK_SSTORE(buf)                                                        \
-  {                                                                             \
-    double2* pa_ = reinterpret_cast<double2*>(&Ka[buf][lrow * SB]) + lc;        \
-    double2* pb_ = reinterpret_cast<double2*>(&Kb[buf][lrow * SB]) + lc;        \
-    pa_[0] = make_double2(va0.x * wi, va0.y * wi);                              \
-    pa_[16] = make_double2(va1.x * wi, va1.y * wi);                             \
-    pa_[32] = make_double2(va2.x * wi, va2.y * wi);                             \
-    pa_[48] = make_double2(va3.x * wi, va3.y * wi);                             \
-    pb_[0] = vb0; pb_[16] = vb1; pb_[32] = vb2; pb_[48] = vb3;                  \
-    if (tid < BK) {                                                             \
-      rw[buf][tid] = (tv != nullptr) ? vr : vr * vrr;   /* (w r)_i or tv_i */      \
-      rv[buf][tid] = vrr;                                                       \
-    }                                                                           \
-  }
-
-  if (nsteps > 0) {
-    SYRK_GLOAD(0);
-    SYRK_SSTORE(0);
-  }
-  __syncthreads();
-  for (int step = 0; step < nsteps; ++step) {
-    const int cur = step & 1;
-    if (step + 1 < nsteps) SYRK_GLOAD(step + 1);
-    const double* As = Ka[cur];
-    const double* Bs = Kb[cur];
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int krow = kk * 4 + (lane >> 4);
-      double af[4], bf[4];
-#pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        af[f] = As[krow * SB + wr * 64 + f * 16 + (lane & 15)];
-        bf[f] = Bs[krow * SB + wc * 64 + f * 16 + (lane & 15)];
-      }
-#pragma unroll
-      for (int fm = 0; fm < 4; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < 4; ++fn)
-          acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
-    }
-    if (with_t && diag && tid < T128) {
-      // t_a += sum_i (w_i r_i) K_ia over this step's rows (unscaled operand image)
-#pragma unroll
-      for (int q = 0; q < BK; ++q) tacc = fma(rw[cur][q], Bs[q * SB + tid], tacc);
-    }
-    if (with_t && diag && ta == 0 && tid == 255) {
-      double s = 0.0;
-      for (int q = 0; q < BK; ++q) s += rw[cur][q] * rv[cur][q];
-      rr_acc += s;
-    }
-    if (step + 1 < nsteps) SYRK_SSTORE(cur ^ 1);
-    __syncthreads();
-  }
-#undef SYRK_GLOAD
-#undef SYRK_SSTORE
-
-  double* out = slab_s + ((int64_t)split * T + tile) * (T128 * T128);
-#pragma unroll
-  for (int fm = 0; fm < 4; ++fm)
-#pragma unroll
-    for (int fn = 0; fn < 4; ++fn)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
-        const int col = wc * 64 + fn * 16 + (lane & 15);
-        out[row * T128 + col] = acc[fm][fn][q];
-      }
-  if (diag && tid < T128) slab_t[((int64_t)split * nb + ta) * T128 + tid] = tacc;
-  if (diag && ta == 0 && tid == 255) slab_rr[split] = rr_acc;
-}
-
 // ============================================================================ SYRK, 64-blocks
 // S = K^T diag(w) K without the diagonal tiles' redundant upper halves.  The lower triangle of
 // 64 x 64 blocks (nb64 = mp/64 block rows) is covered by workgroups of 4 blocks (one per wave):
 //   * every strictly-lower 128-tile (a > b): its 4 blocks (2a+r, 2b+c), operands = the 128-col
-//     K blocks a (image A) and b (image B) -- as k_syrk;
+//     K blocks a (image A) and b (image B);
 //   * the diagonal 128-tiles' 3 lower blocks D0 = (2t,2t), L = (2t+1,2t), D1 = (2t+1,2t+1) are
 //     packed: group g (g < G = ceil(3 nb / 4)) takes tile g's three blocks from image A = K block
 //     g, plus one block of tile G + k/3 (k = g; block kind k % 3) from image B = that K block,
@@ -223,12 +93,18 @@ __device__ __forceinline__ void syrk_group(int64_t gi, int nb, int wv, int& ta, 
   }
 }
 
+template <bool WITH_T>
 __global__ void __launch_bounds__(256, 2)
 k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __restrict__ w,
-           int64_t chunk, int ngroups, int nb, double* __restrict__ slab) {
+           const double* __restrict__ r, const double* __restrict__ tv,
+           int64_t chunk, int ngroups, int nb, double* __restrict__ slab,
+           double* __restrict__ slab_t, double* __restrict__ slab_rr) {
   __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
   __shared__ __attribute__((aligned(16))) double Kb[2][BK * SB];
   __shared__ double ws[2][BK];
+  __shared__ double rw[2][BK];   // with_t: (w r)_i or tv_i of the step's rows
+  __shared__ double rv[2][BK];   // with_t: r_i
+  __shared__ double rr_acc;
 
   const int64_t nwg = (int64_t)gridDim.x;
   const int64_t wgid = xcd_remap(blockIdx.x, nwg);
@@ -238,6 +114,18 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
   int ta, tb, rs, cs, rp, cp;
   syrk_group(gi, nb, wv, ta, tb, rs, cs, rp, cp);
   const bool active = rs >= 0;
+  // t = K^T (w r) (or K^T tv) for the K column blocks this group holds whole and is the owner
+  // of: image A's block g for diagonal group g, and image B's block te for the first of the
+  // three groups that take an extra block of tile te.  rr from diagonal group 0.
+  const int64_t noff = (int64_t)nb * (nb - 1) / 2;
+  const int dg = (gi >= noff) ? (int)(gi - noff) : -1;
+  const int dte = (dg >= 0) ? (3 * nb + 3) / 4 + dg / 3 : nb;
+  constexpr bool with_t = WITH_T;
+  const bool t_a = with_t && dg >= 0 && tid < T128;
+  const bool t_b = with_t && dg >= 0 && tid >= T128 && dte < nb && (dg % 3) == 0;
+  const bool t_rr = with_t && dg == 0 && tid == 255;
+  double tacc = 0.0, vrr = 0.0, vr = 0.0;
+  if (tid == 0) rr_acc = 0.0;
   const int64_t rbeg = (int64_t)split * chunk;
   int64_t rend = rbeg + chunk;
   if (rend > n_pad) rend = n_pad;
@@ -264,7 +152,14 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
     const int64_t o_ = (int64_t)(step) * gstep;                                 \
     va0 = gA[o_]; va1 = gA[o_ + 16]; va2 = gA[o_ + 32]; va3 = gA[o_ + 48];      \
     vb0 = gB[o_]; vb1 = gB[o_ + 16]; vb2 = gB[o_ + 32]; vb3 = gB[o_ + 48];      \
-    if (w != nullptr && tid < BK) vw = w[rbeg + (int64_t)(step) * BK + tid];    \
+    if (tid < BK) {                                                             \
+      const int64_t rr_ = rbeg + (int64_t)(step) * BK + tid;                    \
+      if (w != nullptr) vw = w[rr_];                                            \
+      if (with_t) {                                                             \
+        vrr = r[rr_];                                                           \
+        vr = (tv != nullptr) ? tv[rr_] : ((w != nullptr) ? w[rr_] : 1.0);       \
+      }                                                                         \
+    }                                                                           \
   }
 #define SYRKB_SSTORE(buf)                                                       \
   {                                                                             \
@@ -272,7 +167,13 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
     double2* pb_ = reinterpret_cast<double2*>(&Kb[buf][lrow * SB]) + lc;        \
     pa_[0] = va0; pa_[16] = va1; pa_[32] = va2; pa_[48] = va3;                  \
     pb_[0] = vb0; pb_[16] = vb1; pb_[32] = vb2; pb_[48] = vb3;                  \
-    if (tid < BK) ws[buf][tid] = vw;                                            \
+    if (tid < BK) {                                                             \
+      ws[buf][tid] = vw;                                                        \
+      if (with_t) {                                                             \
+        rw[buf][tid] = (tv != nullptr) ? vr : vr * vrr;   /* (w r)_i or tv_i */  \
+        rv[buf][tid] = vrr;                                                     \
+      }                                                                         \
+    }                                                                           \
   }
 
   if (nsteps > 0) {
@@ -303,12 +204,27 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
             acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
       }
     }
+    if (t_a) {
+#pragma unroll
+      for (int q = 0; q < BK; ++q) tacc = fma(rw[cur][q], Ka[cur][q * SB + tid], tacc);
+    } else if (t_b) {
+#pragma unroll
+      for (int q = 0; q < BK; ++q) tacc = fma(rw[cur][q], Kb[cur][q * SB + tid - T128], tacc);
+    }
+    if (t_rr) {
+      double sacc = 0.0;
+      for (int q = 0; q < BK; ++q) sacc += rw[cur][q] * rv[cur][q];
+      rr_acc += sacc;
+    }
     if (step + 1 < nsteps) SYRKB_SSTORE(cur ^ 1);
     __syncthreads();
   }
 #undef SYRKB_GLOAD
 #undef SYRKB_SSTORE
 
+  if (t_a) slab_t[((int64_t)split * nb + dg) * T128 + tid] = tacc;
+  if (t_b) slab_t[((int64_t)split * nb + dte) * T128 + tid - T128] = tacc;
+  if (t_rr) slab_rr[split] = rr_acc;
   if (!active) return;
   const int64_t bid = (int64_t)rp * (rp + 1) / 2 + cp;
   const int64_t nblk = (int64_t)(2 * nb) * (2 * nb + 1) / 2;
@@ -344,7 +260,7 @@ k_syrk_reduce_blk(const double* __restrict__ slab, int splits, int64_t nblk, int
 
 // ============================================================================ TN GEMM
 // C = A^T B over n rows (A: n_pad x ma, B: n_pad x mb, both row-major; ma, mb multiples of
-// 128): split-K over row chunks like k_syrk, one 128x128 tile per workgroup, deterministic
+// 128): split-K over row chunks like k_syrk_blk, one 128x128 tile per workgroup, deterministic
 // slabs [split][tile][128 x 128].  grid = splits * (ma/128) * (mb/128).
 __global__ void __launch_bounds__(256, 2)
 k_gemm_tn(const double* __restrict__ A, int64_t lda, const double* __restrict__ B, int64_t ldb,
@@ -368,7 +284,7 @@ k_gemm_tn(const double* __restrict__ A, int64_t lda, const double* __restrict__ 
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-  const int lrow = tid >> 4, lc = tid & 15;   // double2 columns lc + 16 q (as k_syrk)
+  const int lrow = tid >> 4, lc = tid & 15;   // double2 columns lc + 16 q (as k_syrk_blk)
   const double2* gA = reinterpret_cast<const double2*>(A + (rbeg + lrow) * lda + ta * (int64_t)T128) + lc;
   const double2* gB = reinterpret_cast<const double2*>(B + (rbeg + lrow) * ldb + tb * (int64_t)T128) + lc;
   const int64_t sa = BK * lda / 2, sb = BK * ldb / 2;
@@ -441,24 +357,6 @@ k_gemm_tn_reduce(const double* __restrict__ slab, int splits, int nta, int ntb,
   const int ta = tile / ntb, tb = tile % ntb;
   const int64_t a = (int64_t)ta * T128 + e / T128, b = (int64_t)tb * T128 + e % T128;
   C[a * (int64_t)ntb * T128 + b] = s;
-}
-
-// S (mp x mp full) from the per-split lower tiles; red = [S, t, rr]
-__global__ void __launch_bounds__(256)
-k_syrk_reduce(const double* __restrict__ slab_s, int splits, int T, int64_t mp,
-              double* __restrict__ red) {
-  const int tile = blockIdx.y;
-  const int e = blockIdx.x * 256 + threadIdx.x;  // element of the 128x128 tile
-  int ta = (int)((sqrtf(8.0f * tile + 1.0f) - 1.0f) * 0.5f);
-  while ((ta + 1) * (ta + 2) / 2 <= tile) ++ta;
-  while (ta * (ta + 1) / 2 > tile) --ta;
-  const int tb = tile - ta * (ta + 1) / 2;
-  double s = 0.0;
-  for (int sp = 0; sp < splits; ++sp) s += slab_s[((int64_t)sp * T + tile) * (T128 * T128) + e];
-  const int64_t a = (int64_t)ta * T128 + e / T128;
-  const int64_t b = (int64_t)tb * T128 + e % T128;
-  red[a * mp + b] = s;
-  red[b * mp + a] = s;
 }
 
 __global__ void __launch_bounds__(256)
@@ -1216,46 +1114,36 @@ SyrkPlan syrk_plan_blk(int64_t n_pad, int64_t mp) {
 }  // namespace
 
 int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp) {
-  SyrkPlan p = syrk_plan(n_pad, mp);
   SyrkPlan q = syrk_plan_blk(n_pad, mp);
   const int64_t nblk = (int64_t)(2 * q.nb) * (2 * q.nb + 1) / 2;
-  const int64_t old_ = (int64_t)p.splits * p.T * T128 * T128 + (int64_t)p.splits * p.nb * T128 +
-                       p.splits;
-  const int64_t blk_ = (int64_t)q.splits * nblk * 4096;
-  return old_ > blk_ ? old_ : blk_;
+  return (int64_t)q.splits * nblk * 4096 + (int64_t)q.splits * q.nb * T128 + q.splits;
 }
 
 hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const double* r,
                            const double* w, double* slab, int64_t slab_cap, double* red,
                            hipStream_t s, int part, const double* tv, int with_t) {
-  if (!with_t) {   // S only: the packed 64-block kernel (no redundant diagonal-tile halves)
+  {   // the packed 64-block kernel (no redundant diagonal-tile halves)
     SyrkPlan q = syrk_plan_blk(n_pad, mp);
     const int64_t nblk = (int64_t)(2 * q.nb) * (2 * q.nb + 1) / 2;
-    if ((int64_t)q.splits * nblk * 4096 > slab_cap) return hipErrorInvalidValue;
-    if (part & 1)
-      hipLaunchKernelGGL(k_syrk_blk, dim3((unsigned)(q.splits * q.T)), dim3(256), 0, s, K, n_pad,
-                         mp, w, q.chunk, q.T, q.nb, slab);
-    if (part & 2)
+    double* sl_s = slab;
+    double* sl_t = sl_s + (int64_t)q.splits * nblk * 4096;
+    double* sl_rr = sl_t + (int64_t)q.splits * q.nb * T128;
+    if (sl_rr + q.splits > slab + slab_cap) return hipErrorInvalidValue;
+    if ((part & 1) && with_t)
+      hipLaunchKernelGGL(k_syrk_blk<true>, dim3((unsigned)(q.splits * q.T)), dim3(256), 0, s, K,
+                         n_pad, mp, w, r, tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr);
+    else if (part & 1)
+      hipLaunchKernelGGL(k_syrk_blk<false>, dim3((unsigned)(q.splits * q.T)), dim3(256), 0, s, K,
+                         n_pad, mp, w, r, tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr);
+    if (part & 2) {
       hipLaunchKernelGGL(k_syrk_reduce_blk, dim3(4096 / 256, (unsigned)nblk), dim3(256), 0, s,
-                         slab, q.splits, nblk, mp, red);
+                         sl_s, q.splits, nblk, mp, red);
+      if (with_t)
+        hipLaunchKernelGGL(k_syrk_reduce_t, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s,
+                           sl_t, sl_rr, q.splits, q.nb, mp, red);
+    }
     return hipGetLastError();
   }
-  SyrkPlan p = syrk_plan(n_pad, mp);
-  double* slab_s = slab;
-  double* slab_t = slab_s + (int64_t)p.splits * p.T * T128 * T128;
-  double* slab_rr = slab_t + (int64_t)p.splits * p.nb * T128;
-  if (slab_rr + p.splits > slab + slab_cap) return hipErrorInvalidValue;
-  if (part & 1)
-    hipLaunchKernelGGL(k_syrk, dim3((unsigned)(p.splits * p.T)), dim3(256), 0, s, K, n_pad, mp,
-                       r, w, tv, with_t, p.chunk, p.T, p.nb, slab_s, slab_t, slab_rr);
-  if (part & 2) {
-    hipLaunchKernelGGL(k_syrk_reduce, dim3(T128 * T128 / 256, p.T), dim3(256), 0, s, slab_s,
-                       p.splits, p.T, mp, red);
-    if (with_t)
-      hipLaunchKernelGGL(k_syrk_reduce_t, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s,
-                         slab_t, slab_rr, p.splits, p.nb, mp, red);
-  }
-  return hipGetLastError();
 }
 
 int64_t gemm_tn_splits(int64_t n_pad, int ntile) {

@@ -8,7 +8,7 @@ import collections
 import csv
 import sys
 
-DEFAULT = ["k_contract<8, 0, false, false, false>", "k_syrk(", "k_build_knm<true, 8>"]
+DEFAULT = ["k_contract<8, 0, false, false, false>", "k_syrk_blk", "k_build_knm<true, 8>"]
 SIMDS = 1024   # 256 CUs x 4 SIMDs (MI355X)
 
 
