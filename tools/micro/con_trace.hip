@@ -62,6 +62,17 @@ int main(int argc, char** argv) {
     float ms; hipEventElapsedTime(&ms, e0, e1);
     printf("run %d: %.3f ms  %.2f TF/s\n", it, ms, 2.0 * n * m * m / (ms * 1e-3) / 1e12);
   }
+  // one workgroup per CU: pad the launch with dynamic LDS so a second one cannot fit
+  for (int it = 0; it < 3; ++it) {
+    hipEventRecord(e0, 0);
+    hipLaunchKernelGGL((k_contract<8, EPI_GRAD>), dim3((unsigned)nwg), dim3(256), 80 * 1024, 0,
+                       kp, K, M, X, n_pad, n, n_pad, Uu, mp, m, mp, ca, slab, (int)(kp.L + 5),
+                       (double*)nullptr);
+    hipEventRecord(e1, 0);
+    hipEventSynchronize(e1);
+    float ms; hipEventElapsedTime(&ms, e0, e1);
+    printf("1 WG/CU run %d: %.3f ms  %.2f TF/s\n", it, ms, 2.0 * n * m * m / (ms * 1e-3) / 1e12);
+  }
   std::vector<unsigned long long> ht(nwg * 8);
   hipMemcpy(ht.data(), tr, ht.size() * 8, hipMemcpyDeviceToHost);
   FILE* f = fopen(argc > 1 ? argv[1] : "con_trace.csv", "w");

@@ -83,6 +83,92 @@ __global__ void __launch_bounds__(256, 2) k_loop(const double* __restrict__ K, i
   if (s == 1234.5) out[tid] = s;
 }
 
+// BK = 32 per step, double-buffered, one workgroup per CU (launch_bounds(256, 1): up to 512
+// VGPRs per wave): half the barriers per MFMA of the BK = 16 loop
+template <int SBW>
+__global__ void __launch_bounds__(256, 1) k_loop32(const double* __restrict__ K, int64_t mp,
+                                                   int nsteps, double* out) {
+  constexpr int B2 = 32;
+  __shared__ __attribute__((aligned(16))) double Ka[2][B2 * SBW];
+  __shared__ __attribute__((aligned(16))) double Kb[2][B2 * SBW];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int ta = blockIdx.x % 8, tb = (blockIdx.x / 8) % 8;
+  const int64_t rbeg = (int64_t)(blockIdx.x / 64) * nsteps * B2;
+  d4 acc[4][4];
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+  const int lrow = tid >> 4, lc = tid & 15;   // 16 rows per pass, two passes per step
+  const double2* gA = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + ta * 128) + lc;
+  const double2* gB = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + tb * 128) + lc;
+  const int64_t gstep = B2 * mp / 2, ghalf = 16 * mp / 2;
+  double2 va[8], vb[8];
+  auto gload = [&](int step) {
+    const int64_t o = (int64_t)step * gstep;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        va[h * 4 + q] = gA[o + h * ghalf + 16 * q];
+        vb[h * 4 + q] = gB[o + h * ghalf + 16 * q];
+      }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      double2* pa = reinterpret_cast<double2*>(&Ka[buf][(lrow + 16 * h) * SBW]) + lc;
+      double2* pb = reinterpret_cast<double2*>(&Kb[buf][(lrow + 16 * h) * SBW]) + lc;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { pa[16 * q] = va[h * 4 + q]; pb[16 * q] = vb[h * 4 + q]; }
+    }
+  };
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
+    if (step + 1 < nsteps) gload(step + 1);
+    const double* As = Ka[cur];
+    const double* Bs = Kb[cur];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int krow = kk * 4 + (lane >> 4);
+      double af[4], bf[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        af[f] = As[krow * SBW + wr * 64 + f * 16 + (lane & 15)];
+        bf[f] = Bs[krow * SBW + wc * 64 + f * 16 + (lane & 15)];
+      }
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
+    }
+    if (step + 1 < nsteps) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  double s = 0.0;
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b) s += acc[a][b][0] + acc[a][b][1] + acc[a][b][2] + acc[a][b][3];
+  if (s == 1234.5) out[tid] = s;
+}
+
+template <int SBW>
+void run32(const double* K, int64_t mp, int nsteps16, double* out, int wgs) {
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  const int nsteps = nsteps16 / 2;
+  hipLaunchKernelGGL(k_loop32<SBW>, dim3(wgs), dim3(256), 0, 0, K, mp, nsteps / 4, out);
+  hipEventRecord(e0);
+  hipLaunchKernelGGL(k_loop32<SBW>, dim3(wgs), dim3(256), 0, 0, K, mp, nsteps, out);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms; hipEventElapsedTime(&ms, e0, e1);
+  const double flops = 2.0 * 128 * 128 * 32 * (double)nsteps * wgs;
+  printf("BK32 SB=%d wgs=%d: %.3f ms  %.2f TF/s\n", SBW, wgs, ms, flops / (ms * 1e-3) / 1e12);
+}
+
 template <int MODE>
 void run(const double* K, int64_t mp, int nsteps, double* out) {
   const int nwg = 512;
@@ -115,11 +201,14 @@ int main() {
     free(h);
   }
   const int nsteps = 4000;
+  run32<144>(K, mp, nsteps, out, 256);
+  run32<144>(K, mp, nsteps, out, 512);
   run<0>(K, mp, nsteps, out);
   run<1>(K, mp, nsteps, out);
   run<2>(K, mp, nsteps, out);
   run<3>(K, mp, nsteps, out);
   run<4>(K, mp, nsteps, out);
   run<0>(K, mp, nsteps, out);
+  run32<144>(K, mp, nsteps, out, 256);
   return 0;
 }
