@@ -512,6 +512,17 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
 #ifdef SGP_CON_TRACE
   if (tid == 0) SGP_CON_TRACE(1);
 #endif
+#ifdef SGP_CON_NO_EPILOGUE
+  if constexpr (EPI == EPI_GRAD) {   // timing probe only: k-loop cost without the epilogue
+    double v = 0.0;
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn) v += acc[fm][fn][0] + acc[fm][fn][3];
+    if (v == 1234.5) slab[tid] = v;
+    return;
+  }
+#endif
   // ---------------- alpha (per row), shared by both epilogues ----------------
   double* s_alpha = lds;                    // 128
   double* s_rs = s_alpha + T128;            // 128
@@ -684,10 +695,14 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
             Cc[fn] += w;
             acc[fm][fn][q] = w;
           }
-#pragma unroll
-          for (int r4 = 0; r4 < 4; ++r4)
-            P[fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[fm][fn][r4], xb[r4], P[fn], 0, 0, 0);
         }
+        // r4-major: consecutive MFMAs go to the four independent accumulators P[fn] instead of
+        // four dependent ones into the same P[fn]
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4)
+#pragma unroll
+          for (int fn = 0; fn < 4; ++fn)
+            P[fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[fm][fn][r4], xb[r4], P[fn], 0, 0, 0);
 #ifdef SGP_CON_TRACE
         if (fm == 0 && tid == 0) SGP_CON_TRACE(3);
 #endif
