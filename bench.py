@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--m", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--knots", action="store_true",
+                    help="also the m*d knot gradient (xu_opt = 'simultaneous', SURVEY 8(a) a16)")
     args = ap.parse_args()
     if args.config is None:
         args.config = "C5" if args.mode == "laplace" else "C3"
@@ -118,7 +120,7 @@ def main():
     n_loc = s1 - s0
 
     backend = HipRowBackend(P["X"][s0:s1], P["y"][s0:s1], P["mu"][s0:s1], m, dev_index, cov_fun,
-                            args.mode)
+                            args.mode, knots=args.knots)
     ctx = backend.ctx
     nr_iters = []
     if args.mode == "laplace":
@@ -132,7 +134,19 @@ def main():
                 return o, g
         runner = _Runner()
     else:
-        runner = RowShardedVI(backend, n, None)
+        vi = RowShardedVI(backend, n, None)
+        if args.knots:
+            # the knot bounds of the whole data set, as every rank must use them
+            rng = P["X"].max(axis=0) - P["X"].min(axis=0)
+            kb = np.stack([P["X"].min(axis=0) - rng / 10, P["X"].max(axis=0) + rng / 10], axis=1)
+
+            class _KnotRunner:
+                def eval(self, theta, U, delta):
+                    o, g = vi.eval(theta, U, delta)
+                    return o, (g, ctx.knot_gradient(kb))
+            runner = _KnotRunner()
+        else:
+            runner = vi
     del P["X"]
 
     # an optimizer-like trajectory: theta moves every step (no result can be reused)
@@ -204,7 +218,8 @@ def main():
             "dtype": "f64",
             "data": f"synthetic (SURVEY.md 8(d) {args.config} generator, numpy PCG64)",
             "config": {"workload": f"{args.config}: {workload}, n={n}, m={m}, d={d}, "
-                                   f"{cov_fun}, P={len(names)}, knots fixed",
+                                   f"{cov_fun}, P={len(names)}, "
+                                   + ("+ knot gradient (m*d)" if args.knots else "knots fixed"),
                        "n": n, "m": m, "d": d, "kernel": cov_fun,
                        "parallelism": f"rows{world}" if world > 1 else "single"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
