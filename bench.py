@@ -55,6 +55,7 @@ def cpu_baseline(sizes=(500, 1000, 2000), n_target=1_000_000, m=1024):
     resid = float(np.max(np.abs(A @ np.array([a, b]) - np.asarray(ts))))
     t_target = a + b * n_target
     threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    adj = cpu_adjoint(m=m, n_target=n_target)
     return {
         "value": 1.0 / t_target,
         "unit": "evals/s",
@@ -65,6 +66,35 @@ def cpu_baseline(sizes=(500, 1000, 2000), n_target=1_000_000, m=1024):
                    f"t={[round(t, 3) for t in ts]} s; least-squares t(n)=a+b*n, a={a:.3f}s, "
                    f"b={b:.3e}s/row, max resid {resid:.3f}s; extrapolated to n={n_target}: "
                    f"{t_target:.1f} s/eval"),
+        "adjoint_cpu": adj,
+    }
+
+
+def cpu_adjoint(sizes=(10000, 20000, 40000), n_target=1_000_000, m=1024):
+    """Second CPU bar: the same adjoint algorithm the GPU runs (one SYRK + one
+    K12 P contraction per eval), as the numpy model oracle/adjoint_ref.py, timed on C3 row
+    samples and extrapolated linearly in n like the literal port."""
+    from oracle import adjoint_ref as A
+    W = make_problem("C3", n=1000, m=m)              # warm-up (BLAS thread pool, page faults)
+    A.eval_vi("ard", np.array(list(W["cov_par"].values())), W["X"], W["y"], W["mu"], W["U"],
+              W["delta"])
+    ts = []
+    for ns in sizes:
+        P = make_problem("C3", n=ns, m=m)
+        theta = np.array(list(P["cov_par"].values()))
+        t0 = time.perf_counter()
+        A.eval_vi("ard", theta, P["X"], P["y"], P["mu"], P["U"], P["delta"])
+        ts.append(time.perf_counter() - t0)
+    Amat = np.vstack([np.ones(len(sizes)), np.asarray(sizes, dtype=np.float64)]).T
+    (a, b), *_ = np.linalg.lstsq(Amat, np.asarray(ts), rcond=None)
+    t_target = a + b * n_target
+    return {
+        "value": 1.0 / t_target,
+        "unit": "evals/s",
+        "kind": "port (adjoint algorithm)",
+        "sample": (f"oracle/adjoint_ref.py eval_vi (numpy+OpenBLAS) on C3 rows n={list(sizes)}, "
+                   f"m={m}: t={[round(t, 3) for t in ts]} s; t(n)=a+b*n, a={a:.3f}s, "
+                   f"b={b:.3e}s/row; extrapolated to n={n_target}: {t_target:.1f} s/eval"),
     }
 
 

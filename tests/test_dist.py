@@ -2,7 +2,7 @@
 
 The product backend (HipRowBackend) needs a GPU; here the same driver
 (sparsergps_amd.dist.RowShardedVI) runs the numpy model of libsgp's phase protocol
-(tests/adjoint_ref.py) on each rank's row block, with the two all-reduces going through
+(oracle/adjoint_ref.py) on each rank's row block, with the two all-reduces going through
 torch.distributed/gloo, and the result must equal the single-process literal oracle.
 """
 import os
@@ -29,7 +29,7 @@ class NumpyBackend:
     """Test backend: numpy phases, torch CPU tensors as the reduction buffers."""
 
     def __init__(self, X, y, mu, cov_fun, mode="vi"):
-        import adjoint_ref
+        from oracle import adjoint_ref
         self.rk = (adjoint_ref.NumpyVIRank if mode == "vi" else adjoint_ref.NumpyFITCRank)(X, y, mu)
         self.cov_fun = cov_fun
 
@@ -101,7 +101,7 @@ def test_shard_rows_partition():
 
 class NumpyLaplaceBackend:
     def __init__(self, X, y, mu, f0, cov_fun):
-        import adjoint_ref
+        from oracle import adjoint_ref
         self.rk = adjoint_ref.NumpyLaplaceRank(X, y, mu)
         self.rk.set_f(f0)
         self.cov_fun = cov_fun

@@ -105,7 +105,7 @@ def test_more_knots_than_c3(sgp, mode):
     |K22| underflows here, so the literal oracle's objective is R's det() quirk -inf (Q4): the
     objective is checked against the adjoint model (log-determinants from the factorisation),
     the gradient -- which the reference computes without det() -- against the oracle."""
-    import adjoint_ref as A
+    from oracle import adjoint_ref as A
     P = O.make_gaussian_problem("C3", n=2000, m=1536)
     cp = P["cov_par"]
     theta = np.array(list(cp.values()))

@@ -38,7 +38,7 @@ def test_fitc_det_underflow_case(sgp):
     """C2 with m=1024 > n: the oracle's log(det(Sigma22)) underflows to -inf (R's det()); the
     product computes log-determinants from the factorisation, so it is checked against the
     adjoint model instead (same algebra, numpy)."""
-    import adjoint_ref as A
+    from oracle import adjoint_ref as A
     P = O.make_gaussian_problem("C2", n=900, m=1024)
     th = np.array(list(P["cov_par"].values()))
     o, g = A.eval_fitc("sqexp", th, P["X"], P["y"], P["mu"], P["U"], P["delta"])
@@ -49,7 +49,7 @@ def test_fitc_det_underflow_case(sgp):
 
 
 def test_fitc_larger_against_adjoint_model(sgp):
-    import adjoint_ref as A
+    from oracle import adjoint_ref as A
     P = O.make_gaussian_problem("C3", n=5000, m=260)
     th = np.array(list(P["cov_par"].values()))
     o, g = A.eval_fitc("ard", th, P["X"], P["y"], P["mu"], P["U"], P["delta"])

@@ -96,7 +96,7 @@ def test_warm_start_sequence(sgp):
 
 
 def test_laplace_larger_against_adjoint_model(sgp):
-    import adjoint_ref as A
+    from oracle import adjoint_ref as A
     P = _problem(6000, 256)
     th = np.array(list(P["cov_par"].values()))
     o, g, f, it = A.eval_laplace("sqexp", th, P["X"], P["y"], P["mu"], P["U"], P["f0"], P["a"],

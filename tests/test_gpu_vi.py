@@ -128,7 +128,7 @@ def test_vi_coincident_knots(sgp, cfg):
 
 
 def test_vi_larger_against_adjoint_model(sgp):
-    import adjoint_ref as A
+    from oracle import adjoint_ref as A
     P = _problem("C3", 6000, 300)
     theta = np.array(list(P["cov_par"].values()))
     obj_ref, g_ref = A.eval_vi("ard", theta, P["X"], P["y"], P["mu"], P["U"], P["delta"])
@@ -185,7 +185,7 @@ def test_repeated_evals_full_knot_count(sgp):
             outs.append(ctx.eval_vi(th * (1 + 1e-3 * k), "ard", P["U"], P["delta"]))
             if k >= 1:
                 assert any(name == "contract_knm" for name, _ in ctx.timings())
-    import adjoint_ref as A
+    from oracle import adjoint_ref as A
     o, g = A.eval_vi("ard", th * (1 + 3e-3), P["X"], P["y"], P["mu"], P["U"], P["delta"])
     assert abs(outs[-1][0] - o) / abs(o) < 1e-9
     assert _rel(outs[-1][1], g) < 1e-7

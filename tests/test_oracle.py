@@ -8,7 +8,7 @@ restatement is pinned independently:
   * central finite differences of the objectives in log(theta) vs the analytic gradients
     (the reference's own commented FD checks, covariance_function_derivatives.R:156-173);
   * the committed golden fixtures (tests/golden/make_golden.py) for regression;
-  * the adjoint (S, t, G) protocol of libsgp (tests/adjoint_ref.py) against the literal path.
+  * the adjoint (S, t, G) protocol of libsgp (oracle/adjoint_ref.py) against the literal path.
 """
 import math
 import os
@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 
 from oracle import sgp_oracle as O
-import adjoint_ref as A
+from oracle import adjoint_ref as A
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -216,9 +216,9 @@ def test_golden_fills():
 
 @pytest.mark.parametrize("cov_fun,coinc", [("sqexp", False), ("ard", True)])
 def test_laplace_adjoint_model_matches_oracle(cov_fun, coinc):
-    """The adjoint-form Laplace algebra the GPU implements (tests/adjoint_ref.py) reproduces the
+    """The adjoint-form Laplace algebra the GPU implements (oracle/adjoint_ref.py) reproduces the
     literal newtrap_sparseGP + dlogq_dcov_par, including the reference's comp3 form."""
-    import adjoint_ref as A
+    from oracle import adjoint_ref as A
     P = O.make_poisson_problem(n=260, m=18)
     U = P["U"].copy()
     if coinc:

@@ -1,5 +1,5 @@
 """Diagnostic: phase-by-phase comparison of libsgp's VI protocol with the numpy model
-(tests/adjoint_ref.py) for a list of (n, m) sizes.  Usage: python tools/diag_parity.py"""
+(oracle/adjoint_ref.py) for a list of (n, m) sizes.  Usage: python tools/diag_parity.py"""
 import os
 import sys
 
@@ -7,9 +7,9 @@ import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+sys.path[:0] = [ROOT]
 from oracle import sgp_oracle as O          # noqa: E402
-import adjoint_ref as A                     # noqa: E402
+from oracle import adjoint_ref as A         # noqa: E402
 from sparsergps_amd.dist import HipRowBackend  # noqa: E402
 
 
