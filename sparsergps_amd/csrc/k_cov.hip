@@ -19,50 +19,72 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-// kernel value from raw coordinate differences (xi - uj computed per coordinate)
+// kernel value from raw coordinate differences (xi - uj computed per coordinate).  DT is a
+// compile-time bound on d (8 or SGP_MAXD): the coordinate loops unroll with a c < d guard, so
+// the callers' coordinate arrays stay in registers (runtime-indexed ones went to scratch).
+template <int DT>
 __device__ __forceinline__ double kvalue(const KernParams& kp, const double* xi,
                                          const double* uj) {
+  const int d = kp.d;
   double s = 0.0;
   if (kp.kernel == 0) {
-    for (int c = 0; c < kp.d; ++c) { double t = xi[c] - uj[c]; s = fma(t, t, s); }
+#pragma unroll
+    for (int c = 0; c < DT; ++c)
+      if (c < d) { double t = xi[c] - uj[c]; s = fma(t, t, s); }
     return kp.sig2 * exp(kp.coef * s);
   } else if (kp.kernel == 1) {
-    for (int c = 0; c < kp.d; ++c) { double t = (xi[c] - uj[c]) * kp.rl[c]; s = fma(t, t, s); }
+#pragma unroll
+    for (int c = 0; c < DT; ++c)
+      if (c < d) { double t = (xi[c] - uj[c]) * kp.rl[c]; s = fma(t, t, s); }
     return kp.sig2 * exp(-s / 2.0);
   } else {
-    for (int c = 0; c < kp.d; ++c) s += fabs(xi[c] - uj[c]);
+#pragma unroll
+    for (int c = 0; c < DT; ++c)
+      if (c < d) s += fabs(xi[c] - uj[c]);
     return kp.sig2 * exp(kp.coef * s);
   }
 }
 
 // d K / d log theta_param for one pair (covariance_function_derivativesC.cpp:35-171, 232-301)
+template <int DT>
 __device__ __forceinline__ double dkvalue(const KernParams& kp, const double* xi,
                                           const double* uj, int param, bool sym) {
   const int d = kp.d;
   if (param == kp.P - 1) {  // tau: 2 tau^2 iff all(x1 == x2)   (l.157-163)
     if (kp.kernel == 2 && !sym) return 0.0;   // exp cross-mode returns zeros (l.520)
     bool eq = true;
-    for (int c = 0; c < d; ++c) eq = eq && (xi[c] == uj[c]);
+#pragma unroll
+    for (int c = 0; c < DT; ++c)
+      if (c < d) eq = eq && (xi[c] == uj[c]);
     return eq ? 2.0 * kp.tau * kp.tau : 0.0;
   }
   if (kp.kernel == 0) {
     double s = 0.0;
-    for (int c = 0; c < d; ++c) { double t = xi[c] - uj[c]; s = fma(t, t, s); }
+#pragma unroll
+    for (int c = 0; c < DT; ++c)
+      if (c < d) { double t = xi[c] - uj[c]; s = fma(t, t, s); }
     double e = exp(kp.coef * s);
     if (param == 0) return 2.0 * kp.sigma * e * kp.sigma;                       // l.47
     return (kp.sig2 * e) * ((1.0 / (kp.l[0] * kp.l[0] * kp.l[0])) * s) * kp.l[0];  // l.98-99
   } else if (kp.kernel == 1) {
     double s = 0.0;
-    for (int c = 0; c < d; ++c) { double t = (xi[c] - uj[c]) * kp.rl[c]; s = fma(t, t, s); }
+#pragma unroll
+    for (int c = 0; c < DT; ++c)
+      if (c < d) { double t = (xi[c] - uj[c]) * kp.rl[c]; s = fma(t, t, s); }
     double e = exp(-(s / 2.0));
     if (param == 0) return 2.0 * kp.sigma * e * kp.sigma;                       // l.78
     const int c = param - 1;
     const double lc = kp.l[c];
-    const double dc = xi[c] - uj[c];
+    double dc = 0.0;   // xi[c] - uj[c] without a runtime register index
+#pragma unroll
+    for (int q = 0; q < DT; ++q)
+      if (q == c) dc = xi[q] - uj[q];
     return (kp.sig2 * e) * ((1.0 / (lc * lc * lc)) * (dc * dc)) * lc;          // l.133-134
   } else {  // exp: derivatives use the L2 distance (quirk Q12, l.244, 264)
     double s = 0.0;
-    for (int c = 0; c < d; ++c) { double t = xi[c] - uj[c]; s = fma(t, t, s); }
+#pragma unroll
+    for (int c = 0; c < DT; ++c)
+      if (c < d) { double t = xi[c] - uj[c]; s = fma(t, t, s); }
     double dist = sqrt(s);
     double e = exp(-(1.0 / kp.l[0]) * dist);
     if (param == 0) return 2.0 * kp.sigma * e * kp.sigma;
@@ -71,7 +93,7 @@ __device__ __forceinline__ double dkvalue(const KernParams& kp, const double* xi
 }
 
 // Layer-1 filler: out (n x np, column-major).  Block = 64 rows x 4 column lanes.
-template <bool DERIV>
+template <bool DERIV, int DT>
 __global__ void __launch_bounds__(256) k_fill(KernParams kp, const double* __restrict__ x,
                                               int64_t n, int64_t ldx,
                                               const double* __restrict__ xp, int64_t np,
@@ -80,19 +102,20 @@ __global__ void __launch_bounds__(256) k_fill(KernParams kp, const double* __res
                                               int cols_per_block) {
   const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
   const int64_t j0 = (int64_t)blockIdx.y * cols_per_block;
-  double xi[SGP_MAXD], uj[SGP_MAXD];
-  if (i < n)
-    for (int c = 0; c < kp.d; ++c) xi[c] = x[i + c * ldx];
+  double xi[DT], uj[DT];
+#pragma unroll
+  for (int c = 0; c < DT; ++c) xi[c] = (i < n && c < kp.d) ? x[i + c * ldx] : 0.0;
   for (int64_t jj = threadIdx.y; jj < cols_per_block; jj += 4) {
     const int64_t j = j0 + jj;
     if (j >= np) break;
-    for (int c = 0; c < kp.d; ++c) uj[c] = xp[j + c * ldxp];
+#pragma unroll
+    for (int c = 0; c < DT; ++c) uj[c] = (c < kp.d) ? xp[j + c * ldxp] : 0.0;
     if (i >= n) continue;
     double v;
     if (DERIV) {
-      v = dkvalue(kp, xi, uj, param, sym != 0);
+      v = dkvalue<DT>(kp, xi, uj, param, sym != 0);
     } else {
-      v = kvalue(kp, xi, uj);
+      v = kvalue<DT>(kp, xi, uj);
       if (sym && i == j) v = v + kp.tau2 + kp.delta;   // covariance_functionsC.cpp:91
     }
     out[i + j * ldo] = v;
@@ -180,6 +203,10 @@ __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* 
 }
 
 // K22 (mp x mp, row-major) with diagonal ((sig2 + tau2 + delta) - diag_sub), identity padding.
+// K22 (symmetric mode, nugget on the diagonal).  DT = compile-time coordinate bound so the
+// knot coordinates stay in registers (a runtime-sized local array went to scratch: 108 us at
+// m = 1024 against ~5 us).  Same per-pair arithmetic and summation order as kvalue().
+template <int DT>
 __global__ void __launch_bounds__(256) k_build_kmm(KernParams kp, const double* __restrict__ U,
                                                    int64_t ldu, int64_t m, int64_t mp,
                                                    double diag_sub, double* __restrict__ K22) {
@@ -188,9 +215,27 @@ __global__ void __launch_bounds__(256) k_build_kmm(KernParams kp, const double* 
   if (j >= mp || k >= mp) return;
   double v;
   if (j < m && k < m) {
-    double uj[SGP_MAXD], uk[SGP_MAXD];
-    for (int c = 0; c < kp.d; ++c) { uj[c] = U[j + c * ldu]; uk[c] = U[k + c * ldu]; }
-    v = kvalue(kp, uj, uk);
+    const int d = kp.d;
+    double s = 0.0;
+    if (kp.kernel == 0) {
+#pragma unroll
+      for (int c = 0; c < DT; ++c)
+        if (c < d) { const double t = U[j + c * ldu] - U[k + c * ldu]; s = fma(t, t, s); }
+      v = kp.sig2 * exp(kp.coef * s);
+    } else if (kp.kernel == 1) {
+#pragma unroll
+      for (int c = 0; c < DT; ++c)
+        if (c < d) {
+          const double t = (U[j + c * ldu] - U[k + c * ldu]) * kp.rl[c];
+          s = fma(t, t, s);
+        }
+      v = kp.sig2 * exp(-s / 2.0);
+    } else {
+#pragma unroll
+      for (int c = 0; c < DT; ++c)
+        if (c < d) s += fabs(U[j + c * ldu] - U[k + c * ldu]);
+      v = kp.sig2 * exp(kp.coef * s);
+    }
     if (j == k) v = ((v + kp.tau2) + kp.delta) - diag_sub;
   } else {
     v = (j == k) ? 1.0 : 0.0;
@@ -236,7 +281,7 @@ __global__ void __launch_bounds__(256) k_contract_kmm(KernParams kp, const doubl
     const int64_t o = j * mp + k;
     double g = auj * uvec[k] + b * (Ainv[o] - Binv[o]) + c * M3[o];
     if (vvec) g += e2 * (vj * wvec[k] + wj * vvec[k]);
-    const double kv = kvalue(kp, uj, uk);
+    const double kv = kvalue<DT>(kp, uj, uk);
     const double gk = g * kv;
     acc[0] += 2.0 * gk;                                   // sigma: dK/dlog sigma = 2K
     if (kp.kernel == 0) {
@@ -274,6 +319,7 @@ __global__ void __launch_bounds__(256) k_contract_kmm(KernParams kp, const doubl
 // Knot part of the m x m contraction for d K22 / d u_kc = e_k v^T + v e_k^T,
 // v_l = K22_lk (u_lc - u_kc) / l_c^2: one block per knot k, out[k*d + c] =
 // 2 sum_l G22_kl K22_kl (u_lc - u_kc) (raw coordinates; the 1/l_c^2 is applied by the caller).
+template <int DT>
 __global__ void __launch_bounds__(256) k_knot_kmm(KernParams kp, const double* __restrict__ U,
                                                   int64_t ldu, int64_t m, int64_t mp,
                                                   const double* __restrict__ uvec,
@@ -284,24 +330,28 @@ __global__ void __launch_bounds__(256) k_knot_kmm(KernParams kp, const double* _
                                                   const double* __restrict__ vvec,
                                                   const double* __restrict__ wvec, double e2,
                                                   double* __restrict__ out) {
-  __shared__ double red[4][SGP_MAXD];
+  __shared__ double red[4][DT];
   const int64_t k = blockIdx.x;
-  double uk[SGP_MAXD], acc[SGP_MAXD];
-  for (int q = 0; q < kp.d; ++q) {
-    uk[q] = U[k + q * ldu];
+  double uk[DT], acc[DT];
+#pragma unroll
+  for (int q = 0; q < DT; ++q) {
+    uk[q] = (q < kp.d) ? U[k + q * ldu] : 0.0;
     acc[q] = 0.0;
   }
   for (int64_t l = threadIdx.x; l < m; l += 256) {
-    double ul[SGP_MAXD];
-    for (int q = 0; q < kp.d; ++q) ul[q] = U[l + q * ldu];
+    double ul[DT];
+#pragma unroll
+    for (int q = 0; q < DT; ++q) ul[q] = (q < kp.d) ? U[l + q * ldu] : 0.0;
     const int64_t o = k * mp + l;
     double g = a * uvec[k] * uvec[l] + b * (Ainv[o] - Binv[o]) + c * M3[o];
     if (vvec) g += e2 * (vvec[k] * wvec[l] + wvec[k] * vvec[l]);
-    const double gk = 2.0 * g * kvalue(kp, ul, uk);
-    for (int q = 0; q < kp.d; ++q) acc[q] = fma(gk, ul[q] - uk[q], acc[q]);
+    const double gk = 2.0 * g * kvalue<DT>(kp, ul, uk);
+#pragma unroll
+    for (int q = 0; q < DT; ++q) acc[q] = fma(gk, ul[q] - uk[q], acc[q]);
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int q = 0; q < kp.d; ++q) {
+#pragma unroll
+  for (int q = 0; q < DT; ++q) {
     double v = wave_sum(acc[q]);
     if (lane == 0) red[w][q] = v;
   }
@@ -318,8 +368,12 @@ hipError_t launch_knot_kmm(const KernParams& kp, const double* U, int64_t ldu, i
                            const double* Binv, const double* M3, double a, double b, double c,
                            const double* vvec, const double* wvec, double e2, double* out,
                            hipStream_t s) {
-  hipLaunchKernelGGL(k_knot_kmm, dim3((unsigned)m), dim3(256), 0, s, kp, U, ldu, m, mp, uvec, Ainv,
-                     Binv, M3, a, b, c, vvec, wvec, e2, out);
+  if (kp.d <= 8)
+    hipLaunchKernelGGL(k_knot_kmm<8>, dim3((unsigned)m), dim3(256), 0, s, kp, U, ldu, m, mp, uvec,
+                       Ainv, Binv, M3, a, b, c, vvec, wvec, e2, out);
+  else
+    hipLaunchKernelGGL(k_knot_kmm<SGP_MAXD>, dim3((unsigned)m), dim3(256), 0, s, kp, U, ldu, m,
+                       mp, uvec, Ainv, Binv, M3, a, b, c, vvec, wvec, e2, out);
   return hipGetLastError();
 }
 
@@ -329,8 +383,12 @@ hipError_t launch_fill_cov(const KernParams& kp, const double* x, int64_t n, int
   const int cpb = 64;
   dim3 grid((unsigned)((n + 63) / 64), (unsigned)((np + cpb - 1) / cpb));
   if (n == 0 || np == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_fill<false>, grid, dim3(64, 4), 0, s, kp, x, n, ldx, xp, np, ldxp,
-                     sym ? 1 : 0, 0, out, ldo, cpb);
+  if (kp.d > 8)
+    hipLaunchKernelGGL((k_fill<false, SGP_MAXD>), grid, dim3(64, 4), 0, s, kp, x, n, ldx, xp, np,
+                       ldxp, sym ? 1 : 0, 0, out, ldo, cpb);
+  else
+    hipLaunchKernelGGL((k_fill<false, 8>), grid, dim3(64, 4), 0, s, kp, x, n, ldx, xp, np, ldxp,
+                       sym ? 1 : 0, 0, out, ldo, cpb);
   return hipGetLastError();
 }
 
@@ -340,8 +398,12 @@ hipError_t launch_fill_dcov(const KernParams& kp, const double* x, int64_t n, in
   const int cpb = 64;
   dim3 grid((unsigned)((n + 63) / 64), (unsigned)((np + cpb - 1) / cpb));
   if (n == 0 || np == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_fill<true>, grid, dim3(64, 4), 0, s, kp, x, n, ldx, xp, np, ldxp,
-                     sym ? 1 : 0, param, out, ldo, cpb);
+  if (kp.d > 8)
+    hipLaunchKernelGGL((k_fill<true, SGP_MAXD>), grid, dim3(64, 4), 0, s, kp, x, n, ldx, xp, np,
+                       ldxp, sym ? 1 : 0, param, out, ldo, cpb);
+  else
+    hipLaunchKernelGGL((k_fill<true, 8>), grid, dim3(64, 4), 0, s, kp, x, n, ldx, xp, np, ldxp,
+                       sym ? 1 : 0, param, out, ldo, cpb);
   return hipGetLastError();
 }
 
@@ -421,7 +483,11 @@ hipError_t launch_build_knm_t(const KernParams& kp, const double* X, int64_t ldx
 hipError_t launch_build_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,
                             int64_t mp, double diag_sub, double* K22, hipStream_t s) {
   dim3 grid((unsigned)(mp / 64), (unsigned)((mp + 3) / 4));
-  hipLaunchKernelGGL(k_build_kmm, grid, dim3(64, 4), 0, s, kp, U, ldu, m, mp, diag_sub, K22);
+  if (kp.d <= 8)
+    hipLaunchKernelGGL(k_build_kmm<8>, grid, dim3(64, 4), 0, s, kp, U, ldu, m, mp, diag_sub, K22);
+  else
+    hipLaunchKernelGGL(k_build_kmm<SGP_MAXD>, grid, dim3(64, 4), 0, s, kp, U, ldu, m, mp,
+                       diag_sub, K22);
   return hipGetLastError();
 }
 

@@ -137,13 +137,23 @@ __device__ __forceinline__ double rsqrt_nr(double p) {
 }
 
 // Pivot of the SPD Gauss-Jordan inverse: P = inv(B) for a 64x64 SPD block B (a Schur
-// complement) read from B[i * ldb + j] (global or LDS), by the symmetric sweep operator:
-// 64 in-place sweeps, each one barrier and a 4x4 register-blocked rank-1 update per thread
-// (no square roots, no separate triangular inverse).  The sweep pivots d_k are the Schur
-// complements L_kk^2 of the Cholesky factor, so *logd_slot = sum log L_kk = 1/2 sum log d_k;
-// a non-positive pivot sets status = gofs + k + 1 (R's chol() leading-minor order).
+// complement) read from B[i * ldb + j] (global or LDS), by the symmetric sweep operator
+// applied in four 16-wide blocks K (sweeps compose, so sweeping K at once equals its 16
+// scalar sweeps in turn):
+//   W_KK <- Q = -inv(W_KK)          16 scalar sweeps by the one wave that owns rows K, in
+//                                   registers, lanes exchanging by ds_bpermute: no barriers
+//   W_RK <- -F_R,  F = W_:K Q       one 16x16x16 MFMA product per wave
+//   W_KR <- -Q W_RK^T
+//   W_RR <- W_RR + F_R W_RK^T       rank-16 update, MFMA
+// so a pivot costs 64 barrier-free scalar sweeps plus 12 block barriers instead of 64
+// block-wide barriers.  Layout: wave w owns rows 16w..16w+15 as four 16x16 MFMA
+// accumulator tiles (lane l: column l & 15, rows (l >> 4) + 4q).  The scalar sweeps keep
+// the reference arithmetic of the sweep operator; the final W is -inv(B).  The sweep pivots
+// d_k are the Schur complements L_kk^2 of the Cholesky factor, so *logd_slot = sum log L_kk
+// = 1/2 sum log d_k; a non-positive pivot sets status = gofs + k + 1 (R's chol() order).
 // lds: GJ_PIVOT_LDS doubles.  Called by all 256 threads of the block.
-constexpr int GJ_PIVOT_LDS = 2 * 64 + 64;
+constexpr int GJP_LD = 17;                                  // padded row stride (doubles)
+constexpr int GJ_PIVOT_LDS = 2 * 64 * GJP_LD + 64 * GJP_LD + 16 * GJP_LD + 64;
 
 __device__ __forceinline__ double rcp_nr(double d) {
   double r = __builtin_amdgcn_rcp(d);
@@ -152,68 +162,133 @@ __device__ __forceinline__ double rcp_nr(double d) {
   return r;
 }
 
+// lane `src`'s value to every lane (scalar register path)
+__device__ __forceinline__ double readlane_f64(double v, int src) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, src);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// lane K of every 16-lane row to the whole row (DPP row_newbcast, gfx90a+)
+template <int K>
+__device__ __forceinline__ double row_bcast_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x150 + K, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x150 + K, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// runtime-k form for unrolled loops (folds to one case once k is a constant)
+__device__ __forceinline__ double row_bcast_f64(double v, int k) {
+  switch (k) {
+    case 0: return row_bcast_f64<0>(v);    case 1: return row_bcast_f64<1>(v);
+    case 2: return row_bcast_f64<2>(v);    case 3: return row_bcast_f64<3>(v);
+    case 4: return row_bcast_f64<4>(v);    case 5: return row_bcast_f64<5>(v);
+    case 6: return row_bcast_f64<6>(v);    case 7: return row_bcast_f64<7>(v);
+    case 8: return row_bcast_f64<8>(v);    case 9: return row_bcast_f64<9>(v);
+    case 10: return row_bcast_f64<10>(v);  case 11: return row_bcast_f64<11>(v);
+    case 12: return row_bcast_f64<12>(v);  case 13: return row_bcast_f64<13>(v);
+    case 14: return row_bcast_f64<14>(v);  default: return row_bcast_f64<15>(v);
+  }
+}
+
 __device__ __forceinline__ void gj_pivot_body(const double* B, int64_t ldb, int64_t gofs,
                                               double* __restrict__ P,
                                               double* __restrict__ logd_slot,
                                               int* __restrict__ status, double* lds) {
-  double (*colv)[64] = reinterpret_cast<double (*)[64]>(lds);
-  double* piv_s = lds + 128;
-  const int tid = threadIdx.x;
-  const int bi = tid >> 4, bj = tid & 15;
-  double a[4][4];
+  double* Es0 = lds;                          // [2][64][GJP_LD]  column panel W_:K (old)
+  double* Fs = lds + 2 * 64 * GJP_LD;         // [64][GJP_LD]     F = W_:K Q (own rows per wave)
+  double* Qs = Fs + 64 * GJP_LD;              // [16][GJP_LD]     Q = -inv(W_KK)
+  double* piv = Qs + 16 * GJP_LD;             // [64]             sweep pivots
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int lr = lane >> 4, lc = lane & 15;
+  d4 acc[4];
 #pragma unroll
-  for (int ii = 0; ii < 4; ++ii)
+  for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) a[ii][jj] = B[(4 * bi + ii) * ldb + 4 * bj + jj];
-  for (int kb4 = 0; kb4 < 16; ++kb4) {
+    for (int q = 0; q < 4; ++q) acc[ct][q] = B[(16 * wv + lr + 4 * q) * ldb + 16 * ct + lc];
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int kc = 4 * kb4 + kk;
-      const int b = kc & 1;
-      if (bj == kb4) {
+  for (int kb = 0; kb < 4; ++kb) {
+    double* Es = Es0 + (kb & 1) * 64 * GJP_LD;
+    // publish the column panel E = W_:K (every wave's tile kb)
 #pragma unroll
-        for (int ii = 0; ii < 4; ++ii) colv[b][4 * bi + ii] = a[ii][kk];
-      }
-      __syncthreads();
-      const double d = colv[b][kc];
-      const double r = rcp_nr(d);
-      if (tid == 0) {
-        piv_s[kc] = d;
-        if (!(d > 0.0) || !isfinite(d)) atomicCAS(status, 0, (int)(gofs + kc + 1));
-      }
-      // sweep: a_ij <- a_ij - v_i v_j / d with v = column kc and v_kc = -1, row/col kc
-      // zeroed first (gives a_ik = a_ik / d, a_kk = -1/d); the result is -inv(B)
-      double vi[4], vj[4];
+    for (int q = 0; q < 4; ++q) Es[(16 * wv + lr + 4 * q) * GJP_LD + lc] = acc[kb][q];
+    __syncthreads();
+    if (wv == kb) {
+      // 16 scalar sweeps of W_KK in registers: lane (lr, lc) holds rows lr + 4q of column lc
 #pragma unroll
-      for (int ii = 0; ii < 4; ++ii) {
-        const int i = 4 * bi + ii;
-        vi[ii] = (i == kc) ? -r : colv[b][i] * r;
-      }
+      for (int k = 0; k < 16; ++k) {
+        const int kq = k >> 2, kr = k & 3;
+        const double vc = __shfl(acc[kb][kq], lc + 16 * kr, 64);          // W_k,lc
+        const double d = readlane_f64(acc[kb][kq], k + 16 * kr);          // W_kk (uniform)
+        double vr[4];                                                      // W_i,k: lane k
+#pragma unroll                                                             // of each row
+        for (int q = 0; q < 4; ++q) vr[q] = row_bcast_f64(acc[kb][q], k);
+        const double r = rcp_nr(d);
+        if (lane == 0) {
+          piv[16 * kb + k] = d;
+          if (!(d > 0.0) || !isfinite(d)) atomicCAS(status, 0, (int)(gofs + 16 * kb + k + 1));
+        }
+        const double vj = (lc == k) ? -1.0 : vc;
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int j = 4 * bj + jj;
-        vj[jj] = (j == kc) ? -1.0 : colv[b][j];
-      }
-      if (bi == kb4) {
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) a[kk][jj] = 0.0;
-      }
-      if (bj == kb4) {
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) a[ii][kk] = 0.0;
+        for (int q = 0; q < 4; ++q) {
+          const int i = lr + 4 * q;
+          const double vi = (i == k) ? -r : vr[q] * r;
+          const double base = (i == k || lc == k) ? 0.0 : acc[kb][q];
+          acc[kb][q] = fma(-vi, vj, base);
+        }
       }
 #pragma unroll
-      for (int ii = 0; ii < 4; ++ii)
+      for (int q = 0; q < 4; ++q) Qs[(lr + 4 * q) * GJP_LD + lc] = acc[kb][q];
+    }
+    __syncthreads();
+    if (wv == kb) {
+      // W_KR <- -Q E_R^T  (tiles ct != kb of the pivot rows)
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) a[ii][jj] = fma(-vi[ii], vj[jj], a[ii][jj]);
+      for (int ct = 0; ct < 4; ++ct) {
+        if (ct == kb) continue;
+        d4 t = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int sk = 0; sk < 4; ++sk) {
+          const double af = -Qs[lc * GJP_LD + 4 * sk + lr];
+          const double bf = Es[(16 * ct + lc) * GJP_LD + 4 * sk + lr];
+          t = __builtin_amdgcn_mfma_f64_16x16x4f64(af, bf, t, 0, 0, 0);
+        }
+        acc[ct] = t;
+      }
+    } else {
+      // F_w = E_w Q; W_wK <- -F_w; W_wR <- W_wR + F_w E_R^T
+      d4 f = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int sk = 0; sk < 4; ++sk) {
+        const double af = Es[(16 * wv + lc) * GJP_LD + 4 * sk + lr];
+        const double bf = Qs[(4 * sk + lr) * GJP_LD + lc];
+        f = __builtin_amdgcn_mfma_f64_16x16x4f64(af, bf, f, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Fs[(16 * wv + lr + 4 * q) * GJP_LD + lc] = f[q];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        if (ct == kb) continue;
+#pragma unroll
+        for (int sk = 0; sk < 4; ++sk) {
+          const double af = Fs[(16 * wv + lc) * GJP_LD + 4 * sk + lr];
+          const double bf = Es[(16 * ct + lc) * GJP_LD + 4 * sk + lr];
+          acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, bf, acc[ct], 0, 0, 0);
+        }
+      }
+      acc[kb] = -f;
     }
   }
 #pragma unroll
-  for (int ii = 0; ii < 4; ++ii)
+  for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) P[(4 * bi + ii) * 64 + 4 * bj + jj] = -a[ii][jj];
+    for (int q = 0; q < 4; ++q) P[(16 * wv + lr + 4 * q) * 64 + 16 * ct + lc] = -acc[ct][q];
   __syncthreads();
-  double lg = (tid < 64) ? log(piv_s[tid]) : 0.0;
+  double lg = (tid < 64) ? log(piv[tid]) : 0.0;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) lg += __shfl_xor(lg, off, 64);
   if (tid == 0) *logd_slot = 0.5 * lg;
