@@ -173,8 +173,8 @@ __device__ __forceinline__ double readlane_f64(double v, int src) {
 template <int K>
 __device__ __forceinline__ double row_bcast_f64(double v) {
   const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x150 + K, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x150 + K, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, 0x150 + K, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0x150 + K, 0xF, 0xF, false);
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
@@ -216,6 +216,7 @@ __device__ __forceinline__ void gj_pivot_body(const double* B, int64_t ldb, int6
     __syncthreads();
     if (wv == kb) {
       // 16 scalar sweeps of W_KK in registers: lane (lr, lc) holds rows lr + 4q of column lc
+      double dk[16];                                                       // the pivots
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         const int kq = k >> 2, kr = k & 3;
@@ -225,10 +226,7 @@ __device__ __forceinline__ void gj_pivot_body(const double* B, int64_t ldb, int6
 #pragma unroll                                                             // of each row
         for (int q = 0; q < 4; ++q) vr[q] = row_bcast_f64(acc[kb][q], k);
         const double r = rcp_nr(d);
-        if (lane == 0) {
-          piv[16 * kb + k] = d;
-          if (!(d > 0.0) || !isfinite(d)) atomicCAS(status, 0, (int)(gofs + 16 * kb + k + 1));
-        }
+        dk[k] = d;
         const double vj = (lc == k) ? -1.0 : vc;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -240,6 +238,16 @@ __device__ __forceinline__ void gj_pivot_body(const double* B, int64_t ldb, int6
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) Qs[(lr + 4 * q) * GJP_LD + lc] = acc[kb][q];
+      // record the pivots; the first non-positive one (R's chol() leading-minor order) sets
+      // status unless an earlier block already did
+      double dl = dk[0];
+#pragma unroll
+      for (int k = 1; k < 16; ++k) dl = (lane == k) ? dk[k] : dl;
+      const bool bad = lane < 16 && (!(dl > 0.0) || !isfinite(dl));
+      const unsigned long long badm = __ballot(bad);
+      if (lane < 16) piv[16 * kb + lane] = dl;
+      if (lane == 0 && badm)
+        atomicCAS(status, 0, (int)(gofs + 16 * kb + __builtin_ctzll(badm) + 1));
     }
     __syncthreads();
     if (wv == kb) {

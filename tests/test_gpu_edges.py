@@ -121,3 +121,25 @@ def test_more_knots_than_c3(sgp, mode):
         g = O.dlogp_dcov_par(cp, "ard", P["U"], P["X"], P["y"], P["mu"], P["delta"])["gradient"]
     assert o_lit == -np.inf                  # the quirk this case exercises
     _close(obj, grad, o, g, cp)
+
+
+@pytest.mark.parametrize("dup_at,order", [(150, 151), (40, 41)])
+def test_not_positive_definite_order(sgp, dup_at, order):
+    """A duplicated knot with a negative jitter makes K22 = Kuu + delta I indefinite from the
+    leading minor of order dup_at + 1 on (the earlier minors are PD: min eigenvalue 0.14);
+    the reference's chol() fails there (an R error, caught by try() in the knot proposals).
+    The GPU inverse must report the same order (SGP_ENOTPD, include/sgp.h)."""
+    from sparsergps_amd._lib import NotPositiveDefinite
+    g = np.random.Generator(np.random.PCG64(77))
+    n, m, d = 500, 200, 3
+    U = g.uniform(0.0, 10.0, size=(m, d))
+    U[dup_at] = U[3]
+    X = g.uniform(0.0, 10.0, size=(n, d))
+    y = np.sin(X).sum(axis=1) + g.normal(0.0, 0.5, size=n)
+    cp = OrderedDict([("sigma", 1.0), ("l", 0.3), ("tau", 0.5)])
+    with pytest.raises(NotPositiveDefinite, match=f"order {order} of Sigma22"):
+        sgp.vi_eval(cp, "sqexp", U, X, y, np.full(n, y.mean()), -1e-3)
+    # the context recovers: a valid evaluation right after succeeds
+    P = _gauss(300, 40, 3, "sqexp", seed=5)
+    obj, _ = sgp.vi_eval(P["cov_par"], "sqexp", P["U"], P["X"], P["y"], P["mu"], P["delta"])
+    assert np.isfinite(obj)
