@@ -861,26 +861,49 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   }
 }
 
-// knot partials: part[r][col] = sum_{ti = r, r+64, ...} slab[ti][col]   (grid: ncol/256 x 64)
+// knot partials: part[r][col] = sum_{ti = r, r+G, ...} slab[ti][col]   (grid: ncol/256 x G).
+// Four independent accumulators keep four loads in flight per thread (the column sum is
+// latency-bound: ~60 rows per thread at n = 1e6).
 __global__ void __launch_bounds__(256)
 k_knot_reduce1(const double* __restrict__ slab, int64_t ntiles, int64_t ncol,
                double* __restrict__ part) {
   const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t r = blockIdx.y;
+  const int64_t r = blockIdx.y, G = gridDim.y;
   if (col >= ncol) return;
-  double s = 0.0;
-  for (int64_t t = r; t < ntiles; t += gridDim.y) s += slab[t * ncol + col];
-  part[r * ncol + col] = s;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int64_t t = r;
+  for (; t + 3 * G < ntiles; t += 4 * G) {
+    s0 += slab[t * ncol + col];
+    s1 += slab[(t + G) * ncol + col];
+    s2 += slab[(t + 2 * G) * ncol + col];
+    s3 += slab[(t + 3 * G) * ncol + col];
+  }
+  for (; t < ntiles; t += G) s0 += slab[t * ncol + col];
+  part[r * ncol + col] = (s0 + s1) + (s2 + s3);
 }
 
+// out[col] (+)= sum_r part[r][col]: 64 columns x 4 row groups per block, LDS combine
 __global__ void __launch_bounds__(256)
 k_knot_reduce2(const double* __restrict__ part, int rows, int64_t ncol, double* __restrict__ out,
                int accumulate) {
-  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (col >= ncol) return;
-  double s = 0.0;
-  for (int r = 0; r < rows; ++r) s += part[(int64_t)r * ncol + col];
-  out[col] = accumulate ? out[col] + s : s;
+  __shared__ double sh[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + tx;
+  double s0 = 0.0, s1 = 0.0;
+  if (col < ncol) {
+    int r = ty;
+    for (; r + 4 < rows; r += 8) {
+      s0 += part[(int64_t)r * ncol + col];
+      s1 += part[(int64_t)(r + 4) * ncol + col];
+    }
+    for (; r < rows; r += 4) s0 += part[(int64_t)r * ncol + col];
+  }
+  sh[ty][tx] = s0 + s1;
+  __syncthreads();
+  if (ty == 0 && col < ncol) {
+    const double s = (sh[0][tx] + sh[1][tx]) + (sh[2][tx] + sh[3][tx]);
+    out[col] = accumulate ? out[col] + s : s;
+  }
 }
 
 // ============================================================================ coincidences
@@ -1217,8 +1240,8 @@ hipError_t launch_knot_reduce(const double* knot_slab, int64_t ntiles, int64_t m
   if (gy * ncol > part_cap) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_knot_reduce1, dim3(gx, (unsigned)gy), dim3(256), 0, s, knot_slab, ntiles,
                      ncol, part);
-  hipLaunchKernelGGL(k_knot_reduce2, dim3(gx), dim3(256), 0, s, part, (int)gy, ncol, out,
-                     accumulate ? 1 : 0);
+  hipLaunchKernelGGL(k_knot_reduce2, dim3((unsigned)((ncol + 63) / 64)), dim3(256), 0, s, part,
+                     (int)gy, ncol, out, accumulate ? 1 : 0);
   return hipGetLastError();
 }
 
