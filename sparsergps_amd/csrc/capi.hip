@@ -144,6 +144,9 @@ struct sgp_ctx {
   int64_t knots_mp = 0;
   uint64_t* khash = nullptr;              // sorted knot coordinate hashes (k_coinc)
   int* kidx = nullptr;                    // knot index of each sorted hash
+  uint8_t* cflag = nullptr;               // per data row: equals some knot (k_coinc)
+  int64_t knots_gen = 0;                  // bumped whenever the resident knot set changes
+  int64_t cflag_gen = -1;                 // knot set cflag was computed for
   std::vector<double> xmin, xmax;         // column ranges of this context's rows
   int phase = 0;
   int last_mode = 0;   // 1 VI, 2 FITC, 3 Laplace: the evaluation sgp_posterior_u refers to
@@ -304,6 +307,7 @@ void ctx_free(sgp_ctx* c) {
     if (p) hipFree(p);
   if (c->khash) hipFree(c->khash);
   if (c->kidx) hipFree(c->kidx);
+  if (c->cflag) hipFree(c->cflag);
   if (c->g_bm) hipGraphExecDestroy(c->g_bm);
   if (c->g_bm_graph) hipGraphDestroy(c->g_bm_graph);
   if (c->g_k22) hipGraphExecDestroy(c->g_k22);
@@ -354,6 +358,7 @@ int upload_knots(sgp_ctx* c, const double* U, int64_t m, int64_t ldu) {
     if (same) return SGP_OK;
   }
   c->knots_valid = false;
+  ++c->knots_gen;
   // staging through pinned host memory, copies async on the context stream; the previous
   // upload's copies must have drained before the buffer is rewritten
   HIPCHK(hipEventSynchronize(c->ev_pin));
@@ -622,6 +627,7 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->tslab, (np_ / 64) * mp);
   st = st ? st : dalloc(&c->khash, mp);
   st = st ? st : dalloc(&c->kidx, mp);
+  st = st ? st : dalloc(&c->cflag, np_);
   if (!st && (hipHostMalloc(reinterpret_cast<void**>(&c->pin),
                             sizeof(double) * (mp * d + m_max + (m_max + 1) / 2 + 8 + RB_N),
                             hipHostMallocDefault) != hipSuccess ||
@@ -770,9 +776,13 @@ static int contract_pass(sgp_ctx* c, const double* M, ConArgs ca, double* rec_ou
                               c->mp, ca, c->slab_con, &nrec, &nwg, c->stream));
   HIPCHK(launch_rowsum(c->slab_con, nrec, nwg, c->slab_small, c->slab_small_cap, rec_out, c->stream));
   // tau's coincidence sums -> record fields 1+L .. 3+L
+  // the rows that equal some knot depend only on (X, knot set): found by hashing once per knot
+  // set (cflag written), later evaluations only revisit the flagged rows
+  const bool flags_known = c->cflag_gen == c->knots_gen;
   HIPCHK(launch_coinc(c->X, c->n_pad, c->n, c->kp.d, c->U, c->mp, c->m, c->khash, c->kidx, c->K,
                       c->mp, M, ca, fused ? c->alpha : ca.alpha_in, c->slab_small,
-                      rec_out + 1 + c->kp.L, c->stream));
+                      rec_out + 1 + c->kp.L, c->cflag, flags_known ? 2 : 1, c->stream));
+  c->cflag_gen = c->knots_gen;
   if (c->knot_on)
     HIPCHK(launch_knot_reduce(c->knot_slab, c->n_pad / SGP_TILE, c->mp, c->kp.d, c->knot_part,
                               KNOT_PART_ROWS * c->mp_max * c->d,
@@ -1825,6 +1835,7 @@ int sgp_eval_full(sgp_ctx* c, int kernel, const double* theta, double delta, uns
   HIPCHK(hipMemcpy2DAsync(c->U, sizeof(double) * mp, c->X, sizeof(double) * c->n_pad,
                           sizeof(double) * mp, (size_t)c->d, hipMemcpyDeviceToDevice, c->stream));
   c->knots_valid = false;
+  ++c->knots_gen;
   HIPCHK(hipMemsetAsync(c->status, 0, sizeof(int) * 4, c->stream));
   HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->stream));
   st = k22_stage(c, 0.0);   // Sigma11 = k(xy, xy) + (tau^2 + delta) I and its inverse

@@ -934,9 +934,13 @@ k_coinc(const double* __restrict__ X, int64_t ldx, int64_t n, int d, const doubl
         const double* __restrict__ alpha, const double* __restrict__ uvec,
         const double* __restrict__ beta, const double* __restrict__ vvec,
         const double* __restrict__ rs_vec, double rs, const double* __restrict__ cdiag,
-        double* __restrict__ part) {
+        double* __restrict__ part, uint8_t* __restrict__ cflag, int flag_mode) {
+  // flag_mode 1: hash every row and record in cflag whether it equals some knot;
+  //           2: cflag is current for this knot set -- only flagged rows are revisited
   double a[3] = {0.0, 0.0, 0.0};
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    if (flag_mode == 2 && !cflag[i]) continue;
+    bool any = false;
     const uint64_t h = coord_hash(X + i, ldx, d);
     int64_t lo = 0, hi = m;   // first position with khash >= h
     while (lo < hi) {
@@ -948,6 +952,7 @@ k_coinc(const double* __restrict__ X, int64_t ldx, int64_t n, int d, const doubl
       bool eq = true;
       for (int c = 0; c < d; ++c) eq = eq && (X[i + c * ldx] == U[j + c * ldu]);
       if (!eq) continue;
+      any = true;
       double t = 0.0;
       for (int64_t k = 0; k < m; ++k) t = fma(K[i * mp + k], M[k * mp + j], t);
       double g = (rs_vec ? rs * rs_vec[i] : rs) * t;
@@ -957,6 +962,7 @@ k_coinc(const double* __restrict__ X, int64_t ldx, int64_t n, int d, const doubl
       a[1] += 1.0;
       a[2] += cdiag ? cdiag[j] : 0.0;
     }
+    if (flag_mode == 1) cflag[i] = any ? 1 : 0;
   }
   __shared__ double sh[4][3];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1216,12 +1222,13 @@ hipError_t launch_gemm_tn(const double* A, int64_t lda, int64_t ma, const double
 hipError_t launch_coinc(const double* X, int64_t ldx, int64_t n, int d, const double* U,
                         int64_t ldu, int64_t m, const uint64_t* khash, const int* kidx,
                         const double* K, int64_t mp, const double* M, const ConArgs& ca,
-                        const double* alpha, double* part, double* rec, hipStream_t s) {
+                        const double* alpha, double* part, double* rec, uint8_t* cflag,
+                        int flag_mode, hipStream_t s) {
   int64_t nb = (n + 255) / 256;
   if (nb > 1024) nb = 1024;
   hipLaunchKernelGGL(k_coinc, dim3((unsigned)nb), dim3(256), 0, s, X, ldx, n, d, U, ldu, m, khash,
                      kidx, K, mp, M, alpha, ca.uvec, ca.beta_in, ca.vvec, ca.rs_vec, ca.rs,
-                     ca.cdiag, part);
+                     ca.cdiag, part, cflag, flag_mode);
   hipLaunchKernelGGL(k_coinc_add, dim3(1), dim3(256), 0, s, part, (int)nb, rec);
   return hipGetLastError();
 }

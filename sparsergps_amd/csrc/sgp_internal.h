@@ -278,4 +278,5 @@ hipError_t launch_colnorm2(const double* K, int64_t n_pad, int64_t mp, double* p
 hipError_t launch_coinc(const double* X, int64_t ldx, int64_t n, int d, const double* U,
                         int64_t ldu, int64_t m, const uint64_t* khash, const int* kidx,
                         const double* K, int64_t mp, const double* M, const ConArgs& ca,
-                        const double* alpha, double* part, double* rec, hipStream_t s);
+                        const double* alpha, double* part, double* rec, uint8_t* cflag,
+                        int flag_mode, hipStream_t s);

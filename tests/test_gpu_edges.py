@@ -143,3 +143,24 @@ def test_not_positive_definite_order(sgp, dup_at, order):
     P = _gauss(300, 40, 3, "sqexp", seed=5)
     obj, _ = sgp.vi_eval(P["cov_par"], "sqexp", P["U"], P["X"], P["y"], P["mu"], P["delta"])
     assert np.isfinite(obj)
+
+
+@pytest.mark.parametrize("mode", ["vi", "fitc"])
+def test_coincidence_flags_follow_knot_changes(sgp, mode):
+    """One context, knot sets alternating between data rows (x_i == u_j exactly: the tau
+    coincidence rule, quirk Q5) and random knots.  The rows that equal a knot are found once
+    per knot set and cached; every evaluation must still match the oracle."""
+    P = _gauss(400, 30, 3, "sqexp", seed=31)
+    X, y, mu, cp = P["X"], P["y"], P["mu"], P["cov_par"]
+    U_on = X[[5, 17, 40, 99, 123] + list(range(200, 225))].copy()
+    U_off = P["U"]
+    for U in (U_on, U_off, U_on, U_on, U_off):
+        if mode == "vi":
+            obj, grad = sgp.vi_eval(cp, "sqexp", U, X, y, mu, P["delta"])
+            o = O.elbo_eval(cp, "sqexp", U, X, y, mu, P["delta"])
+            g = O.delbo_dcov_par(cp, "sqexp", U, X, y, mu, P["delta"])["gradient"]
+        else:
+            obj, grad = sgp.fitc_eval(cp, "sqexp", U, X, y, mu, P["delta"])
+            o = O.fitc_obj_eval(cp, "sqexp", U, X, y, mu, P["delta"])
+            g = O.dlogp_dcov_par(cp, "sqexp", U, X, y, mu, P["delta"])["gradient"]
+        _close(obj, grad, o, g, cp)
