@@ -7,6 +7,8 @@
 //   MODE 2  no global loads, no LDS stores (fragment reads + barrier + MFMA)
 //   MODE 3  no barrier (fragment reads + MFMA only)
 //   MODE 4  MFMA only (fragments in registers)
+// k_loop8: the same tile with 8 waves per workgroup (64 x 32 per wave).  MI355X r1: MODE 2
+// 74.4 vs 73.1 TF/s, but the full loop 68.1 vs 69.2 (the 4-wave loop stays)
 //   build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -o kloop kloop.hip ; run: ./kloop
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -184,6 +186,86 @@ void run(const double* K, int64_t mp, int nsteps, double* out) {
   printf("MODE %d: %.3f ms  %.2f TF/s\n", MODE, ms, flops / (ms * 1e-3) / 1e12);
 }
 
+
+// 8 waves per 128x128 workgroup (2 x 4, 64 x 32 per wave: 4 x 2 fragments, 64 accumulator
+// VGPRs), 2 WGs per CU = 4 waves per SIMD: more waves to hide LDS / barrier latency at 1.5x
+// the fragment reads per MFMA.  MODE as k_loop (0 full, 2 no global loads / LDS stores).
+template <int MODE>
+__global__ void __launch_bounds__(512, 2) k_loop8(const double* __restrict__ K, int64_t mp,
+                                                  int nsteps, double* out) {
+  __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
+  __shared__ __attribute__((aligned(16))) double Kb[2][BK * SB];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 2, wc = wv & 3;
+  const int ta = blockIdx.x % 8, tb = (blockIdx.x / 8) % 8;
+  const int64_t rbeg = (int64_t)(blockIdx.x / 64) * nsteps * BK;
+  d4 acc[4][2];
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+  const int lrow = tid >> 5, lc = tid & 31;   // 16 rows x 32 double2 per operand
+  const double2* gA = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + ta * 128) + lc;
+  const double2* gB = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + tb * 128) + lc;
+  const int64_t gstep = BK * mp / 2;
+  double2 va0, va1, vb0, vb1;
+  va0 = va1 = vb0 = vb1 = make_double2(1.0 + tid * 1e-9, 1.0);
+  auto gload = [&](int step) {
+    const int64_t o = (int64_t)step * gstep;
+    va0 = gA[o]; va1 = gA[o + 32];
+    vb0 = gB[o]; vb1 = gB[o + 32];
+  };
+  auto sstore = [&](int buf) {
+    double2* pa = reinterpret_cast<double2*>(&Ka[buf][lrow * SB]) + lc;
+    double2* pb = reinterpret_cast<double2*>(&Kb[buf][lrow * SB]) + lc;
+    pa[0] = va0; pa[32] = va1;
+    pb[0] = vb0; pb[32] = vb1;
+  };
+  if (MODE == 0) gload(0);
+  sstore(0);
+  sstore(1);
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
+    if (MODE == 0 && step + 1 < nsteps) gload(step + 1);
+    const double* As = Ka[cur];
+    const double* Bs = Kb[cur];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int krow = kk * 4 + (lane >> 4);
+      double af[4], bf[2];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) af[f] = As[krow * SB + wr * 64 + f * 16 + (lane & 15)];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) bf[f] = Bs[krow * SB + wc * 32 + f * 16 + (lane & 15)];
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 2; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
+    }
+    if (MODE <= 1 && step + 1 < nsteps) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  double s = 0.0;
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 2; ++b) s += acc[a][b][0] + acc[a][b][1] + acc[a][b][2] + acc[a][b][3];
+  if (s == 1234.5) out[tid] = s;
+}
+
+template <int MODE>
+void run8(const double* K, int64_t mp, int nsteps, double* out) {
+  const int nwg = 512;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  hipLaunchKernelGGL(k_loop8<MODE>, dim3(nwg), dim3(512), 0, 0, K, mp, nsteps / 4, out);
+  hipEventRecord(e0);
+  hipLaunchKernelGGL(k_loop8<MODE>, dim3(nwg), dim3(512), 0, 0, K, mp, nsteps, out);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms; hipEventElapsedTime(&ms, e0, e1);
+  const double flops = 2.0 * 128 * 128 * 16 * (double)nsteps * nwg;
+  printf("8-wave MODE %d: %.3f ms  %.2f TF/s\n", MODE, ms, flops / (ms * 1e-3) / 1e12);
+}
+
 int main() {
   const int64_t mp = 1024, rows = 8 * 16 * 4000;   // 8 row chunks x 4000 steps
   double *K, *out;
@@ -209,6 +291,9 @@ int main() {
   run<3>(K, mp, nsteps, out);
   run<4>(K, mp, nsteps, out);
   run<0>(K, mp, nsteps, out);
-  run32<144>(K, mp, nsteps, out, 256);
+  run8<0>(K, mp, nsteps, out);
+  run8<2>(K, mp, nsteps, out);
+  run8<0>(K, mp, nsteps, out);
+  run<0>(K, mp, nsteps, out);
   return 0;
 }
