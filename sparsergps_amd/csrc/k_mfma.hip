@@ -530,10 +530,9 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   double* s_cd = s_u + T128;                // 128
   double* s_beta = s_cd + T128;             // 128
   double* s_v = s_beta + T128;              // 128
-  double* s_xs = s_v + T128;                // 128 x d   ([row][c], scaled)
-  // s_xs: [row][c] scaled rows (128 x d), or for DT == 8 the MFMA B image [x~ | x~^2] (128 x 16)
-  double* s_us = s_xs + T128 * (DT == 8 ? 16 : kp.d);   // 128 x (d|1) ([col][c], scaled; odd
-                                                      // stride: 16 columns on distinct banks)
+  double* s_xs = s_v + T128;                // MFMA B image [x~ | x~^2] of one coordinate chunk
+  double* s_us = s_xs + T128 * 16;          // 128 x 9 ([col][c], scaled; odd stride: 16
+                                            // columns on distinct banks)
   ku += __shfl_xor(ku, 1, 64);                       // the two halves of row `arow`
   double a2 = 0.0;                                    // alpha^2, counted once (tj == 0)
   if ((tid & 1) == 0) {
@@ -594,7 +593,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   } else {
     // ---------------- gradient epilogue ----------------
     const int d = kp.d;
-    const int sus = d | 1;
+    constexpr int sus = 9;                 // s_us row stride: one chunk of 8, odd
     const bool ard = (kp.kernel == 1);
     const double rl2s = kp.rl2[0];
     const int L = kp.L;
@@ -605,12 +604,12 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
       s_cd[e] = (cdiag && j < m) ? cdiag[j] : 0.0;
     }
     double e_sig = 0.0;
-    double e_l[DT];
-#pragma unroll
-    for (int c = 0; c < DT; ++c) e_l[c] = 0.0;
+    double e_sq = 0.0;                           // one length scale: sum over all coordinates
     double* s_kn;
-
-    if constexpr (DT == 8) {
+    static_assert(DT % 8 == 0, "coordinates are processed in chunks of 8");
+    static_assert(!KNOT || DT == 8, "the knot epilogue is instantiated for d <= 8");
+    constexpr int NCH = DT / 8;
+    {
       // MFMA epilogue.  With W = G o K (zero outside (n, m)) and x~, u~ the (ARD-scaled)
       // coordinates, every per-pair sum the gradient needs is a small product over rows:
       //   D[j][c']   = sum_i W_ij XB_ic',  XB = [x~ | x~^2]  (c' < 8 | c' >= 8)
@@ -625,6 +624,9 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
       // 1 KiB row per wave-instruction, no VGPRs held), the first stage before the coordinate
       // staging so its latency hides behind it.  (Fragment-shaped loads straight to VGPRs
       // serialised on one HBM round trip per fragment at this register pressure.)
+      // Coordinates go through the D products in chunks of 8 (DT / 8 chunks): the first chunk
+      // rides on the pass that forms W; each further chunk restages [x~ | x~^2] and u~ and adds
+      // one 16-column MFMA product over the W kept in the accumulators.
       constexpr int KST = 136;                  // stage row stride (doubles)
       double* kst = s_us + ((T128 * sus + 1) & ~1);   // 32 x KST, 16-byte aligned
 #define CON_KSTAGE(fm_)                                                                  \
@@ -635,23 +637,26 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
             (const __attribute__((address_space(1))) void*)(K + row_ * mp + j0 + 2 * lane), \
             (__attribute__((address_space(3))) void*)(kst + rho_ * KST), 16, 0, 0);       \
       }
-      CON_KSTAGE(0);
-      for (int e = tid; e < T128 * 8; e += 256) {
-        const int rr = e % T128, c = e / T128;
-        const int64_t i = i0 + rr, j = j0 + rr;
-        double xv = 0.0;
-        if (c < d) {
-          const double sc = ard ? kp.rl[c] : 1.0;
-          xv = (i < n) ? X[i + c * ldx] * sc : 0.0;
-          s_us[rr * sus + c] = (j < m) ? U[j + c * ldu] * sc : 0.0;
-        }
-        s_xs[rr * 16 + c] = xv;
-        s_xs[rr * 16 + 8 + c] = xv * xv;
+      // chunk ch of the coordinates: s_xs = [x~ | x~^2] (128 x 16), s_us = u~ (128 x sus)
+#define CON_XSTAGE(ch_)                                                                  \
+      for (int e = tid; e < T128 * 8; e += 256) {                                        \
+        const int rr = e % T128, c = e / T128, cg = 8 * (ch_) + c;                       \
+        const int64_t i = i0 + rr, j = j0 + rr;                                          \
+        double xv = 0.0;                                                                 \
+        if (cg < d) {                                                                    \
+          const double sc = ard ? kp.rl[cg] : 1.0;                                       \
+          xv = (i < n) ? X[i + cg * ldx] * sc : 0.0;                                     \
+          s_us[rr * sus + c] = (j < m) ? U[j + cg * ldu] * sc : 0.0;                     \
+        }                                                                                \
+        s_xs[rr * 16 + c] = xv;                                                          \
+        s_xs[rr * 16 + 8 + c] = xv * xv;                                                 \
       }
+      CON_KSTAGE(0);
+      CON_XSTAGE(0);
       __builtin_amdgcn_s_waitcnt(0);            // K stage 0 (LDS-DMA) landed
       __syncthreads();
-      s_kn = s_us + ((T128 * sus + 1) & ~1);   // KNOT: [2 (wr)][128 cols][d] (aliases the K
-                                               // stage below; written after its last use)
+      s_kn = kst;                               // KNOT: [2 (wr)][128 cols][d] (aliases the K
+                                                // stage; written after its last use)
 #ifdef SGP_CON_TRACE
       if (tid == 0) SGP_CON_TRACE(4);
 #endif
@@ -715,111 +720,63 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
 #endif
       // D fragment fn: lane l, register q -> column wc*64 + fn*16 + (l>>4) + 4q, c' = l & 15
       const int cp = lane & 15, cc = cp & 7;
-      double E = 0.0;
 #pragma unroll
-      for (int fn = 0; fn < 4; ++fn) {
-        double C = Cc[fn];
-        C += __shfl_xor(C, 16, 64);
-        C += __shfl_xor(C, 32, 64);            // every lane: C of column (lane & 15)
-        if ((lane >> 4) == 0) e_sig += C;
+      for (int ch = 0; ch < NCH; ++ch) {
+        if (8 * ch >= d) break;                 // d is uniform: every thread breaks alike
+        if (ch > 0) {
+          __syncthreads();                      // the previous chunk's s_xs / s_us are read
+          CON_XSTAGE(ch);
+          __syncthreads();
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int jl = wc * 64 + fn * 16 + (lane >> 4) + 4 * q;
-          const double Cq = __shfl(C, (lane >> 4) + 4 * q, 64);
-          const double u = (cc < d) ? s_us[jl * sus + cc] : 0.0;
-          const double pv = P[fn][q];
-          E += (cp >= 8) ? pv : u * fma(u, Cq, -2.0 * pv);
-          if constexpr (KNOT) {
-            if (cp < 8 && cc < d) s_kn[(wr * T128 + jl) * d + cc] = pv - u * Cq;
+          for (int fn = 0; fn < 4; ++fn) P[fn] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int fm = 0; fm < 4; ++fm) {
+            double xb[4];
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4)
+              xb[r4] = s_xs[(wr * 64 + fm * 16 + 4 * r4 + (lane >> 4)) * 16 + (lane & 15)];
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4)
+#pragma unroll
+              for (int fn = 0; fn < 4; ++fn)
+                P[fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[fm][fn][r4], xb[r4], P[fn], 0,
+                                                             0, 0);
           }
         }
-      }
-      E += __shfl_xor(E, 8, 64);
-      E += __shfl_xor(E, 16, 64);
-      E += __shfl_xor(E, 32, 64);              // lanes c (0..7): sum_ij W_ij (x~_ic - u~_jc)^2
-      if (ard) {
+        const bool cok = 8 * ch + cc < d;
+        double E = 0.0;
 #pragma unroll
-        for (int c = 0; c < DT; ++c) e_l[c] = __shfl(E, c, 64);
-      } else {
-        double t = E;
-        t += __shfl_xor(t, 1, 64);
-        t += __shfl_xor(t, 2, 64);
-        t += __shfl_xor(t, 4, 64);
-        e_l[0] = t * rl2s;
-      }
-    } else {
-      for (int e = tid; e < T128 * d; e += 256) {
-        const int rr = e % T128, c = e / T128;
-        const int64_t i = i0 + rr, j = j0 + rr;
-        const double sc = ard ? kp.rl[c] : 1.0;
-        s_xs[rr * d + c] = (i < n) ? X[i + c * ldx] * sc : 0.0;
-        s_us[rr * sus + c] = (j < m) ? U[j + c * ldu] * sc : 0.0;
-      }
-      __syncthreads();
-      s_kn = s_us + T128 * sus;
-
-#pragma unroll
-      for (int fn = 0; fn < 4; ++fn) {
-        const int col = wc * 64 + fn * 16 + (lane & 15);
-        const bool cvalid = (j0 + col) < m;
-
-        double uj[DT];
-#pragma unroll
-        for (int c = 0; c < DT; ++c) uj[c] = (c < d) ? s_us[col * sus + c] : 0.0;
-        const double ucol = s_u[col];
-        const double vcol = with_v ? s_v[col] : 0.0;
-        double kn[DT];
-        if constexpr (KNOT) {
-#pragma unroll
-          for (int c = 0; c < DT; ++c) kn[c] = 0.0;
-        }
-#pragma unroll
-        for (int fm = 0; fm < 4; ++fm) {
-          // the fragment's 4 K values (K is zero-padded: every address valid)
-          double kv[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            kv[q] = Kt[(int64_t)(wr * 64 + fm * 16 + (lane >> 4) + 4 * q) * mp + col];
+        for (int fn = 0; fn < 4; ++fn) {
+          double C = Cc[fn];
+          C += __shfl_xor(C, 16, 64);
+          C += __shfl_xor(C, 32, 64);            // every lane: C of column (lane & 15)
+          if (ch == 0 && (lane >> 4) == 0) e_sig += C;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
-            const bool valid = cvalid && ((i0 + row) < n);
-            double G = s_rs[row] * acc[fm][fn][q];
-            if constexpr (V2) G = fma(s_beta[row], vcol, G);
-            G = fma(s_alpha[row], ucol, G);
-            const double gk = valid ? G * kv[q] : 0.0;
-            e_sig += gk;
-            const double* xr = &s_xs[row * d];
-            double s2 = 0.0;
-#pragma unroll
-            for (int c = 0; c < DT; ++c) {
-              if (c < d) {
-                const double t = xr[c] - uj[c];
-                const double tt = t * t;
-                s2 += tt;
-                if (ard) e_l[c] = fma(gk, tt, e_l[c]);
-                if constexpr (KNOT) kn[c] = fma(gk, t, kn[c]);
-              }
-            }
-            if (!ard) e_l[0] = fma(gk, s2 * rl2s, e_l[0]);
-            // tau's coincidence sums (x_i == u_j exactly) are not accumulated here: k_coinc
-            // finds those pairs by hash and recomputes their G_ij (launch_coinc)
-          }
-        }
-        if constexpr (KNOT) {
-          // column sums over this wave's 64 rows: the 4 lanes sharing (lane & 15)
-#pragma unroll
-          for (int c = 0; c < DT; ++c) {
-            if (c < d) {
-              double v2 = kn[c];
-              v2 += __shfl_xor(v2, 16, 64);
-              v2 += __shfl_xor(v2, 32, 64);
-              if ((lane >> 4) == 0) s_kn[(wr * T128 + col) * d + c] = v2;
+            const int jl = wc * 64 + fn * 16 + (lane >> 4) + 4 * q;
+            const double Cq = __shfl(C, (lane >> 4) + 4 * q, 64);
+            const double u = cok ? s_us[jl * sus + cc] : 0.0;
+            const double pv = P[fn][q];
+            E += (cp >= 8) ? pv : u * fma(u, Cq, -2.0 * pv);
+            if constexpr (KNOT) {
+              if (cp < 8 && cc < d) s_kn[(wr * T128 + jl) * d + cc] = pv - u * Cq;
             }
           }
         }
-        __builtin_amdgcn_sched_barrier(0);
+        E += __shfl_xor(E, 8, 64);
+        E += __shfl_xor(E, 16, 64);
+        E += __shfl_xor(E, 32, 64);              // lanes c (0..7): sum_ij W_ij (x~_ic - u~_jc)^2
+        if (ard) {
+          if (lane < 8 && 8 * ch + lane < d) red[wv][1 + 8 * ch + lane] = E;
+        } else {
+          double t = E;
+          t += __shfl_xor(t, 1, 64);
+          t += __shfl_xor(t, 2, 64);
+          t += __shfl_xor(t, 4, 64);
+          e_sq += t;
+        }
       }
+#undef CON_XSTAGE
     }
     if constexpr (KNOT) {
       __syncthreads();
@@ -838,13 +795,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     double v;
     v = wave_sum(e_sig);
     if (lane == 0) red[wv][0] = v;
-#pragma unroll
-    for (int c = 0; c < DT; ++c) {
-      if (c < L) {
-        v = (DT == 8) ? e_l[c] : wave_sum(e_l[c]);   // DT == 8: already wave totals
-        if (lane == 0) red[wv][1 + c] = v;
-      }
-    }
+    if (!ard && lane == 0) red[wv][1] = e_sq * rl2s;   // ARD: red[wv][1 + c] written above
     v = wave_sum(a2);
     if (lane == 0) {
       red[wv][1 + L] = 0.0;
@@ -1287,6 +1238,20 @@ hipError_t launch_rowsum(const double* slab, int64_t nrow, int64_t len, double* 
   return hipGetLastError();
 }
 
+template <int DT>
+static void launch_con_grad(bool v2, const KernParams& kp, const double* K, const double* M,
+                            const double* X, int64_t ldx, int64_t n, int64_t n_pad,
+                            const double* U, int64_t ldu, int64_t m, int64_t mp,
+                            const ConArgs& ca, double* slab, int nrec, int64_t nwg,
+                            hipStream_t s) {
+  if (v2)
+    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, true>), dim3((unsigned)nwg), dim3(256), 0, s, kp,
+                       K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
+  else
+    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD>), dim3((unsigned)nwg), dim3(256), 0, s, kp, K,
+                       M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
+}
+
 hipError_t launch_contract_args(const KernParams& kp, const double* K, const double* M,
                                 const double* X, int64_t ldx, int64_t n, int64_t n_pad,
                                 const double* U, int64_t ldu, int64_t m, int64_t mp,
@@ -1327,16 +1292,13 @@ hipError_t launch_contract_args(const KernParams& kp, const double* K, const dou
       hipLaunchKernelGGL((k_contract<8, EPI_GRAD, false, true>), dim3((unsigned)nwg), dim3(256),
                          0, s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec,
                          (double*)nullptr);
-  } else if (ca.beta_in != nullptr) {
-    if (kp.d > 8) return hipErrorInvalidValue;   // two-term epilogue is instantiated for d <= 8
-    hipLaunchKernelGGL((k_contract<8, EPI_GRAD, true>), dim3((unsigned)nwg), dim3(256), 0, s, kp,
-                       K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
-  } else if (kp.d <= 8) {
-    hipLaunchKernelGGL((k_contract<8, EPI_GRAD>), dim3((unsigned)nwg), dim3(256), 0, s, kp, K, M,
-                       X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
   } else {
-    hipLaunchKernelGGL((k_contract<SGP_MAXD, EPI_GRAD>), dim3((unsigned)nwg), dim3(256), 0, s, kp,
-                       K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
+    // coordinate bound DT: one chunk of 8 (C3 and below) or up to SGP_MAXD in chunks of 8
+    const bool v2 = ca.beta_in != nullptr;   // FITC / Laplace two-term epilogue
+    if (kp.d <= 8) launch_con_grad<8>(v2, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab,
+                                      nrec, nwg, s);
+    else launch_con_grad<SGP_MAXD>(v2, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec,
+                                   nwg, s);
   }
   return hipGetLastError();
 }

@@ -164,3 +164,59 @@ def test_coincidence_flags_follow_knot_changes(sgp, mode):
             o = O.fitc_obj_eval(cp, "sqexp", U, X, y, mu, P["delta"])
             g = O.dlogp_dcov_par(cp, "sqexp", U, X, y, mu, P["delta"])["gradient"]
         _close(obj, grad, o, g, cp)
+
+
+def _gauss_hd(n, m, d, cov_fun, seed):
+    """Higher-dimensional inputs (d > 8: the contraction processes coordinates in chunks of 8);
+    length scales ~ sqrt(d) keep K12 away from underflow."""
+    P = _gauss(n, m, d, cov_fun, seed)
+    s = math.sqrt(d)
+    if cov_fun == "ard":
+        P["cov_par"] = OrderedDict([("sigma", 1.2)] + [(f"l{c + 1}", 1.2 * s + 0.2 * c)
+                                                        for c in range(d)] + [("tau", 0.5)])
+    else:
+        P["cov_par"] = OrderedDict([("sigma", 1.2), ("l", 1.4 * s), ("tau", 0.5)])
+    return P
+
+
+HD_SHAPES = [(600, 40, 12, "ard"), (600, 40, 12, "sqexp"), (500, 33, 20, "ard"),
+             (300, 20, 32, "ard")]
+
+
+@pytest.mark.parametrize("n,m,d,cov_fun", HD_SHAPES)
+def test_vi_high_dim(sgp, n, m, d, cov_fun):
+    P = _gauss_hd(n, m, d, cov_fun, seed=400 + d)
+    cp = P["cov_par"]
+    obj, grad = sgp.vi_eval(cp, cov_fun, P["U"], P["X"], P["y"], P["mu"], P["delta"])
+    o = O.elbo_eval(cp, cov_fun, P["U"], P["X"], P["y"], P["mu"], P["delta"])
+    g = O.delbo_dcov_par(cp, cov_fun, P["U"], P["X"], P["y"], P["mu"], P["delta"])["gradient"]
+    assert max(abs(v) for v in g.values()) > 1.0    # a non-trivial gradient
+    _close(obj, grad, o, g, cp)
+
+
+@pytest.mark.parametrize("n,m,d,cov_fun", HD_SHAPES[:3])
+def test_fitc_high_dim(sgp, n, m, d, cov_fun):
+    P = _gauss_hd(n, m, d, cov_fun, seed=500 + d)
+    cp = P["cov_par"]
+    obj, grad = sgp.fitc_eval(cp, cov_fun, P["U"], P["X"], P["y"], P["mu"], P["delta"])
+    o = O.fitc_obj_eval(cp, cov_fun, P["U"], P["X"], P["y"], P["mu"], P["delta"])
+    g = O.dlogp_dcov_par(cp, cov_fun, P["U"], P["X"], P["y"], P["mu"], P["delta"])["gradient"]
+    _close(obj, grad, o, g, cp)
+
+
+def test_laplace_high_dim(sgp):
+    g0 = np.random.Generator(np.random.PCG64(77))
+    n, m, d = 400, 30, 10
+    X = g0.uniform(0.0, 10.0, size=(n, d))
+    U = g0.uniform(0.0, 10.0, size=(m, d))
+    f = 0.5 * np.sin(X).sum(axis=1) / math.sqrt(d) + math.log(2.0)
+    y = g0.poisson(np.exp(f)).astype(np.float64)
+    mu = np.full(n, math.log(y.mean()))
+    f0 = mu.copy()
+    cp = OrderedDict([("sigma", 1.0), ("l", 1.4 * math.sqrt(d)), ("tau", 0.1)])
+    nr = O.newtrap_sparseGP(f0, cp, "sqexp", X, U, y, mu, 1.0, 1e-6, tol=1e-5)
+    g = O.dlogq_dcov_par(cp, "sqexp", U, X, y, nr["gp"], mu, 1.0, 1e-6)["gradient"]
+    r = sgp.laplace_eval(cp, "sqexp", U, X, y, mu, f0, 1.0, 1e-6, tol=1e-5)
+    ov = nr["objective_function_values"]
+    assert r["nr_iter"] == len(ov)
+    _close(r["objective"], r["gradient"], ov[-1], g, cp)

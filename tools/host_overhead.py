@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Host-side cost of one VI evaluation at C3 on one GPU: wall time of each API call of the
 phase protocol (the GPU runs asynchronously except in finish), to find host gaps between
-evaluations.  usage: python tools/host_overhead.py [steps]"""
+evaluations.  usage: python tools/host_overhead.py [steps] [rows]"""
 import os
 import sys
 import time
@@ -18,7 +18,8 @@ def main():
     from sparsergps_amd.workloads import make_gaussian_problem
     from sparsergps_amd.dist import HipRowBackend
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-    P = make_gaussian_problem("C3")
+    rows = int(sys.argv[2]) if len(sys.argv) > 2 else None
+    P = make_gaussian_problem("C3", n=rows)
     n, m = P["X"].shape[0], P["U"].shape[0]
     names = S.param_names("ard", 8)
     th0 = np.array([P["cov_par"][k] for k in names])
