@@ -213,7 +213,7 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
 /* Knot gradients (xu_opt = "simultaneous"; the knot branches of delbo_dcov_par
  * R/vi_functions.R:425-593, dlogp_dcov_par R/laplace_approx_gradient.R:973-1126 and
  * dlogq_dcov_par 341-543, with dsqexp_dx2 / dsqexp_dx2_ard
- * R/covariance_function_derivatives.R:178-302 as dcov_fun_dknot; d <= 8).  When enabled,
+ * R/covariance_function_derivatives.R:178-302 as dcov_fun_dknot).  When enabled,
  * every evaluation also contracts G against dK12/du in the same GEMM epilogue, and the
  * multi-GPU second reduction buffers grow by sgp_knot_red_extra(d, m) doubles (VI, FITC;
  * sgp_lap_red_count already has room).  sgp_knot_gradient then returns, row-major

@@ -133,7 +133,7 @@ struct sgp_ctx {
   int64_t m = 0, mp = 0, n_global = 0;
   double delta = 0.0;
   unsigned flags = 0;
-  // knot gradients (opt-in, d <= 8)
+  // knot gradients (opt-in)
   bool knot_on = false;
   double *knot_slab = nullptr, *knot_part = nullptr, *knot_kmm = nullptr;
   std::vector<double> knot_raw;           // d F / d u (m x d, row-major), before the chain factor
@@ -613,8 +613,9 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->cdiag, mp);
   st = st ? st : dalloc(&c->status, 4);
   st = st ? st : dalloc(&c->red1, sgp_vi_red1_count(m_max));
-  st = st ? st : dalloc(&c->red2, 64 + mp * 8);
-  st = st ? st : dalloc(&c->red2f, sgp_fitc_red2_count(SGP_KERNEL_ARD, SGP_MAXD, m_max) + mp * 8);
+  // second reductions, with room for the knot partials (mp x d) after the records
+  st = st ? st : dalloc(&c->red2, 64 + mp * d);
+  st = st ? st : dalloc(&c->red2f, sgp_fitc_red2_count(SGP_KERNEL_ARD, SGP_MAXD, m_max) + mp * d);
   st = st ? st : dalloc(&c->slab_syrk, c->slab_syrk_cap);
   st = st ? st : dalloc(&c->slab_con, c->slab_con_cap);
   // small-reduction partials: the dot/colsum helpers, and k_contract_kmm's one record per knot
@@ -822,10 +823,6 @@ static int knot_finish(sgp_ctx* c, const double* knot_red, const double* uvec, c
 int sgp_ctx_enable_knot_grad(sgp_ctx* c, int enable) {
   if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
   if (!enable) { c->knot_on = false; return SGP_OK; }
-  if (c->d > 8) {
-    set_err("knot gradients are implemented for d <= 8 (d = %d)", c->d);
-    return SGP_EINVAL;
-  }
   HIPCHK(hipSetDevice(c->device));
   if (!c->knot_slab) {
     int st = dalloc(&c->knot_slab, (c->n_pad / SGP_TILE) * c->mp_max * c->d);
@@ -1402,7 +1399,7 @@ static int64_t lap_rec_off(int64_t mp) { return mp * mp + mp + 8; }
 
 int64_t sgp_lap_red_count(int kernel, int d, int64_t m) {
   const int64_t mp = round_up(m, SGP_TILE);
-  return 2 * (mp * mp + mp + 8) + 2 * (num_ls(kernel, d) + 5) + 8 + mp * 8;
+  return 2 * (mp * mp + mp + 8) + 2 * (num_ls(kernel, d) + 5) + 8 + mp * d;   // + knot partials
 }
 
 static int lap_ensure(sgp_ctx* c) {

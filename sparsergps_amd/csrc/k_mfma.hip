@@ -607,7 +607,6 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     double e_sq = 0.0;                           // one length scale: sum over all coordinates
     double* s_kn;
     static_assert(DT % 8 == 0, "coordinates are processed in chunks of 8");
-    static_assert(!KNOT || DT == 8, "the knot epilogue is instantiated for d <= 8");
     constexpr int NCH = DT / 8;
     {
       // MFMA epilogue.  With W = G o K (zero outside (n, m)) and x~, u~ the (ARD-scaled)
@@ -655,8 +654,8 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
       CON_XSTAGE(0);
       __builtin_amdgcn_s_waitcnt(0);            // K stage 0 (LDS-DMA) landed
       __syncthreads();
-      s_kn = kst;                               // KNOT: [2 (wr)][128 cols][d] (aliases the K
-                                                // stage; written after its last use)
+      s_kn = kst;                               // KNOT: [2 (wr)][128 cols][8] per chunk
+                                                // (aliases the K stage, after its last use)
 #ifdef SGP_CON_TRACE
       if (tid == 0) SGP_CON_TRACE(4);
 #endif
@@ -759,7 +758,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
             const double pv = P[fn][q];
             E += (cp >= 8) ? pv : u * fma(u, Cq, -2.0 * pv);
             if constexpr (KNOT) {
-              if (cp < 8 && cc < d) s_kn[(wr * T128 + jl) * d + cc] = pv - u * Cq;
+              if (cp < 8) s_kn[(wr * T128 + jl) * 8 + cc] = pv - u * Cq;
             }
           }
         }
@@ -775,16 +774,18 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
           t += __shfl_xor(t, 4, 64);
           e_sq += t;
         }
+        if constexpr (KNOT) {
+          // this chunk's knot partials: the two 64-row halves (wr) combined, [tile][col][d]
+          __syncthreads();
+          for (int e = tid; e < T128 * 8; e += 256) {
+            const int col = e >> 3, c = e & 7, cg = 8 * ch + c;
+            if (cg < d)
+              ca.knot_slab[(ti * mp + j0 + col) * d + cg] =
+                  s_kn[col * 8 + c] + s_kn[(T128 + col) * 8 + c];
+          }
+        }
       }
 #undef CON_XSTAGE
-    }
-    if constexpr (KNOT) {
-      __syncthreads();
-      for (int e = tid; e < T128 * d; e += 256) {
-        const int col = e / d, c = e % d;
-        ca.knot_slab[(ti * mp + j0 + col) * d + c] =
-            s_kn[col * d + c] + s_kn[(T128 + col) * d + c];
-      }
     }
 
 #ifdef SGP_CON_TRACE
@@ -1238,18 +1239,20 @@ hipError_t launch_rowsum(const double* slab, int64_t nrow, int64_t len, double* 
   return hipGetLastError();
 }
 
-template <int DT>
+template <int DT, bool KNOT = false>
 static void launch_con_grad(bool v2, const KernParams& kp, const double* K, const double* M,
                             const double* X, int64_t ldx, int64_t n, int64_t n_pad,
                             const double* U, int64_t ldu, int64_t m, int64_t mp,
                             const ConArgs& ca, double* slab, int nrec, int64_t nwg,
                             hipStream_t s) {
   if (v2)
-    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, true>), dim3((unsigned)nwg), dim3(256), 0, s, kp,
-                       K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
+    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, true, KNOT>), dim3((unsigned)nwg), dim3(256), 0,
+                       s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec,
+                       (double*)nullptr);
   else
-    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD>), dim3((unsigned)nwg), dim3(256), 0, s, kp, K,
-                       M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
+    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, false, KNOT>), dim3((unsigned)nwg), dim3(256), 0,
+                       s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec,
+                       (double*)nullptr);
 }
 
 hipError_t launch_contract_args(const KernParams& kp, const double* K, const double* M,
@@ -1283,15 +1286,11 @@ hipError_t launch_contract_args(const KernParams& kp, const double* K, const dou
     return hipGetLastError();
   }
   if (ca.knot_slab != nullptr) {
-    if (kp.d > 8) return hipErrorInvalidValue;   // knot epilogue is instantiated for d <= 8
-    if (ca.beta_in != nullptr)
-      hipLaunchKernelGGL((k_contract<8, EPI_GRAD, true, true>), dim3((unsigned)nwg), dim3(256), 0,
-                         s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec,
-                         (double*)nullptr);
-    else
-      hipLaunchKernelGGL((k_contract<8, EPI_GRAD, false, true>), dim3((unsigned)nwg), dim3(256),
-                         0, s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec,
-                         (double*)nullptr);
+    const bool v2 = ca.beta_in != nullptr;
+    if (kp.d <= 8) launch_con_grad<8, true>(v2, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca,
+                                            slab, nrec, nwg, s);
+    else launch_con_grad<SGP_MAXD, true>(v2, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab,
+                                         nrec, nwg, s);
   } else {
     // coordinate bound DT: one chunk of 8 (C3 and below) or up to SGP_MAXD in chunks of 8
     const bool v2 = ca.beta_in != nullptr;   // FITC / Laplace two-term epilogue

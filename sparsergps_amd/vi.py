@@ -153,7 +153,7 @@ class SparseGPContext:
         return obj.value, grad
 
     def enable_knot_grad(self, on=True):
-        """Also contract the adjoint against dK/du (knot gradients; d <= 8)."""
+        """Also contract the adjoint against dK/du (knot gradients)."""
         _lib.check(self._lib.sgp_ctx_enable_knot_grad(self.handle, 1 if on else 0))
 
     def knot_red_extra(self, m):

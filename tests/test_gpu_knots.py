@@ -104,3 +104,51 @@ def test_knot_gradient_larger_m(sgp):
             u = P["U"][k, c]
             chain = (b[c, 1] - b[c, 0]) / ((u - b[c, 0]) * (b[c, 1] - u) + 1e-4)
             assert abs(fd * chain - g[k * 3 + c]) / max(1.0, abs(g[k * 3 + c])) < 1e-5
+
+
+def _hd_problem(n, m, d, seed):
+    g = np.random.Generator(np.random.PCG64(seed))
+    X = g.uniform(0.0, 10.0, size=(n, d))
+    U = g.uniform(0.0, 10.0, size=(m, d))
+    y = np.sin(X).sum(axis=1) / np.sqrt(d) + g.normal(0.0, 0.5, size=n)
+    cp = OrderedDict([("sigma", 1.2)] + [(f"l{c + 1}", np.sqrt(d) + 0.2 * c)
+                                          for c in range(d)] + [("tau", 0.45)])
+    return X, U, y, np.full(n, y.mean()), cp
+
+
+@pytest.mark.parametrize("mode,d", [("vi", 12), ("fitc", 12), ("vi", 20)])
+def test_knot_gradient_high_dim(sgp, mode, d):
+    """d > 8: the knot partials leave the contraction epilogue one chunk of 8 coordinates at a
+    time (k_contract<32, ..., KNOT>)."""
+    X, U, y, mu, cp = _hd_problem(200, 7, d, seed=600 + d)
+    delta = 1e-6
+    if mode == "vi":
+        ref = O.delbo_dcov_par(cp, "ard", U, X, y, mu, delta, dcov_fun_dknot="ard")
+        got = sgp.delbo_dcov_par(cp, "ard", True, "dsqexp_dx2_ard", None, U, X, y, None, mu, True,
+                                 delta)
+    else:
+        ref = O.dlogp_dcov_par(cp, "ard", U, X, y, mu, delta, dcov_fun_dknot="ard")
+        got = sgp.dlogp_dcov_par(cp, "ard", True, "ard", None, U, X, y, None, mu, True, delta)
+    kg, kr = np.asarray(got["knot_gradient"]), np.asarray(ref["knot_gradient"])
+    assert np.max(np.abs(kg - kr)) < RTOL * np.max(np.abs(kr))   # relative to the largest
+    for k in cp:
+        assert abs(got["gradient"][k] - ref["gradient"][k]) / max(1, abs(ref["gradient"][k])) < RTOL
+
+
+def test_laplace_knot_gradient_high_dim(sgp):
+    g = np.random.Generator(np.random.PCG64(707))
+    n, m, d = 150, 6, 10
+    X = g.uniform(0.0, 10.0, size=(n, d))
+    U = g.uniform(0.0, 10.0, size=(m, d))
+    f = 0.5 * np.sin(X).sum(axis=1) / np.sqrt(d) + np.log(2.0)
+    y = g.poisson(np.exp(f)).astype(np.float64)
+    mu = np.full(n, np.log(y.mean()))
+    ff = mu + 0.05 * np.cos(np.arange(n))
+    cp = OrderedDict([("sigma", 1.0)] + [(f"l{c + 1}", np.sqrt(d) + 0.2 * c) for c in range(d)]
+                     + [("tau", 0.1)])
+    ref = O.dlogq_dcov_par(cp, "ard", U, X, y, ff, mu, 1.0, 1e-6, dcov_fun_dknot="ard")
+    got = sgp.dlogq_dcov_par(cp, "ard", True, "ard", None, U, X, y, ff, mu, 1.0, 1e-6)
+    kg, kr = np.asarray(got["knot_gradient"]), np.asarray(ref["knot_gradient"])
+    assert np.max(np.abs(kg - kr)) < RTOL * np.max(np.abs(kr))
+    for k in cp:
+        assert abs(got["gradient"][k] - ref["gradient"][k]) / max(1, abs(ref["gradient"][k])) < RTOL

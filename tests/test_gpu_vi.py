@@ -193,8 +193,8 @@ def test_repeated_evals_full_knot_count(sgp):
 
 @pytest.mark.parametrize("d", [12, 32])
 def test_high_dimension_ard_matches_oracle(sgp, d):
-    """d > 8 runs the generic contraction epilogue (k_contract<32>); d = 32 is SGP_MAXD, the
-    widest gradient record (L + 5 = 37 fields)."""
+    """d > 8 runs the contraction epilogue in chunks of 8 coordinates (k_contract<32>); d = 32
+    is SGP_MAXD, the widest gradient record (L + 5 = 37 fields)."""
     rng = np.random.default_rng(100 + d)
     n, m = 300, 24
     X = rng.uniform(0, 10, size=(n, d))
