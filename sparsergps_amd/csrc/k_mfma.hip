@@ -93,7 +93,9 @@ __device__ __forceinline__ void syrk_group(int64_t gi, int nb, int wv, int& ta, 
   }
 }
 
-template <bool WITH_T>
+// WEIGHTED: rows scaled by w (FITC / Laplace); compiled out for the unweighted VI SYRK, whose
+// k-loop otherwise multiplies every A fragment by 1.0 (16 fp64 VALU ops per 64 MFMAs).
+template <bool WITH_T, bool WEIGHTED>
 __global__ void __launch_bounds__(256, 2)
 k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __restrict__ w,
            const double* __restrict__ r, const double* __restrict__ tv,
@@ -154,7 +156,7 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
     vb0 = gB[o_]; vb1 = gB[o_ + 16]; vb2 = gB[o_ + 32]; vb3 = gB[o_ + 48];      \
     if (tid < BK) {                                                             \
       const int64_t rr_ = rbeg + (int64_t)(step) * BK + tid;                    \
-      if (w != nullptr) vw = w[rr_];                                            \
+      if (WEIGHTED) vw = w[rr_];                                                \
       if (with_t) {                                                             \
         vrr = r[rr_];                                                           \
         vr = (tv != nullptr) ? tv[rr_] : ((w != nullptr) ? w[rr_] : 1.0);       \
@@ -190,12 +192,16 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         const int krow = kk * 4 + (lane >> 4);
-        const double wk = (w != nullptr) ? ws[cur][krow] : 1.0;
         double af[4], bf[4];
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-          af[f] = As[krow * SB + f * 16 + (lane & 15)] * wk;
+          af[f] = As[krow * SB + f * 16 + (lane & 15)];
           bf[f] = Bs[krow * SB + f * 16 + (lane & 15)];
+        }
+        if constexpr (WEIGHTED) {
+          const double wk = ws[cur][krow];
+#pragma unroll
+          for (int f = 0; f < 4; ++f) af[f] *= wk;
         }
 #pragma unroll
         for (int fm = 0; fm < 4; ++fm)
@@ -1125,12 +1131,21 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
     double* sl_t = sl_s + (int64_t)q.splits * nblk * 4096;
     double* sl_rr = sl_t + (int64_t)q.splits * q.nb * T128;
     if (sl_rr + q.splits > slab + slab_cap) return hipErrorInvalidValue;
-    if ((part & 1) && with_t)
-      hipLaunchKernelGGL(k_syrk_blk<true>, dim3((unsigned)(q.splits * q.T)), dim3(256), 0, s, K,
-                         n_pad, mp, w, r, tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr);
-    else if (part & 1)
-      hipLaunchKernelGGL(k_syrk_blk<false>, dim3((unsigned)(q.splits * q.T)), dim3(256), 0, s, K,
-                         n_pad, mp, w, r, tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr);
+    const dim3 grid((unsigned)(q.splits * q.T));
+    if (part & 1) {
+      if (with_t && w)
+        hipLaunchKernelGGL((k_syrk_blk<true, true>), grid, dim3(256), 0, s, K, n_pad, mp, w, r, tv,
+                           q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr);
+      else if (with_t)
+        hipLaunchKernelGGL((k_syrk_blk<true, false>), grid, dim3(256), 0, s, K, n_pad, mp, w, r,
+                           tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr);
+      else if (w)
+        hipLaunchKernelGGL((k_syrk_blk<false, true>), grid, dim3(256), 0, s, K, n_pad, mp, w, r,
+                           tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr);
+      else
+        hipLaunchKernelGGL((k_syrk_blk<false, false>), grid, dim3(256), 0, s, K, n_pad, mp, w, r,
+                           tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr);
+    }
     if (part & 2) {
       hipLaunchKernelGGL(k_syrk_reduce_blk, dim3(4096 / 256, (unsigned)nblk), dim3(256), 0, s,
                          sl_s, q.splits, nblk, mp, red);
