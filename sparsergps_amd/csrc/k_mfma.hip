@@ -126,7 +126,7 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
   const bool t_a = with_t && dg >= 0 && tid < T128;
   const bool t_b = with_t && dg >= 0 && tid >= T128 && dte < nb && (dg % 3) == 0;
   const bool t_rr = with_t && dg == 0 && tid == 255;
-  double tacc = 0.0, vrr = 0.0, vr = 0.0;
+  double tacc4[4] = {0.0, 0.0, 0.0, 0.0}, vrr = 0.0, vr = 0.0;
   if (tid == 0) rr_acc = 0.0;
   const int64_t rbeg = (int64_t)split * chunk;
   int64_t rend = rbeg + chunk;
@@ -210,12 +210,17 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
             acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
       }
     }
+    // t rides on the diagonal groups' waves 0-1 (four independent FMA chains).  Those
+    // workgroups are the round's slowest: the weighted SYRK with t takes 19.5 ms at C3 against
+    // 17.3 ms without (FITC) -- spreading t over all groups is the known fix, not yet taken.
     if (t_a) {
 #pragma unroll
-      for (int q = 0; q < BK; ++q) tacc = fma(rw[cur][q], Ka[cur][q * SB + tid], tacc);
+      for (int q = 0; q < BK; ++q)
+        tacc4[q & 3] = fma(rw[cur][q], Ka[cur][q * SB + tid], tacc4[q & 3]);
     } else if (t_b) {
 #pragma unroll
-      for (int q = 0; q < BK; ++q) tacc = fma(rw[cur][q], Kb[cur][q * SB + tid - T128], tacc);
+      for (int q = 0; q < BK; ++q)
+        tacc4[q & 3] = fma(rw[cur][q], Kb[cur][q * SB + tid - T128], tacc4[q & 3]);
     }
     if (t_rr) {
       double sacc = 0.0;
@@ -228,6 +233,7 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
 #undef SYRKB_GLOAD
 #undef SYRKB_SSTORE
 
+  const double tacc = (tacc4[0] + tacc4[1]) + (tacc4[2] + tacc4[3]);
   if (t_a) slab_t[((int64_t)split * nb + dg) * T128 + tid] = tacc;
   if (t_b) slab_t[((int64_t)split * nb + dte) * T128 + tid - T128] = tacc;
   if (t_rr) slab_rr[split] = rr_acc;
