@@ -14,6 +14,9 @@
 // MFMA f64 16x16x4 lane maps (cdna_hip_programming.md Sec.3):
 //   A: lane l holds A[l&15][l>>4];  B: lane l holds B[l>>4][l&15];
 //   C/D: register r of lane l is C[(l>>4) + 4r][l&15].
+#include <algorithm>
+#include <vector>
+
 #include "sgp_internal.h"
 
 namespace {
@@ -93,6 +96,14 @@ __device__ __forceinline__ void syrk_group(int64_t gi, int nb, int wv, int& ta, 
   }
 }
 
+// t = K^T (w r) slices (a kernel argument): group gi computes columns [slice * W, slice * W +
+// W) of K column panel `panel` (entry panel * S + slice, W = 128 / S; -1: none), spread so that
+// no workgroup of the single residency round carries more than one slice (syrk_t_table).
+struct SyrkTMap {
+  signed char e[128];   // per group: panel * S + slice, or -1
+  int S;                // slices per panel
+};
+
 // WEIGHTED: rows scaled by w (FITC / Laplace); compiled out for the unweighted VI SYRK, whose
 // k-loop otherwise multiplies every A fragment by 1.0 (16 fp64 VALU ops per 64 MFMAs).
 template <bool WITH_T, bool WEIGHTED>
@@ -100,13 +111,11 @@ __global__ void __launch_bounds__(256, 2)
 k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __restrict__ w,
            const double* __restrict__ r, const double* __restrict__ tv,
            int64_t chunk, int ngroups, int nb, double* __restrict__ slab,
-           double* __restrict__ slab_t, double* __restrict__ slab_rr) {
+           double* __restrict__ slab_t, double* __restrict__ slab_rr, SyrkTMap tm) {
   __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
   __shared__ __attribute__((aligned(16))) double Kb[2][BK * SB];
   __shared__ double ws[2][BK];
   __shared__ double rw[2][BK];   // with_t: (w r)_i or tv_i of the step's rows
-  __shared__ double rv[2][BK];   // with_t: r_i
-  __shared__ double rr_acc;
 
   const int64_t nwg = (int64_t)gridDim.x;
   const int64_t wgid = xcd_remap(blockIdx.x, nwg);
@@ -116,18 +125,24 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
   int ta, tb, rs, cs, rp, cp;
   syrk_group(gi, nb, wv, ta, tb, rs, cs, rp, cp);
   const bool active = rs >= 0;
-  // t = K^T (w r) (or K^T tv) for the K column blocks this group holds whole and is the owner
-  // of: image A's block g for diagonal group g, and image B's block te for the first of the
-  // three groups that take an extra block of tile te.  rr from diagonal group 0.
+  // t = K^T (w r) (or K^T tv): this group's slice of one of its two K column panels
+  // (c_tmap); rr from diagonal group 0.
   const int64_t noff = (int64_t)nb * (nb - 1) / 2;
   const int dg = (gi >= noff) ? (int)(gi - noff) : -1;
-  const int dte = (dg >= 0) ? (3 * nb + 3) / 4 + dg / 3 : nb;
   constexpr bool with_t = WITH_T;
-  const bool t_a = with_t && dg >= 0 && tid < T128;
-  const bool t_b = with_t && dg >= 0 && tid >= T128 && dte < nb && (dg % 3) == 0;
-  const bool t_rr = with_t && dg == 0 && tid == 255;
+  const int tmap = with_t ? (int)tm.e[gi] : -1;
+  const int tS = with_t ? tm.S : 1, tW = T128 / tS;
+  const int tpan = tmap >= 0 ? tmap / tS : -1;
+  // all 256 threads share the slice: column tid % tW, rows trg, trg + tng, ... of each step
+  const int tng = 256 / tW, trg = tid / tW;
+  const int tcol = tmap >= 0 ? (tmap % tS) * tW + tid % tW : 0;   // column within the panel
+  const bool t_on = with_t && tmap >= 0;
+  const bool t_inb = tpan != ta;                               // panel held as image B
+  // rr = sum (w r)_i r_i: each of the BK staging threads of diagonal group 0 folds in its own
+  // row as it stages it (no per-step loop over the BK rows on one thread)
+  const bool t_rr = with_t && dg == 0 && tid < BK;
+  double rrp = 0.0;
   double tacc4[4] = {0.0, 0.0, 0.0, 0.0}, vrr = 0.0, vr = 0.0;
-  if (tid == 0) rr_acc = 0.0;
   const int64_t rbeg = (int64_t)split * chunk;
   int64_t rend = rbeg + chunk;
   if (rend > n_pad) rend = n_pad;
@@ -172,8 +187,9 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
     if (tid < BK) {                                                             \
       ws[buf][tid] = vw;                                                        \
       if (with_t) {                                                             \
-        rw[buf][tid] = (tv != nullptr) ? vr : vr * vrr;   /* (w r)_i or tv_i */  \
-        rv[buf][tid] = vrr;                                                     \
+        const double rw_ = (tv != nullptr) ? vr : vr * vrr; /* (w r)_i or tv_i */ \
+        rw[buf][tid] = rw_;                                                     \
+        if (t_rr) rrp = fma(rw_, vrr, rrp);                                     \
       }                                                                         \
     }                                                                           \
   }
@@ -210,22 +226,17 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
             acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
       }
     }
-    // t rides on the diagonal groups' waves 0-1 (four independent FMA chains).  Those
-    // workgroups are the round's slowest: the weighted SYRK with t takes 19.5 ms at C3 against
-    // 17.3 ms without (FITC) -- spreading t over all groups is the known fix, not yet taken.
-    if (t_a) {
+    // t: at most one W-column slice per workgroup, shared by all four waves (BK / (256 / W)
+    // rows per thread and step).  The with-t SYRK still runs ~1.3 ms (7 %) longer than the
+    // same weighted SYRK without t at C3 (19.2 vs 17.7-18.0 ms, FITC phase 1 vs 2); the cause is
+    // not the t arithmetic's placement (diagonal groups only, or spread: same time).
+    if (t_on) {
+      const double* img = (t_inb ? Kb[cur] : Ka[cur]) + tcol;
 #pragma unroll
-      for (int q = 0; q < BK; ++q)
-        tacc4[q & 3] = fma(rw[cur][q], Ka[cur][q * SB + tid], tacc4[q & 3]);
-    } else if (t_b) {
-#pragma unroll
-      for (int q = 0; q < BK; ++q)
-        tacc4[q & 3] = fma(rw[cur][q], Kb[cur][q * SB + tid - T128], tacc4[q & 3]);
-    }
-    if (t_rr) {
-      double sacc = 0.0;
-      for (int q = 0; q < BK; ++q) sacc += rw[cur][q] * rv[cur][q];
-      rr_acc += sacc;
+      for (int k = 0; k < 8; ++k) {           // 16 / tng rows per thread (tng = 2, 4 or 8)
+        const int q = trg + k * tng;
+        if (q < BK) tacc4[k & 3] = fma(rw[cur][q], img[q * SB], tacc4[k & 3]);
+      }
     }
     if (step + 1 < nsteps) SYRKB_SSTORE(cur ^ 1);
     __syncthreads();
@@ -233,10 +244,25 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
 #undef SYRKB_GLOAD
 #undef SYRKB_SSTORE
 
-  const double tacc = (tacc4[0] + tacc4[1]) + (tacc4[2] + tacc4[3]);
-  if (t_a) slab_t[((int64_t)split * nb + dg) * T128 + tid] = tacc;
-  if (t_b) slab_t[((int64_t)split * nb + dte) * T128 + tid - T128] = tacc;
-  if (t_rr) slab_rr[split] = rr_acc;
+  if constexpr (WITH_T) {
+    // the row groups' partials of each column, combined in a fixed order (every thread of the
+    // block reaches these barriers: t_on is uniform per workgroup)
+    __syncthreads();                          // the operand images are no longer read
+    double* tsh = &Ka[0][0];
+    if (t_on) tsh[tid] = (tacc4[0] + tacc4[1]) + (tacc4[2] + tacc4[3]);
+    __syncthreads();
+    if (t_on && tid < tW) {
+      double v = 0.0;
+      for (int g = 0; g < tng; ++g) v += tsh[tid + g * tW];
+      slab_t[((int64_t)split * nb + tpan) * T128 + tcol] = v;
+    }
+  }
+  if (dg == 0 && with_t && wv == 0) {          // lanes 0..BK-1 of wave 0 hold the partials
+    double v = t_rr ? rrp : 0.0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (tid == 0) slab_rr[split] = v;
+  }
   if (!active) return;
   const int64_t bid = (int64_t)rp * (rp + 1) / 2 + cp;
   const int64_t nblk = (int64_t)(2 * nb) * (2 * nb + 1) / 2;
@@ -1094,6 +1120,55 @@ SyrkPlan syrk_plan(int64_t n_pad, int64_t mp) {
 }
 
 // k_syrk_blk: the same split rule over its packed groups (T = workgroups per row chunk)
+// Host mirror of syrk_group's image panels (ta, tb) of group gi.
+static void syrk_group_panels(int64_t gi, int nb, int& ta, int& tb) {
+  const int64_t noff = (int64_t)nb * (nb - 1) / 2;
+  if (gi < noff) {
+    int a = 1;
+    while ((int64_t)(a + 1) * a / 2 <= gi) ++a;
+    ta = a;
+    tb = (int)(gi - (int64_t)a * (a - 1) / 2);
+    return;
+  }
+  const int g = (int)(gi - noff), G = (3 * nb + 3) / 4, te = G + g / 3;
+  ta = g;
+  tb = te < nb ? te : g;
+}
+
+// t slices: S slices per panel (4, 2 or 1: the largest a greedy matching places with at most
+// one slice per group; panels with the fewest holding groups first).  Returns S.
+static int syrk_t_table(int nb, int ngroups, int* tmap) {
+  for (int S = 4; S >= 1; S >>= 1) {
+    std::vector<int> used(ngroups, -1);
+    std::vector<std::vector<int>> holders(nb);
+    for (int gi = 0; gi < ngroups; ++gi) {
+      int ta, tb;
+      syrk_group_panels(gi, nb, ta, tb);
+      holders[ta].push_back(gi);
+      if (tb != ta) holders[tb].push_back(gi);
+    }
+    std::vector<int> order(nb);
+    for (int p = 0; p < nb; ++p) order[p] = p;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+      return holders[x].size() < holders[y].size();
+    });
+    bool ok = true;
+    for (int p : order) {
+      for (int sl = 0; sl < S && ok; ++sl) {
+        bool placed = false;
+        for (int gi : holders[p])
+          if (used[gi] < 0) { used[gi] = p * S + sl; placed = true; break; }
+        ok = placed;
+      }
+    }
+    if (ok) {
+      for (int gi = 0; gi < ngroups; ++gi) tmap[gi] = used[gi];
+      return S;
+    }
+  }
+  return 0;   // no placement (does not happen for nb >= 1: S = 1 needs nb distinct holders)
+}
+
 SyrkPlan syrk_plan_blk(int64_t n_pad, int64_t mp) {
   SyrkPlan p = syrk_plan(n_pad, mp);   // nb, and a starting point
   const int nb = p.nb;
@@ -1138,19 +1213,28 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
     double* sl_rr = sl_t + (int64_t)q.splits * q.nb * T128;
     if (sl_rr + q.splits > slab + slab_cap) return hipErrorInvalidValue;
     const dim3 grid((unsigned)(q.splits * q.T));
+    SyrkTMap tm{};
+    tm.S = 1;
+    if ((part & 1) && with_t) {
+      if (q.T > 128) return hipErrorInvalidValue;
+      int tmap[128];
+      tm.S = syrk_t_table(q.nb, q.T, tmap);
+      if (tm.S == 0) return hipErrorInvalidValue;
+      for (int gi = 0; gi < q.T; ++gi) tm.e[gi] = (signed char)tmap[gi];
+    }
     if (part & 1) {
       if (with_t && w)
         hipLaunchKernelGGL((k_syrk_blk<true, true>), grid, dim3(256), 0, s, K, n_pad, mp, w, r, tv,
-                           q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr);
+                           q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm);
       else if (with_t)
         hipLaunchKernelGGL((k_syrk_blk<true, false>), grid, dim3(256), 0, s, K, n_pad, mp, w, r,
-                           tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr);
+                           tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm);
       else if (w)
         hipLaunchKernelGGL((k_syrk_blk<false, true>), grid, dim3(256), 0, s, K, n_pad, mp, w, r,
-                           tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr);
+                           tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm);
       else
         hipLaunchKernelGGL((k_syrk_blk<false, false>), grid, dim3(256), 0, s, K, n_pad, mp, w, r,
-                           tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr);
+                           tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm);
     }
     if (part & 2) {
       hipLaunchKernelGGL(k_syrk_reduce_blk, dim3(4096 / 256, (unsigned)nblk), dim3(256), 0, s,
