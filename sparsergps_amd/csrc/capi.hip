@@ -153,6 +153,7 @@ struct sgp_ctx {
   // K22 stage runs on `aux` concurrently with phase 1 (it depends only on U and theta)
   hipStream_t aux = nullptr;
   hipEvent_t ev_knots = nullptr, ev_k22 = nullptr;
+  hipEvent_t ev_k22m = nullptr;           // K22 itself built (aux); ev_k22: K22 inverted too
   // phase 2's Bm-independent m x m work (K22inv S K22inv, tr(K22inv S)) also runs on `aux`,
   // concurrently with the latency-bound Bm inversion on the main stream
   hipEvent_t ev_s = nullptr, ev_m3 = nullptr, ev_bm = nullptr;
@@ -316,6 +317,7 @@ void ctx_free(sgp_ctx* c) {
   if (c->ev_pin) hipEventDestroy(c->ev_pin);
   if (c->pin) hipHostFree(c->pin);
   if (c->ev_k22) hipEventDestroy(c->ev_k22);
+  if (c->ev_k22m) hipEventDestroy(c->ev_k22m);
   if (c->ev_s) hipEventDestroy(c->ev_s);
   if (c->ev_m3) hipEventDestroy(c->ev_m3);
   if (c->ev_bm) hipEventDestroy(c->ev_bm);
@@ -575,6 +577,7 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
       hipStreamCreateWithPriority(&c->aux_lo, hipStreamNonBlocking, prio_least) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_knots, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_k22, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_k22m, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_s, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_m3, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_bm, hipEventDisableTiming) != hipSuccess) {
@@ -874,6 +877,8 @@ int sgp_knot_gradient(sgp_ctx* c, const double* bounds, double* grad_knot) {
 
 static int k22_sync(sgp_ctx* c);
 static int k22_launch(sgp_ctx* c, double diag_sub);
+static int k22_build(sgp_ctx* c, double diag_sub);
+static int k22_factor(sgp_ctx* c, bool after_main);
 static int k22_stage(sgp_ctx* c, double diag_sub) {
   int st = k22_sync(c);
   return st ? st : k22_launch(c, diag_sub);
@@ -903,16 +908,18 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
     // diagonal tiles as cheap as the others)
     Scope t(c, "build_knm");
     HIPCHK(launch_build_knm_t(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, mpv, m, mpv, c->K, c->r,
-                              c->tslab, c->stream));
+                              c->tslab, c->stream, false));
   }
-  st = k22_launch(c, kp.tau2);   // aux stream, beside the builder's shared-occupancy head
+  // K22 itself only (aux); its inverse runs in phase 2 beside the Bm inverse -- nothing in
+  // phase 1 needs it, and the latency-bound chain no longer gates the one-round SYRK or shares
+  // the CUs with the builder
+  st = k22_build(c, kp.tau2);
   if (st) return st;
   HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_vi_red1_count(m), c->stream));
   HIPCHK(launch_knot_reduce(c->tslab, c->n_pad / 64, mpv, 1, c->T1, c->mp_max * c->mp_max,
                             red1 + mmv, false,
                             c->stream));
   HIPCHK(launch_dot(c->r, c->r, c->n_pad, c->slab_small, red1 + mmv + mpv, c->stream));
-  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));   // keep the SYRK round unshared
   {
     Scope t(c, "syrk");
     HIPCHK(launch_syrk_aug(c->K, c->n_pad, mpv, c->r, nullptr, c->slab_syrk, c->slab_syrk_cap,
@@ -983,14 +990,29 @@ static int k22_sync(sgp_ctx* c) {
   return SGP_OK;
 }
 
-static int k22_launch(sgp_ctx* c, double diag_sub) {
-  const int64_t mp = c->mp;
+// K22 = Kuu + (tau^2 + delta - diag_sub) I on aux (ev_k22m), and its factorisation/inverse
+// after it on aux (ev_k22).  VI runs the two halves in different phases.
+static int k22_build(sgp_ctx* c, double diag_sub) {
+  HIPCHK(launch_build_kmm(c->kp, c->U, c->mp, c->m, c->mp, diag_sub, c->K22, c->aux));
+  HIPCHK(hipEventRecord(c->ev_k22m, c->aux));
+  return SGP_OK;
+}
+
+static int k22_factor(sgp_ctx* c, bool after_main = false) {
+  if (after_main) {   // not before the main stream's queued work (VI: the one-round SYRK)
+    HIPCHK(hipEventRecord(c->ev_s, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->aux, c->ev_s, 0));
+  }
   Scope t(c, "k22_aux", c->aux);
-  HIPCHK(launch_build_kmm(c->kp, c->U, c->mp, c->m, mp, diag_sub, c->K22, c->aux));
   int st = run_graph(c, c->aux, k22_factor_launches, &c->g_k22, &c->g_k22_graph, &c->g_k22_mp);
   if (st) return st;
   HIPCHK(hipEventRecord(c->ev_k22, c->aux));
   return SGP_OK;
+}
+
+static int k22_launch(sgp_ctx* c, double diag_sub) {
+  int st = k22_build(c, diag_sub);
+  return st ? st : k22_factor(c, false);
 }
 
 // Binv (holding K22 + S * s_scale) inverted in place: 48 small launches, captured into a
@@ -1005,7 +1027,7 @@ static int bm_factor_launches(sgp_ctx* c, hipStream_t s) {
 static int bm_stage(sgp_ctx* c, const double* S, double s_scale) {
   const int64_t mp = c->mp, mm = mp * mp;
   Scope t(c, "dense_bm");
-  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22m, 0));   // Bm needs K22, not its inverse
   HIPCHK(dense_axpby(1.0, c->K22, s_scale, S, c->Binv, mm, c->stream));
   return run_graph(c, c->stream, bm_factor_launches, &c->g_bm, &c->g_bm_graph, &c->g_bm_mp);
 }
@@ -1024,6 +1046,10 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
   const double* t = red1 + mm;
   c->n_global = n_global;
   c->flags = flags;
+  // K22's inverse on aux, concurrently with Bm's on the main stream: two latency-bound chains
+  // of 256-workgroup steps that fit one residency round together
+  int st = k22_factor(c, true);
+  if (st) return st;
   {
     // tr(K22inv S) and M3 = K22inv S K22inv need S and K22inv only: on aux_lo beside the Bm
     // inversion (T22 and K22inv are final once the K22 chain on `aux` has finished).  Beside
@@ -1042,7 +1068,7 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
       HIPCHK(hipEventRecord(c->ev_m3, c->aux_lo));
     }
   }
-  int st = bm_stage(c, S, 1.0 / z);
+  st = bm_stage(c, S, 1.0 / z);
   if (st) return st;
   {
     Scope tm(c, "mm_vectors");
@@ -1056,7 +1082,8 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
       return SGP_OK;
     }
     HIPCHK(launch_dot(c->Binv, S, mm, c->slab_small, c->sc + SC_TRBS, c->stream));
-    // P = tau^-2 K22inv - z^-1 Binv
+    // P = tau^-2 K22inv - z^-1 Binv (and cdiag = diag K22inv for the contraction)
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
     HIPCHK(dense_axpby(1.0 / kp.tau2, c->K22inv, -1.0 / z, c->Binv, c->Pm, mm, c->stream));
     HIPCHK(hipEventRecord(c->ev_bm, c->stream));
   }
@@ -2084,8 +2111,11 @@ int sgp_vi_candidates(sgp_ctx* c, int kernel, const double* theta, const double*
   const double z = kp.tau2 + delta;
   const double* S = c->red1;
   const double* t = c->red1 + mm;
+  st = k22_factor(c, true);   // K22's inverse (aux) beside Bm's, as in sgp_vi_phase2
+  if (st) return st;
   st = bm_stage(c, S, 1.0 / z);
   if (st) return st;
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
   {
     Scope tm(c, "mm_vectors");
     HIPCHK(dense_gemv(c->Binv, mp, t, 1.0 / z, c->uvec, c->stream));

@@ -476,8 +476,10 @@ hipError_t launch_build_knm(const KernParams& kp, const double* X, int64_t ldx, 
 
 hipError_t launch_build_knm_t(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
                               int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
-                              double* K, const double* r, double* tslab, hipStream_t s) {
-  return build_knm_impl(kp, X, ldx, n, n_pad, U, ldu, m, mp, K, r, tslab, chain_shared_rb(mp), s);
+                              double* K, const double* r, double* tslab, hipStream_t s,
+                              bool beside_chain) {
+  return build_knm_impl(kp, X, ldx, n, n_pad, U, ldu, m, mp, K, r, tslab,
+                        beside_chain ? chain_shared_rb(mp) : 0, s);
 }
 
 hipError_t launch_build_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,

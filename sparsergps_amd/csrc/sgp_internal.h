@@ -67,7 +67,8 @@ hipError_t launch_fill_dcov(const KernParams& kp, const double* x, int64_t n, in
 // launch_knot_reduce(tslab, n_pad / 64, mp, 1, ...).
 hipError_t launch_build_knm_t(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
                               int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
-                              double* K, const double* r, double* tslab, hipStream_t s);
+                              double* K, const double* r, double* tslab, hipStream_t s,
+                              bool beside_chain = true);
 // K12 (n_pad x mp, row-major, ld = mp).  Rows >= n and columns >= m are written as 0.
 // beside_chain: the K22 chain runs concurrently on the aux stream (phase 1), so the first row
 // blocks are built at reduced occupancy to leave it room (launch_build_knm_t always does).
