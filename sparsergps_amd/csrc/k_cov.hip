@@ -183,7 +183,10 @@ __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* 
       const bool iv = i < n;
       const double v0 = (jv0 && iv) ? sig2 * sgp_exp_nonpos(scale * s0) : 0.0;
       const double v1 = (jv1 && iv) ? sig2 * sgp_exp_nonpos(scale * s1) : 0.0;
-      *reinterpret_cast<double2*>(&K[i * mp + j]) = make_double2(v0, v1);
+      // streaming store (nontemporal): K12 is re-read only by the next kernel, long after it
+      // has left the caches
+      typedef double nt2 __attribute__((ext_vector_type(2)));
+      __builtin_nontemporal_store(nt2{v0, v1}, reinterpret_cast<nt2*>(&K[i * mp + j]));
       if (rvec) {
         tp0 = fma(v0, rsh[r], tp0);
         tp1 = fma(v1, rsh[r], tp1);
