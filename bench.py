@@ -37,65 +37,117 @@ def make_problem(config, n=None, m=None):
     return make_gaussian_problem(config, n=n, m=m)
 
 
-def cpu_baseline(sizes=(500, 1000, 2000), n_target=1_000_000, m=1024):
-    """Time the literal CPU restatement of the reference (oracle/) on row samples of C3 and
-    extrapolate linearly in n (the reference's per-eval cost is a + b*n at fixed m)."""
+def cpu_info():
+    """Host CPU model, logical CPUs visible to this process and physical cores among them."""
+    model, cores = "unknown", set()
+    try:
+        allowed = os.sched_getaffinity(0)
+    except AttributeError:
+        allowed = set(range(os.cpu_count() or 1))
+    try:
+        proc = phys = core = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "processor":
+                proc = int(v)
+            elif k == "model name":
+                model = v
+            elif k == "physical id":
+                phys = v
+            elif k == "core id":
+                core = v
+                if proc in allowed:
+                    cores.add((phys, core))
+    except OSError:
+        pass
+    return {"model": model, "logical_cpus": len(allowed),
+            "physical_cores": len(cores) or None}
+
+
+def _blas_threads():
     from threadpoolctl import threadpool_info
+    return max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+
+
+def _time_literal(ns, m, threads=None):
+    """One literal-port evaluation (elbo_fun + delbo_dcov_par) at C3 rows n = ns."""
+    from threadpoolctl import threadpool_limits
 
     from oracle import sgp_oracle as O
-    ts = []
-    for ns in sizes:
-        P = make_problem("C3", n=ns, m=m)
+    P = make_problem("C3", n=ns, m=m)
+    with threadpool_limits(limits=threads):
         t0 = time.perf_counter()
         O.elbo_eval(P["cov_par"], "ard", P["U"], P["X"], P["y"], P["mu"], P["delta"])
         O.delbo_dcov_par(P["cov_par"], "ard", P["U"], P["X"], P["y"], P["mu"], P["delta"])
-        ts.append(time.perf_counter() - t0)
+        return time.perf_counter() - t0
+
+
+def _fit(sizes, ts, n_target):
     A = np.vstack([np.ones(len(sizes)), np.asarray(sizes, dtype=np.float64)]).T
     (a, b), *_ = np.linalg.lstsq(A, np.asarray(ts), rcond=None)
-    resid = float(np.max(np.abs(A @ np.array([a, b]) - np.asarray(ts))))
-    t_target = a + b * n_target
-    threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    adj = cpu_adjoint(m=m, n_target=n_target)
-    return {
-        "value": 1.0 / t_target,
+    resid = A @ np.array([a, b]) - np.asarray(ts)
+    return a, b, float(np.max(np.abs(resid) / np.asarray(ts))), a + b * n_target
+
+
+def literal_port(sizes, n_target=1_000_000, m=1024, threads=None):
+    """The reference-faithful restatement (oracle/sgp_oracle.py: the R operation graph --
+    LU solves with n right-hand sides, per-parameter GEMM chains -- on numpy + OpenBLAS) timed
+    at C3 row counts; its cost is a + b n at fixed m, so it is fitted and extrapolated to n."""
+    ts = [_time_literal(ns, m, threads) for ns in sizes]
+    a, b, rel, t_target = _fit(sizes, ts, n_target)
+    return {"value": 1.0 / t_target, "unit": "evals/s", "sizes": list(sizes),
+            "t_s": [round(t, 3) for t in ts], "fit": {"a_s": a, "b_s_per_row": b,
+                                                       "max_rel_resid": rel},
+            "t_target_s": t_target, "threads": threads or _blas_threads()}
+
+
+def adjoint_direct(n=1_000_000, m=1024, chunk=8192):
+    """The optimised CPU bar: the GPU's adjoint algorithm (oracle/adjoint_chunked.py, one SYRK
+    + one K12 P contraction, row-chunked) on the host BLAS, timed directly at the full n."""
+    from oracle import adjoint_chunked as AC
+    P = make_problem("C3", n=n, m=m)
+    theta = np.array(list(P["cov_par"].values()))
+    t0 = time.perf_counter()
+    AC.eval_vi("ard", theta, P["X"], P["y"], P["mu"], P["U"], P["delta"], chunk=chunk)
+    t = time.perf_counter() - t0
+    return {"value": 1.0 / t, "unit": "evals/s", "kind": "port (adjoint algorithm)",
+            "cores": _blas_threads(),
+            "sample": f"oracle/adjoint_chunked.py eval_vi (numpy + OpenBLAS, {chunk}-row chunks) "
+                      f"timed once directly at C3 n={n}, m={m}, d=8: {t:.2f} s/eval "
+                      f"(no extrapolation)"}
+
+
+def cpu_baseline(sizes=(4000, 8000), n_target=1_000_000, m=1024, full=None):
+    """cpu_baseline of the bench line (bounded: ~30-60 s of host time)."""
+    lit = literal_port(sizes, n_target, m)
+    out = {
+        "value": lit["value"],
         "unit": "evals/s",
-        "cores": int(threads),
+        "cores": lit["threads"],
         "kind": "port",
+        "cpu": cpu_info(),
         "sample": (f"oracle/sgp_oracle.py elbo_eval+delbo_dcov_par (literal restatement of "
-                   f"vi_functions.R, numpy+OpenBLAS) on C3 rows n={list(sizes)}, m={m}, d=8: "
-                   f"t={[round(t, 3) for t in ts]} s; least-squares t(n)=a+b*n, a={a:.3f}s, "
-                   f"b={b:.3e}s/row, max resid {resid:.3f}s; extrapolated to n={n_target}: "
-                   f"{t_target:.1f} s/eval"),
-        "adjoint_cpu": adj,
+                   f"vi_functions.R, numpy+OpenBLAS, {lit['threads']} BLAS threads) on C3 rows "
+                   f"n={list(sizes)}, m={m}, d=8: t={lit['t_s']} s; t(n)=a+b*n, "
+                   f"a={lit['fit']['a_s']:.3f}s, b={lit['fit']['b_s_per_row']:.3e}s/row, max "
+                   f"rel resid {lit['fit']['max_rel_resid']:.3f}; extrapolated to "
+                   f"n={n_target}: {lit['t_target_s']:.1f} s/eval"),
+        "adjoint_cpu": adjoint_direct(n_target, m),
     }
+    if full:
+        out["full_plan"] = full
+    return out
 
 
-def cpu_adjoint(sizes=(10000, 20000, 40000), n_target=1_000_000, m=1024):
-    """Second CPU bar: the same adjoint algorithm the GPU runs (one SYRK + one
-    K12 P contraction per eval), as the numpy model oracle/adjoint_ref.py, timed on C3 row
-    samples and extrapolated linearly in n like the literal port."""
-    from oracle import adjoint_ref as A
-    W = make_problem("C3", n=1000, m=m)              # warm-up (BLAS thread pool, page faults)
-    A.eval_vi("ard", np.array(list(W["cov_par"].values())), W["X"], W["y"], W["mu"], W["U"],
-              W["delta"])
-    ts = []
-    for ns in sizes:
-        P = make_problem("C3", n=ns, m=m)
-        theta = np.array(list(P["cov_par"].values()))
-        t0 = time.perf_counter()
-        A.eval_vi("ard", theta, P["X"], P["y"], P["mu"], P["U"], P["delta"])
-        ts.append(time.perf_counter() - t0)
-    Amat = np.vstack([np.ones(len(sizes)), np.asarray(sizes, dtype=np.float64)]).T
-    (a, b), *_ = np.linalg.lstsq(Amat, np.asarray(ts), rcond=None)
-    t_target = a + b * n_target
-    return {
-        "value": 1.0 / t_target,
-        "unit": "evals/s",
-        "kind": "port (adjoint algorithm)",
-        "sample": (f"oracle/adjoint_ref.py eval_vi (numpy+OpenBLAS) on C3 rows n={list(sizes)}, "
-                   f"m={m}: t={[round(t, 3) for t in ts]} s; t(n)=a+b*n, a={a:.3f}s, "
-                   f"b={b:.3e}s/row; extrapolated to n={n_target}: {t_target:.1f} s/eval"),
-    }
+def cpu_baseline_full(n_target=1_000_000, m=1024):
+    """SURVEY 8(d)'s whole CPU plan: the literal port on all cores at n in {1e4, 2e4, 5e4} and
+    on one core at n in {2500, 5000, 1e4}, plus the adjoint bar timed directly at n = 1e6
+    (several minutes of host time: `python bench.py --cpu-full`)."""
+    allc = literal_port((10_000, 20_000, 50_000), n_target, m)
+    one = literal_port((2_500, 5_000, 10_000), n_target, m, threads=1)
+    return {"cpu": cpu_info(), "literal_all_cores": allc, "literal_one_core": one,
+            "adjoint_direct": adjoint_direct(n_target, m)}
 
 
 def main():
@@ -110,9 +162,18 @@ def main():
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--m", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-full", default=None, metavar="OUT_JSON",
+                    help="run only SURVEY 8(d)'s full CPU plan (several minutes, no GPU) and "
+                         "write it to OUT_JSON")
     ap.add_argument("--knots", action="store_true",
                     help="also the m*d knot gradient (xu_opt = 'simultaneous', SURVEY 8(a) a16)")
     args = ap.parse_args()
+    if args.cpu_full:
+        res = cpu_baseline_full()
+        with open(args.cpu_full, "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res), flush=True)
+        return
     if args.config is None:
         args.config = "C5" if args.mode == "laplace" else "C3"
     if (args.mode == "laplace") != (args.config == "C5"):
@@ -133,7 +194,10 @@ def main():
     # a reported number (RCCL is the product path)
     rehearse = os.environ.get("SGP_BENCH_REHEARSE") == "1"
     dev_index = 0 if rehearse else local_rank
-    if world > 1:
+    # launched by torch.distributed.run (RANK in the environment): one process group over RCCL,
+    # and the all-reduces run even at N = 1 (the N = 1 torchrun line rehearses the RCCL path)
+    distributed = world > 1 or "RANK" in os.environ
+    if distributed:
         torch.cuda.set_device(dev_index)
         if rehearse:
             dist.init_process_group("gloo")
@@ -155,7 +219,7 @@ def main():
     nr_iters = []
     if args.mode == "laplace":
         ctx.lap_set_f(P["f0"][s0:s1])      # optimize_gp.R:480 start, then warm starts
-        lap = RowShardedLaplace(backend, None)
+        lap = RowShardedLaplace(backend, None, force_collectives=distributed)
 
         class _Runner:
             def eval(self, theta, U, delta):
@@ -164,16 +228,13 @@ def main():
                 return o, g
         runner = _Runner()
     else:
-        vi = RowShardedVI(backend, n, None)
+        vi = RowShardedVI(backend, n, None, force_collectives=distributed)
         if args.knots:
-            # the knot bounds of the whole data set, as every rank must use them
-            rng = P["X"].max(axis=0) - P["X"].min(axis=0)
-            kb = np.stack([P["X"].min(axis=0) - rng / 10, P["X"].max(axis=0) + rng / 10], axis=1)
-
             class _KnotRunner:
                 def eval(self, theta, U, delta):
                     o, g = vi.eval(theta, U, delta)
-                    return o, (g, ctx.knot_gradient(kb))
+                    # knot bounds of the whole data set (quirk Q9), combined over the ranks
+                    return o, (g, backend.knot_gradient())
             runner = _KnotRunner()
         else:
             runner = vi
@@ -189,7 +250,7 @@ def main():
     # HIP events bracket every phase on its launch stream during the timed steps; they are read
     # back once, after the timed region
     ctx.enable_timing(True)
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -197,14 +258,14 @@ def main():
     for k in range(args.steps):
         obj, grad = runner.eval(theta_at(args.warmup + k), P["U"], P["delta"])
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     t1 = time.perf_counter()
     evals = max(ctx.timing_evals(), 1)
     phase_avg = {name: ms / evals for name, ms in ctx.timings()}
     ctx.enable_timing(False)
     elapsed = t1 - t0
-    if world > 1:
+    if distributed:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
@@ -262,11 +323,26 @@ def main():
         }
         if args.mode == "laplace":
             out["nr_iters_per_eval"] = timed_iters
-        if world == 1 and not args.no_cpu_baseline and args.mode == "vi":
-            out["cpu_baseline"] = cpu_baseline()
+        if distributed:
+            out["collectives"] = "rccl" if not rehearse else "gloo (rehearsal)"
+        if (world == 1 and not args.no_cpu_baseline and args.mode == "vi"
+                and args.config == "C3" and n == 1_000_000):
+            full = None
+            fp = os.path.join(ROOT, "profiles", "r2_cpu_baseline_full.json")
+            if os.path.exists(fp):
+                rec = json.load(open(fp))
+                full = {"source": "profiles/r2_cpu_baseline_full.json (bench.py --cpu-full on a "
+                                  "GPU box's host, committed; not re-measured by this run)",
+                        "cpu": rec["cpu"],
+                        "literal_all_cores": {k: rec["literal_all_cores"][k] for k in
+                                              ("value", "sizes", "t_s", "fit", "threads")},
+                        "literal_one_core": {k: rec["literal_one_core"][k] for k in
+                                             ("value", "sizes", "t_s", "fit", "threads")},
+                        "adjoint_direct": rec["adjoint_direct"]["value"]}
+            out["cpu_baseline"] = cpu_baseline(full=full)
         print(json.dumps(out), flush=True)
     backend.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

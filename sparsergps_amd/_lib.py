@@ -116,8 +116,14 @@ def lib(auto_build: bool = True):
     with _lock:
         if _lib is not None:
             return _lib
-        if auto_build and not os.path.exists(LIB):
-            build()
+        if auto_build:
+            # rebuilds only when a source is newer than the library (a stale .so would
+            # otherwise be loaded silently); without hipcc the existing library is used
+            try:
+                build()
+            except RuntimeError:
+                if not os.path.exists(LIB):
+                    raise
         if not os.path.exists(LIB):
             raise RuntimeError(f"libsgp.so not found at {LIB}; run sparsergps_amd._build.build()")
         h = C.CDLL(LIB, mode=C.RTLD_GLOBAL)

@@ -853,6 +853,13 @@ int sgp_knot_gradient(sgp_ctx* c, const double* bounds, double* grad_knot) {
     set_err("no knot gradient: enable it with sgp_ctx_enable_knot_grad before the evaluation");
     return SGP_EINVAL;
   }
+  if (!bounds && c->last_mode != 3 && c->n_global > c->n) {
+    // the default bounds are this context's row range, which differs between the ranks of a
+    // row-sharded evaluation: the caller must pass the bounds of the whole data set
+    set_err("row-sharded context (n_global %lld > local rows %lld): pass the global knot bounds",
+            (long long)c->n_global, (long long)c->n);
+    return SGP_EINVAL;
+  }
   std::vector<double> lb((size_t)d), ub((size_t)d);
   for (int q = 0; q < d; ++q) {
     if (bounds) {
@@ -1607,6 +1614,8 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
     c->lap_obj = o;
     c->lap_it += 1;
     c->lap_objs.push_back(o);
+    // maxit = 0 is this ABI's "evaluate at the given f" mode (sgp.h); any maxit >= 1 performs
+    // the first update before the loop as newtrap_sparseGP.R:79-96 does (iter >= 2)
     const bool go = (st_in == LS_OBJ0 && c->lap_maxit > 0) ||
                     (c->lap_it < c->lap_maxit &&
                      (fabs(c->lap_obj - c->lap_obj_prev) > c->lap_tol || c->lap_cnt > 0.0));

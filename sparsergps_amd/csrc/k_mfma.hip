@@ -130,8 +130,16 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
   const int64_t noff = (int64_t)nb * (nb - 1) / 2;
   const int dg = (gi >= noff) ? (int)(gi - noff) : -1;
   constexpr bool with_t = WITH_T;
-  const int tmap = with_t ? (int)tm.e[gi] : -1;
-  const int tS = with_t ? tm.S : 1, tW = T128 / tS;
+  // tm.S == 0 (more groups than the table holds, m > 1920): one whole-panel slice per panel,
+  // panel a >= 1 on the strictly-lower group (a, 0) and panel 0 on diagonal group 0 -- distinct
+  // groups, each holding its panel as image A
+  int tmap = -1;
+  if (with_t) {
+    if (tm.S > 0) tmap = (int)tm.e[gi];
+    else if (gi < noff) tmap = (tb == 0) ? ta : -1;
+    else if (dg == 0) tmap = 0;
+  }
+  const int tS = (with_t && tm.S > 0) ? tm.S : 1, tW = T128 / tS;
   const int tpan = tmap >= 0 ? tmap / tS : -1;
   // all 256 threads share the slice: column tid % tW, rows trg, trg + tng, ... of each step
   const int tng = 256 / tW, trg = tid / tW;
@@ -1216,11 +1224,14 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
     SyrkTMap tm{};
     tm.S = 1;
     if ((part & 1) && with_t) {
-      if (q.T > 128) return hipErrorInvalidValue;
-      int tmap[128];
-      tm.S = syrk_t_table(q.nb, q.T, tmap);
-      if (tm.S == 0) return hipErrorInvalidValue;
-      for (int gi = 0; gi < q.T; ++gi) tm.e[gi] = (signed char)tmap[gi];
+      // the balanced slice table when the groups fit it; otherwise tm.S = 0 selects the
+      // one-slice-per-panel rule inside the kernel (k_syrk_blk)
+      tm.S = 0;
+      if (q.T <= 128) {
+        int tmap[128];
+        tm.S = syrk_t_table(q.nb, q.T, tmap);
+        for (int gi = 0; gi < q.T; ++gi) tm.e[gi] = (signed char)(tm.S > 0 ? tmap[gi] : -1);
+      }
     }
     if (part & 1) {
       if (with_t && w)

@@ -15,8 +15,15 @@ tests (tests/test_dist.py).
 from __future__ import annotations
 
 import contextlib
+import os
 
 import numpy as np
+
+
+def _force_default():
+    """SGP_FORCE_COLLECTIVES=1: issue the all-reduces even at world size 1, so that a one-GPU
+    run exercises the RCCL path (stream ordering included) exactly as an 8-GPU run does."""
+    return os.environ.get("SGP_FORCE_COLLECTIVES") == "1"
 
 
 def shard_rows(n, world, rank):
@@ -25,6 +32,24 @@ def shard_rows(n, world, rank):
     start = rank * base + min(rank, extra)
     stop = start + base + (1 if rank < extra else 0)
     return start, stop
+
+
+def global_knot_bounds(X_local, group=None):
+    """d x 2 [lower, upper] knot bounds over all ranks' rows: column range widened by a tenth
+    on each side (vi_functions.R:175-178); one MIN and one MAX all-reduce when distributed."""
+    import torch
+    import torch.distributed as dist
+    X_local = np.asarray(X_local, dtype=np.float64)
+    lo = torch.from_numpy(X_local.min(axis=0).copy())
+    hi = torch.from_numpy(X_local.max(axis=0).copy())
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        if dist.get_backend(group) == "nccl":
+            lo, hi = lo.cuda(), hi.cuda()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    lo, hi = lo.cpu().numpy(), hi.cpu().numpy()
+    diff = hi - lo
+    return np.column_stack([lo - diff / 10, hi + diff / 10])
 
 
 class HipRowBackend:
@@ -56,6 +81,9 @@ class HipRowBackend:
             self.ctx.enable_knot_grad(True)
             n2 += self.ctx.knot_red_extra(m_max)
         self.knots = knots
+        # knot bounds of the whole data set (quirk Q9, vi_functions.R:175-178): every rank
+        # must use the same ones, so the per-rank column ranges are combined once here
+        self.knot_bounds = global_knot_bounds(X_local) if knots else None
         self.red1 = torch.zeros(n1, dtype=torch.float64, device=self.dev)
         self.red2 = torch.zeros(n2, dtype=torch.float64, device=self.dev)
         # A dedicated (non-null) stream shared by libsgp's launches and torch.distributed:
@@ -108,32 +136,43 @@ class HipRowBackend:
             return None, True, (obj, grad, it)
         return dst[:cnt], False, None
 
+    def knot_gradient(self, bounds=None):
+        """Row-major m*d knot gradient of the last evaluation (global bounds by default)."""
+        return self.ctx.knot_gradient(self.knot_bounds if bounds is None else bounds)
+
     def close(self):
         self.ctx.close()
 
 
 class RowShardedVI:
-    """ELBO + gradient over row blocks held by the ranks of `group`."""
+    """ELBO + gradient over row blocks held by the ranks of `group`.
 
-    def __init__(self, backend, n_global, group=None):
+    force_collectives: all-reduce even when the group has one rank (default: the
+    SGP_FORCE_COLLECTIVES environment switch); a single rank otherwise skips them."""
+
+    def __init__(self, backend, n_global, group=None, force_collectives=None):
         import torch.distributed as dist
         self.dist = dist
         self.backend = backend
         self.n_global = int(n_global)
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        force = _force_default() if force_collectives is None else bool(force_collectives)
+        if force and not dist.is_initialized():
+            raise RuntimeError("force_collectives needs an initialised torch.distributed group")
+        self.collective = self.world > 1 or force
 
     def eval(self, theta, U, delta=1e-6):
         b = self.backend
-        # the torch stream context orders the collectives after libsgp's kernels; one rank
-        # issues no collective and skips it
-        use_ctx = self.world > 1 and hasattr(b, "stream_context")
+        # the torch stream context orders the collectives after libsgp's kernels (and the next
+        # phase's kernels after the collective), with no host synchronisation in between
+        use_ctx = self.collective and hasattr(b, "stream_context")
         with (b.stream_context() if use_ctx else contextlib.nullcontext()):
             red1 = b.phase1(theta, U, delta)
-            if self.world > 1:
+            if self.collective:
                 self.dist.all_reduce(red1, group=self.group)
             red2 = b.phase2(red1, self.n_global)
-            if self.world > 1:
+            if self.collective:
                 self.dist.all_reduce(red2, group=self.group)
             return b.finish(red2)
 
@@ -147,12 +186,16 @@ class RowShardedLaplace:
     decision is a function of summed buffers, so all ranks iterate identically.
     """
 
-    def __init__(self, backend, group=None):
+    def __init__(self, backend, group=None, force_collectives=None):
         import torch.distributed as dist
         self.dist = dist
         self.backend = backend
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        force = _force_default() if force_collectives is None else bool(force_collectives)
+        if force and not dist.is_initialized():
+            raise RuntimeError("force_collectives needs an initialised torch.distributed group")
+        self.collective = self.world > 1 or force
 
     def eval(self, theta, U, delta=1e-6, expo=1.0, tol=1e-5, maxit=1000):
         """-> (objective, gradient d/dlog theta, NR iteration count)"""
@@ -160,7 +203,7 @@ class RowShardedLaplace:
         with (b.stream_context() if hasattr(b, "stream_context") else contextlib.nullcontext()):
             red = b.lap_begin(theta, U, delta, expo, tol, maxit)
             while True:
-                if self.world > 1:
+                if self.collective:
                     self.dist.all_reduce(red, group=self.group)
                 red, done, res = b.lap_step(red)
                 if done:

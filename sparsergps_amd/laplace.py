@@ -43,6 +43,12 @@ def laplace_eval(cov_par, cov_fun, xu, xy, y, mu, ff=None, m=1.0, delta=1e-6, to
     """NR to the Laplace mode from `ff` (or the context's resident mode when ff is None), then
     dlogq_dcov_par there.  Returns dict(objective, gradient (names(cov_par) order), gp,
     objective_function_values, nr_iter)."""
+    # newtrap_sparseGP.R:79-96 runs the first update whatever maxit is
+    return _eval(cov_par, cov_fun, xu, xy, y, mu, ff, m, delta, tol, max(int(maxit), 1), ctx)
+
+
+def _eval(cov_par, cov_fun, xu, xy, y, mu, ff, m, delta, tol, maxit, ctx):
+    """laplace_eval with the C ABI's maxit as given (0 = objective and gradient at f, no NR)."""
     theta, names, xu_m = _prep(cov_par, cov_fun, xu, xy)
     muv = _mu_vec(mu, y)
     if ctx is None:
@@ -75,7 +81,7 @@ def newtrap_sparseGP(start_vals, cov_par, cov_fun, xy, xu, y, mu, m=1.0, delta=1
     ctx, theta, xu_m = _lap_ctx(cov_par, cov_fun, xu, xy, y, mu, ctx)
     if start_vals is not None:
         ctx.lap_set_f(start_vals)
-    ctx.lap_nr(theta, cov_fun, xu_m, delta, m, tol, maxit)
+    ctx.lap_nr(theta, cov_fun, xu_m, delta, m, tol, max(int(maxit), 1))   # first update always
     return {"gp": ctx.lap_get_f(), "objective_function_values": ctx.lap_objective_values()}
 
 
@@ -91,7 +97,7 @@ def dlogq_dcov_par(cov_par, cov_fun, dcov_fun_dtheta=True, dcov_fun_dknot=None, 
         ctx = _context_for(xy, y, mu, xu_m.shape[0], muv)
         ctx.set_data(y, muv)
     ctx.enable_knot_grad(kind is not None)
-    r = laplace_eval(cov_par, cov_fun, xu, xy, y, mu, ff, m, delta, 0.0, 0, ctx)
+    r = _eval(cov_par, cov_fun, xu, xy, y, mu, ff, m, delta, 0.0, 0, ctx)   # no NR step
     grad = r["gradient"] if dcov_fun_dtheta else 0
     trans_par = OrderedDict((k, float(np.log(v))) for k, v in cov_par.items())
     if kind is not None:

@@ -356,16 +356,26 @@ class SparseGPContext:
 _CTX_CACHE = {}
 
 
+def _fingerprint(a):
+    """Shape plus a strided sample of the values: a cheap guard against arrays mutated in
+    place between calls (the context holds a device copy taken at creation)."""
+    a = np.asarray(a, dtype=np.float64).reshape(-1)
+    step = max(1, a.size // 4096)
+    return (a.size, float(np.sum(a[::step])), float(a[-1]) if a.size else 0.0)
+
+
 def _context_for(xy, y, mu, m, mu_vec=None):
-    """Reuse one device context per (xy, y, mu) triple, like the reference driver reuses xy.
-    mu_vec: the mean actually uploaded when mu is a default marker (None)."""
-    key = (id(xy), id(y), id(mu))
+    """Reuse one device context per (xy, y, mu), like the reference driver reuses xy across
+    iterations.  Arrays are keyed by identity plus a sampled fingerprint; a scalar mu (the
+    mean(y) default, quirk Q14) is keyed by value.  mu_vec: the mean actually uploaded."""
+    mu_key = ("scalar", float(mu)) if np.ndim(mu) == 0 else ("array", id(mu), _fingerprint(mu))
+    key = (id(xy), id(y), mu_key, _fingerprint(xy), _fingerprint(y))
     ent = _CTX_CACHE.get(key)
-    if ent is not None and ent[0] is xy and ent[1] is y and ent[2] is mu and ent[3].m_max >= m:
-        return ent[3]
+    if ent is not None and ent[0] is xy and ent[1] is y and ent[2].m_max >= m:
+        return ent[2]
     ctx = SparseGPContext(xy, y, mu if mu_vec is None else mu_vec, m_max=m)
     _CTX_CACHE.clear()
-    _CTX_CACHE[key] = (xy, y, mu, ctx)
+    _CTX_CACHE[key] = (xy, y, ctx)
     return ctx
 
 

@@ -220,3 +220,53 @@ def test_laplace_high_dim(sgp):
     ov = nr["objective_function_values"]
     assert r["nr_iter"] == len(ov)
     _close(r["objective"], r["gradient"], ov[-1], g, cp)
+
+
+@pytest.mark.parametrize("mode", ["vi", "fitc", "laplace"])
+def test_knots_past_the_syrk_table(sgp, mode):
+    """m = 2048 (nb = 16: 136 packed SYRK groups per row chunk, more than the balanced t-slice
+    table holds, so the weighted SYRK with t -- FITC phase 1, the Laplace objective pass --
+    takes the one-slice-per-panel placement).  Gaussian objectives against the adjoint model
+    (R's det() underflows here, quirk Q4), gradients against the literal oracle."""
+    from oracle import adjoint_ref as A
+    if mode == "laplace":
+        P = O.make_poisson_problem(n=700, m=2048)
+        cp = P["cov_par"]
+        nr = O.newtrap_sparseGP(P["f0"], cp, "sqexp", P["X"], P["U"], P["y"], P["mu"], P["a"],
+                                P["delta"], tol=1e-5)
+        g = O.dlogq_dcov_par(cp, "sqexp", P["U"], P["X"], P["y"], nr["gp"], P["mu"], P["a"],
+                             P["delta"])["gradient"]
+        r = sgp.laplace_eval(cp, "sqexp", P["U"], P["X"], P["y"], P["mu"], P["f0"], P["a"],
+                             P["delta"], tol=1e-5)
+        ov = nr["objective_function_values"]
+        assert r["nr_iter"] == len(ov)
+        _close(r["objective"], r["gradient"], ov[-1], g, cp)
+        return
+    P = O.make_gaussian_problem("C3", n=700, m=2048)
+    cp = P["cov_par"]
+    theta = np.array(list(cp.values()))
+    if mode == "vi":
+        obj, grad = sgp.vi_eval(cp, "ard", P["U"], P["X"], P["y"], P["mu"], P["delta"])
+        o, _ = A.eval_vi("ard", theta, P["X"], P["y"], P["mu"], P["U"], P["delta"])
+        g = O.delbo_dcov_par(cp, "ard", P["U"], P["X"], P["y"], P["mu"], P["delta"])["gradient"]
+    else:
+        obj, grad = sgp.fitc_eval(cp, "ard", P["U"], P["X"], P["y"], P["mu"], P["delta"])
+        o, _ = A.eval_fitc("ard", theta, P["X"], P["y"], P["mu"], P["U"], P["delta"])
+        g = O.dlogp_dcov_par(cp, "ard", P["U"], P["X"], P["y"], P["mu"], P["delta"])["gradient"]
+    _close(obj, grad, o, g, cp)
+
+
+@pytest.mark.parametrize("maxit", [0, 1, 2, 3])
+def test_newtrap_small_maxit(sgp, maxit):
+    """newtrap_sparseGP.R:79-96 performs the first update before its while loop whatever maxit
+    is: maxit <= 2 returns two objective values, maxit = 3 at most three."""
+    P = O.make_poisson_problem(n=400, m=30)
+    cp = P["cov_par"]
+    nr = O.newtrap_sparseGP(P["f0"], cp, "sqexp", P["X"], P["U"], P["y"], P["mu"], P["a"],
+                            P["delta"], maxit=maxit, tol=1e-6)
+    r = sgp.newtrap_sparseGP(P["f0"], cp, "sqexp", P["X"], P["U"], P["y"], P["mu"], P["a"],
+                             P["delta"], maxit=maxit, tol=1e-6)
+    ov, rv = nr["objective_function_values"], np.asarray(r["objective_function_values"])
+    assert len(rv) == len(ov) == (2 if maxit <= 2 else 3)
+    assert np.max(np.abs(rv - ov) / np.abs(ov)) < 1e-9
+    assert np.max(np.abs(r["gp"] - nr["gp"])) < 1e-8
