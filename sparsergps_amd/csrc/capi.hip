@@ -160,12 +160,6 @@ struct sgp_ctx {
   hipStream_t aux_lo = nullptr;           // ... at normal priority (the Bm chain keeps its CUs)
   double* slab_aux = nullptr;             // partials of the aux stream's small reductions
   // launch-bound Bm factorisation captured once per (mp, S pointer) and replayed
-  hipGraphExec_t g_bm = nullptr, g_k22 = nullptr;
-  hipGraph_t g_bm_graph = nullptr, g_k22_graph = nullptr;
-  int64_t g_bm_mp = -1, g_k22_mp = -1;
-  const double* g_bm_S = nullptr;
-  double g_bm_sscale = 0.0;
-  bool use_graphs = false;  // opt-in (SGP_GRAPHS=1): replay faulted in one configuration
   // Poisson-Laplace state (row/knot vectors allocated on first use)
   double *y = nullptr, *mu = nullptr;     // per-row data (n_pad), kept for the Laplace path
   double* lv = nullptr;                   // LV_N x n_pad row vectors
@@ -309,10 +303,6 @@ void ctx_free(sgp_ctx* c) {
   if (c->khash) hipFree(c->khash);
   if (c->kidx) hipFree(c->kidx);
   if (c->cflag) hipFree(c->cflag);
-  if (c->g_bm) hipGraphExecDestroy(c->g_bm);
-  if (c->g_bm_graph) hipGraphDestroy(c->g_bm_graph);
-  if (c->g_k22) hipGraphExecDestroy(c->g_k22);
-  if (c->g_k22_graph) hipGraphDestroy(c->g_k22_graph);
   if (c->ev_knots) hipEventDestroy(c->ev_knots);
   if (c->ev_pin) hipEventDestroy(c->ev_pin);
   if (c->pin) hipHostFree(c->pin);
@@ -586,7 +576,6 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
     delete c;
     return SGP_EHIP;
   }
-  if (getenv("SGP_GRAPHS") && !getenv("SGP_NO_GRAPHS")) c->use_graphs = true;
   c->slab_syrk_cap = syrk_slab_doubles(np_, mp);
   c->slab_con_cap = (np_ / SGP_TILE) * (mp / SGP_TILE) * (SGP_MAXD + 5);   // nrec <= L + 5
   st = st ? st : dalloc(&c->X, np_ * d);
@@ -941,39 +930,6 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   return SGP_OK;
 }
 
-typedef int (*launch_seq_fn)(sgp_ctx*, hipStream_t);
-
-// Replay `fn`'s launches from a hipGraph captured once per shape (all kernel arguments are
-// context pointers, so the graph stays valid); falls back to direct launches if capture fails.
-static int run_graph(sgp_ctx* c, hipStream_t s, launch_seq_fn fn, hipGraphExec_t* exec,
-                     hipGraph_t* graph, int64_t* key) {
-  if (c->use_graphs) {
-    if (!*exec || *key != c->mp) {
-      if (*exec) { (void)hipGraphExecDestroy(*exec); *exec = nullptr; }
-      if (*graph) { (void)hipGraphDestroy(*graph); *graph = nullptr; }
-      bool ok = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess;
-      const int st = ok ? fn(c, s) : SGP_EHIP;
-      hipGraph_t g = nullptr;
-      ok = (hipStreamEndCapture(s, &g) == hipSuccess) && ok && st == SGP_OK && g;
-      if (ok) ok = hipGraphInstantiate(exec, g, nullptr, nullptr, 0) == hipSuccess;
-      if (!ok) {
-        if (g) (void)hipGraphDestroy(g);
-        *exec = nullptr;
-        c->use_graphs = false;
-        (void)hipGetLastError();
-      } else {
-        *graph = g;
-        *key = c->mp;
-      }
-    }
-    if (*exec) {
-      HIPCHK(hipGraphLaunch(*exec, s));
-      return SGP_OK;
-    }
-  }
-  return fn(c, s);
-}
-
 static int k22_factor_launches(sgp_ctx* c, hipStream_t s) {
   const int64_t mp = c->mp;
   HIPCHK(hipMemcpyAsync(c->K22inv, c->K22, sizeof(double) * mp * mp, hipMemcpyDeviceToDevice, s));
@@ -1011,7 +967,7 @@ static int k22_factor(sgp_ctx* c, bool after_main = false) {
     HIPCHK(hipStreamWaitEvent(c->aux, c->ev_s, 0));
   }
   Scope t(c, "k22_aux", c->aux);
-  int st = run_graph(c, c->aux, k22_factor_launches, &c->g_k22, &c->g_k22_graph, &c->g_k22_mp);
+  int st = k22_factor_launches(c, c->aux);
   if (st) return st;
   HIPCHK(hipEventRecord(c->ev_k22, c->aux));
   return SGP_OK;
@@ -1022,8 +978,7 @@ static int k22_launch(sgp_ctx* c, double diag_sub) {
   return st ? st : k22_factor(c, false);
 }
 
-// Binv (holding K22 + S * s_scale) inverted in place: 48 small launches, captured into a
-// hipGraph once per shape and replayed.
+// Binv (holding K22 + S * s_scale) inverted in place (one Gauss-Jordan launch per pivot).
 static int bm_factor_launches(sgp_ctx* c, hipStream_t s) {
   const int64_t mp = c->mp;
   HIPCHK(dense_spd_inverse(c->Binv, mp, c->Xt, c->T1, c->dinv, c->logdB, c->status + 1, s));
@@ -1036,7 +991,7 @@ static int bm_stage(sgp_ctx* c, const double* S, double s_scale) {
   Scope t(c, "dense_bm");
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22m, 0));   // Bm needs K22, not its inverse
   HIPCHK(dense_axpby(1.0, c->K22, s_scale, S, c->Binv, mm, c->stream));
-  return run_graph(c, c->stream, bm_factor_launches, &c->g_bm, &c->g_bm_graph, &c->g_bm_mp);
+  return bm_factor_launches(c, c->stream);
 }
 
 int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned flags,
@@ -1616,6 +1571,9 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
     c->lap_objs.push_back(o);
     // maxit = 0 is this ABI's "evaluate at the given f" mode (sgp.h); any maxit >= 1 performs
     // the first update before the loop as newtrap_sparseGP.R:79-96 does (iter >= 2)
+    // maxit = 0 is the C ABI's "objective and gradient at the given f" mode (dlogq_dcov_par);
+    // every reference-facing caller passes maxit >= 1, so the first update always runs there,
+    // as newtrap_sparseGP.R:79-96 run it before the loop whatever maxit is
     const bool go = (st_in == LS_OBJ0 && c->lap_maxit > 0) ||
                     (c->lap_it < c->lap_maxit &&
                      (fabs(c->lap_obj - c->lap_obj_prev) > c->lap_tol || c->lap_cnt > 0.0));

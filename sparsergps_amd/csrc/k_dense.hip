@@ -1,12 +1,11 @@
 // m x m dense algebra and row reductions for the sparse-GP evaluation on gfx950.
 //
 // The reference calls base-R chol()/solve() (LAPACK dpotrf/dgesv) on the m x m matrices
-// Sigma22 and Sigma22 + t(Sigma12) %*% (B * Sigma12) (R/vi_functions.R:96, 231, 239).  Here:
-//   dense_potrf  right-looking blocked Cholesky, 64-wide panels: the 64x64 diagonal block is
-//                factored (and inverted) in LDS by one workgroup, the panel solve and the
-//                trailing SYRK are f64-MFMA GEMMs (k_gemm64 in k_mfma.hip);
-//   dense_trtri  blocked triangular inverse by block rows (two GEMMs per block row);
-//   X^T X        gives the SPD inverse.
+// Sigma22 and Sigma22 + t(Sigma12) %*% (B * Sigma12) (R/vi_functions.R:96, 231, 239).  Here
+// both are inverted by dense_spd_inverse: a blocked Gauss-Jordan (sweep) SPD inverse, one
+// launch per 64-wide pivot, whose trailing updates are f64 MFMA products; the pivots are the
+// Cholesky factor's squared diagonal, so log-determinants and R's chol() failure order come
+// out of the same pass.
 // Reductions are two-stage with fixed order (deterministic, run-to-run bit-identical).
 #include "sgp_internal.h"
 
@@ -28,103 +27,6 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
   for (int q = 0; q < nw; ++q) t += sh[q];
   __syncthreads();
   return t;
-}
-
-// Factor the 64x64 diagonal block kb of A and invert its factor in ONE right-looking pass.
-// Thread t owns the 4x4 register blocks (bi, bj) = (t>>4, t&15) of both L (in place of A) and
-// X = L^{-1}; column k of A and row k of X are broadcast through double-buffered LDS, so each
-// of the 64 steps costs a single barrier.  Writes L (lower) back, X to dinv, sum log(L_ii) to
-// logd[kb]; the first failing pivot sets status = global index + 1 (R's chol() error).
-__global__ void __launch_bounds__(256) k_potrf_diag(double* A, int64_t lda, int kb,
-                                                    double* __restrict__ dinv,
-                                                    double* __restrict__ logd,
-                                                    int* __restrict__ status) {
-  __shared__ double colv[2][64];
-  __shared__ double xrow[2][64];
-  __shared__ double piv_s[64];
-  __shared__ double red[4];
-  const int tid = threadIdx.x;
-  const int bi = tid >> 4, bj = tid & 15;
-  const bool lower = bi >= bj;
-  const int64_t o = (int64_t)kb * 64;
-  double a[4][4], x[4][4];
-#pragma unroll
-  for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int i = 4 * bi + ii, j = 4 * bj + jj;
-      a[ii][jj] = (lower && j <= i) ? A[(o + i) * lda + o + j] : 0.0;
-      x[ii][jj] = (i == j) ? 1.0 : 0.0;
-    }
-  for (int kb4 = 0; kb4 < 16; ++kb4) {
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int k = 4 * kb4 + kk;
-      const int b = k & 1;
-      // publish column k of A (rows >= k) and row k of X (cols <= k)
-      if (bj == kb4 && bi >= kb4) {
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) colv[b][4 * bi + ii] = a[ii][kk];
-      }
-      if (bi == kb4 && bj <= kb4) {
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) xrow[b][4 * bj + jj] = x[kk][jj];
-      }
-      __syncthreads();
-      const double p2 = colv[b][k];
-      const double piv = sqrt(p2);
-      const double rp = 1.0 / piv;
-      if (tid == 0) {
-        piv_s[k] = piv;
-        if (!(p2 > 0.0) || !isfinite(p2)) atomicCAS(status, 0, (int)(o + k + 1));
-      }
-      if (lower) {
-        double li[4], lj[4], xk[4];
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) li[ii] = colv[b][4 * bi + ii] * rp;
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          lj[jj] = colv[b][4 * bj + jj] * rp;
-          xk[jj] = xrow[b][4 * bj + jj] * rp;
-        }
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) {
-          const int i = 4 * bi + ii;
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            const int j = 4 * bj + jj;
-            if (i > k && j > k && j <= i) a[ii][jj] = fma(-li[ii], lj[jj], a[ii][jj]);
-            if (j == k && i > k) a[ii][jj] = li[ii];
-            if (j == k && i == k) a[ii][jj] = piv;
-            if (i == k && j <= k) x[ii][jj] = xk[jj];
-            if (i > k && j <= k) x[ii][jj] = fma(-li[ii], xk[jj], x[ii][jj]);
-          }
-        }
-      }
-    }
-  }
-  if (lower) {
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int i = 4 * bi + ii, j = 4 * bj + jj;
-        if (j <= i) A[(o + i) * lda + o + j] = a[ii][jj];
-      }
-  }
-  double* D = dinv + (int64_t)kb * 64 * 64;
-#pragma unroll
-  for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int i = 4 * bi + ii, j = 4 * bj + jj;
-      D[i * 64 + j] = (lower && j <= i) ? x[ii][jj] : 0.0;
-    }
-  __syncthreads();
-  double lg = (tid < 64) ? log(piv_s[tid]) : 0.0;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) lg += __shfl_xor(lg, off, 64);
-  if (tid == 0) logd[kb] = lg;
 }
 
 // ---------------------------------------------------------------- blocked Gauss-Jordan
@@ -469,11 +371,6 @@ __global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
   }
 }
 
-__global__ void __launch_bounds__(256) k_copy_block(const double* __restrict__ src,
-                                                    double* __restrict__ dst, int64_t ldd) {
-  for (int e = threadIdx.x; e < 64 * 64; e += 256) dst[(e >> 6) * ldd + (e & 63)] = src[e];
-}
-
 __global__ void __launch_bounds__(256) k_axpby(double a, const double* __restrict__ A, double b,
                                                const double* __restrict__ B,
                                                double* __restrict__ C, int64_t count) {
@@ -493,39 +390,6 @@ __global__ void __launch_bounds__(256) k_gemv(const double* __restrict__ A, int6
   for (int64_t j = lane; j < mp; j += 64) s = fma(A[row * mp + j], x[j], s);
   s = wave_sum(s);
   if (lane == 0) y[row] = scale * s;
-}
-
-// alpha_i = (r_i - K_i u) * invz ; per-block sum of alpha^2.  u staged in LDS.
-__global__ void __launch_bounds__(256) k_alpha(const double* __restrict__ K, int64_t n_pad,
-                                               int64_t mp, const double* __restrict__ r,
-                                               const double* __restrict__ u, double invz,
-                                               const double* __restrict__ invz_vec,
-                                               double* __restrict__ alpha,
-                                               double* __restrict__ slab) {
-  extern __shared__ __attribute__((aligned(16))) double su[];
-  __shared__ double sh[4];
-  for (int64_t j = threadIdx.x; j < mp; j += 256) su[j] = u[j];
-  __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  double a2 = 0.0;
-  for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < n_pad; row += (int64_t)gridDim.x * 4) {
-    const double2* Kr = reinterpret_cast<const double2*>(K + row * mp);
-    double s = 0.0;
-    for (int64_t q = lane; q < mp / 2; q += 64) {
-      const double2 kv = Kr[q];
-      s = fma(kv.x, su[2 * q], s);
-      s = fma(kv.y, su[2 * q + 1], s);
-    }
-    s = wave_sum(s);
-    const double iz = invz_vec ? invz_vec[row] : invz;
-    const double al = (r[row] - s) * iz;
-    if (lane == 0) alpha[row] = al;
-    a2 = fma(al, al, a2);
-  }
-  // every lane of a wave holds the same a2 -> take lane 0's
-  if (lane == 0) sh[w] = a2;
-  __syncthreads();
-  if (threadIdx.x == 0) slab[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
 }
 
 __global__ void __launch_bounds__(256) k_dot_partial(const double* __restrict__ a,
@@ -622,49 +486,6 @@ hipError_t launch_fitc_omega(const double* alpha, const double* w, const double*
   return hipGetLastError();
 }
 
-hipError_t dense_potrf(double* A, int64_t mp, int64_t lda, double* dinv, double* logd,
-                       int* status, hipStream_t s) {
-  const int nb = (int)(mp / SGP_DB);
-  for (int kb = 0; kb < nb; ++kb) {
-    hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(256), 0, s, A, lda, kb, dinv, logd, status);
-    const int64_t rem = mp - (int64_t)(kb + 1) * SGP_DB;
-    if (rem > 0) {
-      double* A21 = A + (int64_t)(kb + 1) * SGP_DB * lda + (int64_t)kb * SGP_DB;
-      double* A22 = A + (int64_t)(kb + 1) * SGP_DB * lda + (int64_t)(kb + 1) * SGP_DB;
-      const double* Dk = dinv + (int64_t)kb * SGP_DB * SGP_DB;
-      hipError_t e = launch_gemm64(false, true, false, rem, SGP_DB, SGP_DB, 1.0, A21, lda, Dk,
-                                   SGP_DB, 0.0, A21, lda, s);
-      if (e != hipSuccess) return e;
-      e = launch_gemm64(false, true, true, rem, rem, SGP_DB, -1.0, A21, lda, A21, lda, 1.0, A22,
-                        lda, s);
-      if (e != hipSuccess) return e;
-    }
-  }
-  return hipGetLastError();
-}
-
-hipError_t dense_trtri(const double* L, int64_t mp, int64_t lda, const double* dinv, double* X,
-                       int64_t ldx, double* T, hipStream_t s) {
-  const int nb = (int)(mp / SGP_DB);
-  hipError_t e = hipMemsetAsync(X, 0, sizeof(double) * mp * ldx, s);
-  if (e != hipSuccess) return e;
-  for (int ib = 0; ib < nb; ++ib) {
-    const double* Di = dinv + (int64_t)ib * SGP_DB * SGP_DB;
-    double* Xii = X + (int64_t)ib * SGP_DB * ldx + (int64_t)ib * SGP_DB;
-    hipLaunchKernelGGL(k_copy_block, dim3(1), dim3(256), 0, s, Di, Xii, ldx);
-    if (ib > 0) {
-      const int64_t w = (int64_t)ib * SGP_DB;
-      e = launch_gemm64(false, false, false, SGP_DB, w, w, 1.0, L + w * lda, lda, X, ldx, 0.0, T,
-                        mp, s);
-      if (e != hipSuccess) return e;
-      e = launch_gemm64(false, false, false, SGP_DB, w, SGP_DB, -1.0, Di, SGP_DB, T, mp, 0.0,
-                        X + w * ldx, ldx, s);
-      if (e != hipSuccess) return e;
-    }
-  }
-  return hipGetLastError();
-}
-
 hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* Cb, double* P,
                              double* logd, int* status, hipStream_t s) {
   // R: mp x mp ping-pong buffer; P: nb 64x64 pivot inverses (mp * 64 doubles); Cb unused.
@@ -686,10 +507,6 @@ hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* Cb, doubl
   return hipGetLastError();
 }
 
-hipError_t dense_inv_from_trtri(const double* X, int64_t mp, double* Ainv, hipStream_t s) {
-  return launch_gemm64(true, false, false, mp, mp, mp, 1.0, X, mp, X, mp, 0.0, Ainv, mp, s);
-}
-
 hipError_t dense_axpby(double a, const double* A, double b, const double* B, double* C,
                        int64_t count, hipStream_t s) {
   int nb = (int)((count + 255) / 256);
@@ -702,17 +519,6 @@ hipError_t dense_gemv(const double* A, int64_t mp, const double* x, double scale
                       hipStream_t s) {
   hipLaunchKernelGGL(k_gemv, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, s, A, mp, x, scale,
                      y);
-  return hipGetLastError();
-}
-
-hipError_t launch_alpha(const double* K, int64_t n_pad, int64_t mp, const double* r,
-                        const double* u, double invz, const double* invz_vec, double* alpha,
-                        double* slab, int* nblocks, hipStream_t s) {
-  int64_t nb = (n_pad + 3) / 4;
-  if (nb > 2048) nb = 2048;
-  *nblocks = (int)nb;
-  hipLaunchKernelGGL(k_alpha, dim3((unsigned)nb), dim3(256), sizeof(double) * mp, s, K, n_pad,
-                     mp, r, u, invz, invz_vec, alpha, slab);
   return hipGetLastError();
 }
 

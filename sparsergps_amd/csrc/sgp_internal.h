@@ -159,32 +159,17 @@ hipError_t launch_gemm64(bool transA, bool transB, bool lower_only, int64_t M, i
                          hipStream_t s);
 
 // ---------------------------------------------------------------- k_dense.hip
-// In-place blocked Cholesky of the lower triangle of A (mp x mp, mp % 64 == 0).
-// dinv receives inverse diagonal blocks (mp/64 blocks of 64x64), logd per-block sums of
-// log(L_ii); status[0] = 0 or (global pivot index + 1) of the first failing pivot.
-hipError_t dense_potrf(double* A, int64_t mp, int64_t lda, double* dinv, double* logd,
-                       int* status, hipStream_t s);
-// X = L^{-1} (lower), using the dinv blocks of dense_potrf.  X must be mp x mp.
-hipError_t dense_trtri(const double* L, int64_t mp, int64_t lda, const double* dinv, double* X,
-                       int64_t ldx, double* T, hipStream_t s);
 // In-place inverse of an SPD matrix A (mp x mp, full storage) by blocked Gauss-Jordan with
 // 64-wide pivots; logd[k] = sum log L_ii of the k-th pivot block's Cholesky factor, so
 // log det A = 2 * sum_k logd[k].  Work: R (64 x mp), Cb (mp x 64), P (64 x 64).
 hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* Cb, double* P,
                              double* logd, int* status, hipStream_t s);
-// Ainv = X^T X
-hipError_t dense_inv_from_trtri(const double* X, int64_t mp, double* Ainv, hipStream_t s);
 // C = a*A + b*B elementwise over mp x mp
 hipError_t dense_axpby(double a, const double* A, double b, const double* B, double* C,
                        int64_t count, hipStream_t s);
 // y = scale * A x  (A: mp x mp row-major)
 hipError_t dense_gemv(const double* A, int64_t mp, const double* x, double scale, double* y,
                       hipStream_t s);
-// alpha_i = (r_i - sum_j K_ij u_j) * invz_i  (invz scalar if invz_vec == nullptr),
-// writes per-block partial sum of alpha_i^2 into slab.
-hipError_t launch_alpha(const double* K, int64_t n_pad, int64_t mp, const double* r,
-                        const double* u, double invz, const double* invz_vec, double* alpha,
-                        double* slab, int* nblocks, hipStream_t s);
 // out[0] = sum_i a_i * b_i over count (b == nullptr: sum a_i); deterministic two-stage.
 hipError_t launch_dot(const double* a, const double* b, int64_t count, double* partial,
                       double* out, hipStream_t s);

@@ -5,7 +5,8 @@ The reference ships no tests or recorded outputs and cannot 
 the reference formulas -- after it has been pinned independently by tests/test_oracle.py
 (finite differences, dense n x n formulation, closed forms).  Inputs and outputs only.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py        # all fixtures
+    python tests/golden/make_golden.py own    # only the C2 (m=256) / C5 (m=512) fixtures
 """
 import os
 import sys
@@ -74,7 +75,17 @@ def fill_case(name):
     save(name, **out)
 
 
+def own_knot_counts():
+    """C2 and C5 at their own knot counts (BASELINE.json configs[1], configs[4]), reduced n."""
+    gauss_case("gauss_c2_m256.npz", "C2", 2000, 256)
+    poisson_case("poisson_c5_m512.npz", 2000, 512)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["own"]:
+        own_knot_counts()
+        sys.exit(0)
+    own_knot_counts()
     fill_case("fills.npz")
     gauss_case("gauss_c2_small.npz", "C2", 200, 16)
     gauss_case("gauss_c3_small.npz", "C3", 150, 12)

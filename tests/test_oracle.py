@@ -207,7 +207,8 @@ def test_chunked_adjoint_model_matches_literal(cfg, coinc):
 
 
 # ----------------------------------------------------------------------- golden fixtures
-@pytest.mark.parametrize("name", ["gauss_c2_small.npz", "gauss_c3_small.npz", "gauss_c2_coincident.npz"])
+@pytest.mark.parametrize("name", ["gauss_c2_small.npz", "gauss_c3_small.npz", "gauss_c2_coincident.npz",
+                                  "gauss_c2_m256.npz"])
 def test_golden_gaussian(name):
     z = np.load(os.path.join(GOLD, name))
     cp = OrderedDict(zip([str(s) for s in z["names"]], z["theta"]))
@@ -219,8 +220,9 @@ def test_golden_gaussian(name):
     assert np.allclose(list(O.dlogp_dcov_par(*args)["gradient"].values()), z["fitc_grad"], rtol=1e-11, atol=1e-11)
 
 
-def test_golden_poisson():
-    z = np.load(os.path.join(GOLD, "poisson_c5_small.npz"))
+@pytest.mark.parametrize("name", ["poisson_c5_small.npz", "poisson_c5_m512.npz"])
+def test_golden_poisson(name):
+    z = np.load(os.path.join(GOLD, name))
     cp = OrderedDict(zip([str(s) for s in z["names"]], z["theta"]))
     nr = O.newtrap_sparseGP(z["f0"], cp, "sqexp", z["X"], z["U"], z["y"], z["mu"], float(z["a"]), tol=1e-5)
     assert np.allclose(nr["gp"], z["ff"], rtol=1e-12, atol=1e-12)
