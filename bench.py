@@ -94,7 +94,11 @@ def literal_port(sizes, n_target=1_000_000, m=1024, threads=None):
     """The reference-faithful restatement (oracle/sgp_oracle.py: the R operation graph --
     LU solves with n right-hand sides, per-parameter GEMM chains -- on numpy + OpenBLAS) timed
     at C3 row counts; its cost is a + b n at fixed m, so it is fitted and extrapolated to n."""
-    ts = [_time_literal(ns, m, threads) for ns in sizes]
+    ts = []
+    for ns in sizes:
+        ts.append(_time_literal(ns, m, threads))
+        print(f"[cpu] literal port n={ns} threads={threads or _blas_threads()}: {ts[-1]:.2f} s",
+              file=sys.stderr, flush=True)
     a, b, rel, t_target = _fit(sizes, ts, n_target)
     return {"value": 1.0 / t_target, "unit": "evals/s", "sizes": list(sizes),
             "t_s": [round(t, 3) for t in ts], "fit": {"a_s": a, "b_s_per_row": b,
