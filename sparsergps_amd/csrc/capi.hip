@@ -88,6 +88,15 @@ int make_params(int kernel, int d, const double* theta, double delta, KernParams
   return SGP_OK;
 }
 
+// kp->ctr = column means of the m x d knot matrix U (column-major, ld ldu; host memory)
+void set_center(KernParams* kp, const double* U, int64_t m, int64_t ldu) {
+  for (int c = 0; c < kp->d; ++c) {
+    double s = 0.0;
+    for (int64_t j = 0; j < m; ++j) s += U[j + c * ldu];
+    kp->ctr[c] = m > 0 ? s / (double)m : 0.0;
+  }
+}
+
 struct Timer {
   std::string name;
   hipEvent_t a, b;
@@ -399,6 +408,7 @@ int check_eval_args(sgp_ctx* c, int kernel, const double* theta, const double* U
     set_err("sigma and tau must be positive");
     return SGP_EINVAL;
   }
+  set_center(kp, U, m, ldu);
   return SGP_OK;
 }
 
@@ -899,12 +909,13 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   st = k22_sync(c);
   if (st) return st;
   const int64_t mpv = c->mp, mmv = mpv * mpv;
+  int64_t t_rows = 0;
   {
     // K12, and t = K^T r riding along in the memory-bound builder (keeps the SYRK's
     // diagonal tiles as cheap as the others)
     Scope t(c, "build_knm");
     HIPCHK(launch_build_knm_t(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, mpv, m, mpv, c->K, c->r,
-                              c->tslab, c->stream, false));
+                              c->tslab, &t_rows, c->stream, false));
   }
   // K22 itself only (aux); its inverse runs in phase 2 beside the Bm inverse -- nothing in
   // phase 1 needs it, and the latency-bound chain no longer gates the one-round SYRK or shares
@@ -912,7 +923,7 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   st = k22_build(c, kp.tau2);
   if (st) return st;
   HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_vi_red1_count(m), c->stream));
-  HIPCHK(launch_knot_reduce(c->tslab, c->n_pad / 64, mpv, 1, c->T1, c->mp_max * c->mp_max,
+  HIPCHK(launch_knot_reduce(c->tslab, t_rows, mpv, 1, c->T1, c->mp_max * c->mp_max,
                             red1 + mmv, false,
                             c->stream));
   HIPCHK(launch_dot(c->r, c->r, c->n_pad, c->slab_small, red1 + mmv + mpv, c->stream));
@@ -1939,6 +1950,7 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
     set_err("invalid sgp_predict arguments");
     return SGP_EINVAL;
   }
+  set_center(&kp, U, m, ldu);
   if (method != SGP_PRED_VI && method != SGP_PRED_LAPLACE && method != SGP_PRED_FULL) {
     set_err("invalid prediction method %d", method);
     return SGP_EINVAL;

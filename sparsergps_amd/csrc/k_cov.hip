@@ -205,6 +205,114 @@ __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* 
   }
 }
 
+// K12 row-major (n_pad x mp) on the matrix cores, d <= 8, sqexp / ARD.
+// The exponent -1/2 |x~ - u~|^2 (x~ = (x - ctr) / l per coordinate, ctr = the knots' mean) is
+// one GEMM with inner dimension 12 over augmented coordinates
+//   A_i = [x~_i (8), -|x~_i|^2 / 2, 1, 0, 0]    B_j = [u~_j (8), 1, -|u~_j|^2 / 2, 0, 0]
+// i.e. three v_mfma_f64_16x16x4_f64 per 16 x 16 tile, so the VALU only evaluates exp (the
+// per-pair coordinate differences of k_build_knm cost ~40 % of its VALU work, which then
+// matched the store time).  The expansion's rounding is ~1e-16 (|x~|^2 + |u~|^2) absolute in the
+// exponent -- ~1e-14 relative in K at the configs' scales, centring keeps it there for data far
+// from the origin.  Block: 4 waves x 16 rows of a 64-row block, 128 knots; tile 2p (2p+1) holds
+// knots j0 + 32p + 2 l' (+1) in MFMA column l' = lane & 15, so each lane stores its two adjacent
+// knots as one 16-byte store (lanes 0-15: 256 contiguous bytes of one row).  Persistent over
+// row blocks rb0 + blockIdx.y + k gridDim.y; with t, the workgroup's t = K^T r partial over all
+// its row blocks goes to slot slot0 + blockIdx.y of tslab (fixed order: deterministic).
+template <bool WITH_T>
+__global__ void __launch_bounds__(256) k_build_knm_mfma(KernParams kp, const double* __restrict__ X,
+                                                        int64_t ldx, int64_t n,
+                                                        const double* __restrict__ U, int64_t ldu,
+                                                        int64_t m, int64_t mp,
+                                                        double* __restrict__ K,
+                                                        const double* __restrict__ rvec,
+                                                        double* __restrict__ tslab, int64_t slot0,
+                                                        int64_t rb0, int64_t rb1) {
+  __shared__ double tsh[WITH_T ? 4 : 1][128];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ln = lane & 15, lq = lane >> 4;
+  const int d = kp.d;
+  const int c0 = lq, c1 = 4 + lq;               // the two coordinates this lane feeds
+  const bool f0 = c0 < d, f1 = c1 < d;
+  const double ct0 = f0 ? kp.ctr[c0] : 0.0, ct1 = f1 ? kp.ctr[c1] : 0.0;
+  const double rl0 = f0 ? kp.rl[c0] : 0.0, rl1 = f1 ? kp.rl[c1] : 0.0;
+  const int64_t j0 = (int64_t)blockIdx.x * 128;
+  double b0[8], b1[8], b2[8];
+  bool jv[8];
+#pragma unroll
+  for (int tt = 0; tt < 8; ++tt) {
+    const int64_t j = j0 + 32 * (tt >> 1) + 2 * ln + (tt & 1);
+    jv[tt] = j < m;
+    const double u0 = (jv[tt] && f0) ? (U[j + c0 * ldu] - ct0) * rl0 : 0.0;
+    const double u1 = (jv[tt] && f1) ? (U[j + c1 * ldu] - ct1) * rl1 : 0.0;
+    double u2 = fma(u0, u0, u1 * u1);
+    u2 += __shfl_xor(u2, 16, 64);
+    u2 += __shfl_xor(u2, 32, 64);
+    b0[tt] = u0;
+    b1[tt] = u1;
+    b2[tt] = lq == 0 ? 1.0 : (lq == 1 ? -0.5 * u2 : 0.0);
+  }
+  const double sig2 = kp.sig2;
+  double tacc[8];
+#pragma unroll
+  for (int tt = 0; tt < 8; ++tt) tacc[tt] = 0.0;
+  typedef double nt2 __attribute__((ext_vector_type(2)));
+  for (int64_t rb = rb0 + blockIdx.y; rb < rb1; rb += gridDim.y) {
+    const int64_t ib = rb * 64 + 16 * w;
+    const int64_t ia = ib + ln;                 // this lane's A row (X is zero-padded to n_pad)
+    const double a0 = f0 ? (X[ia + c0 * ldx] - ct0) * rl0 : 0.0;
+    const double a1 = f1 ? (X[ia + c1 * ldx] - ct1) * rl1 : 0.0;
+    double x2 = fma(a0, a0, a1 * a1);
+    x2 += __shfl_xor(x2, 16, 64);
+    x2 += __shfl_xor(x2, 32, 64);
+    const double a2 = lq == 0 ? -0.5 * x2 : (lq == 1 ? 1.0 : 0.0);
+    bool iv[4];
+    double rr[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t i = ib + lq + 4 * r;
+      iv[r] = i < n;
+      rr[r] = WITH_T ? rvec[i] : 0.0;
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const d4 z = {0.0, 0.0, 0.0, 0.0};
+      d4 e0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0[2 * p], z, 0, 0, 0);
+      d4 e1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0[2 * p + 1], z, 0, 0, 0);
+      e0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1[2 * p], e0, 0, 0, 0);
+      e1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1[2 * p + 1], e1, 0, 0, 0);
+      e0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2[2 * p], e0, 0, 0, 0);
+      e1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2[2 * p + 1], e1, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double v0 = (iv[r] && jv[2 * p]) ? sig2 * sgp_exp_nonpos(fmin(e0[r], 0.0)) : 0.0;
+        const double v1 = (iv[r] && jv[2 * p + 1]) ? sig2 * sgp_exp_nonpos(fmin(e1[r], 0.0)) : 0.0;
+        const int64_t i = ib + lq + 4 * r;
+        __builtin_nontemporal_store(nt2{v0, v1},
+                                    reinterpret_cast<nt2*>(&K[i * mp + j0 + 32 * p + 2 * ln]));
+        if (WITH_T) {
+          tacc[2 * p] = fma(v0, rr[r], tacc[2 * p]);
+          tacc[2 * p + 1] = fma(v1, rr[r], tacc[2 * p + 1]);
+        }
+      }
+    }
+  }
+  if (WITH_T) {
+#pragma unroll
+    for (int tt = 0; tt < 8; ++tt) {
+      double v = tacc[tt];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lq == 0) tsh[w][32 * (tt >> 1) + 2 * ln + (tt & 1)] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 128) {
+      const int cc = threadIdx.x;
+      tslab[(slot0 + blockIdx.y) * mp + j0 + cc] =
+          ((tsh[0][cc] + tsh[1][cc]) + tsh[2][cc]) + tsh[3][cc];
+    }
+  }
+}
+
 // K22 (mp x mp, row-major) with diagonal ((sig2 + tau2 + delta) - diag_sub), identity padding.
 // K22 (symmetric mode, nugget on the diagonal).  DT = compile-time coordinate bound so the
 // knot coordinates stay in registers (a runtime-sized local array went to scratch: 108 us at
@@ -410,56 +518,84 @@ hipError_t launch_fill_dcov(const KernParams& kp, const double* x, int64_t n, in
   return hipGetLastError();
 }
 
-// One builder launch over row blocks [rb0, rb1) with at most wpc workgroups per CU.
+// One builder launch over row blocks [rb0, rb1) with at most wpc workgroups per CU.  t
+// partials (rvec != nullptr) go to tslab rows [slot0, slot0 + *slots): one per workgroup row
+// for the matrix-core builder, one per row block for the VALU builder (d > 8).
 static hipError_t build_knm_range(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
                                   const double* U, int64_t ldu, int64_t m, int64_t mp, double* K,
-                                  const double* r, double* tslab, int64_t rb0, int64_t rb1,
-                                  int wpc, hipStream_t s) {
-  static int cus = 0;
+                                  const double* r, double* tslab, int64_t slot0, int64_t* slots,
+                                  int64_t rb0, int64_t rb1, int wpc, hipStream_t s) {
+  static int cus = 0, occ_t = 0, occ_n = 0;
   if (cus == 0) {
     int dev = 0;
     hipDeviceProp_t prop;
     cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
               ? prop.multiProcessorCount : 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_t, k_build_knm_mfma<true>, 256, 0) !=
+            hipSuccess || occ_t < 1)
+      occ_t = 2;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_n, k_build_knm_mfma<false>, 256, 0) !=
+            hipSuccess || occ_n < 1)
+      occ_n = 2;
   }
+  if (slots) *slots = 0;
   if (rb1 <= rb0) return hipSuccess;
+  if (kp.kernel == 2) return hipErrorInvalidValue;
   const int64_t ncb = mp / 128;   // 128 knot columns per block
+  const bool ard = kp.kernel == 1;
+  if (kp.d <= 8) {
+    // persistent: one residency round of workgroups, each walking its share of row blocks
+    const int occ = r ? occ_t : occ_n;
+    const int per_cu = wpc < occ ? wpc : occ;
+    int64_t gy = ((int64_t)cus * per_cu) / (ncb > 0 ? ncb : 1);
+    gy = gy < 1 ? 1 : (gy > rb1 - rb0 ? rb1 - rb0 : gy);
+    dim3 grid((unsigned)ncb, (unsigned)gy);
+    if (r)
+      hipLaunchKernelGGL(k_build_knm_mfma<true>, grid, dim3(256), 0, s, kp, X, ldx, n, U, ldu, m,
+                         mp, K, r, tslab, slot0, rb0, rb1);
+    else
+      hipLaunchKernelGGL(k_build_knm_mfma<false>, grid, dim3(256), 0, s, kp, X, ldx, n, U, ldu, m,
+                         mp, K, r, tslab, slot0, rb0, rb1);
+    if (slots) *slots = gy;
+    return hipGetLastError();
+  }
   int64_t gy = ((int64_t)cus * wpc) / (ncb > 0 ? ncb : 1);
   gy = gy < 1 ? 1 : (gy > rb1 - rb0 ? rb1 - rb0 : gy);
   dim3 grid((unsigned)ncb, (unsigned)gy);
-  const bool ard = kp.kernel == 1;
-  if (kp.kernel == 2) return hipErrorInvalidValue;
-  if (kp.d <= 8) {
-    if (ard) hipLaunchKernelGGL((k_build_knm<true, 8>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, rb0, rb1);
-    else hipLaunchKernelGGL((k_build_knm<false, 8>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, rb0, rb1);
-  } else {
-    if (ard) hipLaunchKernelGGL((k_build_knm<true, SGP_MAXD>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, rb0, rb1);
-    else hipLaunchKernelGGL((k_build_knm<false, SGP_MAXD>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, rb0, rb1);
-  }
+  // the VALU builder writes one t partial per row block, at tslab row rb
+  if (r && slot0 != rb0) return hipErrorInvalidValue;
+  if (ard) hipLaunchKernelGGL((k_build_knm<true, SGP_MAXD>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, rb0, rb1);
+  else hipLaunchKernelGGL((k_build_knm<false, SGP_MAXD>), grid, dim3(64, 4), 0, s, kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, rb0, rb1);
+  if (slots) *slots = rb1 - rb0;
   return hipGetLastError();
 }
 
-// Full-occupancy builder (64 workgroups per CU is more than fit: the hardware limit applies).
+// Full-occupancy builder (more than fit: the occupancy limit applies).
 constexpr int BUILD_WPC_FULL = 64;
-// While the K22 Gauss-Jordan chain runs on the high-priority aux stream (VI/FITC phase 1), a
-// builder at full occupancy leaves no CU room for the chain's workgroups (they queue behind
-// the builder's and the SYRK then waits for the chain).  The first row blocks are therefore
-// built at BUILD_WPC_SHARED workgroups per CU, sized to last about as long as the chain, and
-// the rest at full occupancy.
+// While the K22 Gauss-Jordan chain runs on the high-priority aux stream (FITC / Laplace phase
+// 1), a builder at full occupancy leaves no CU room for the chain's workgroups (they queue
+// behind the builder's and the next pass then waits for the chain).  The first row blocks are
+// therefore built at BUILD_WPC_SHARED workgroups per CU, sized to last about as long as the
+// chain, and the rest at full occupancy.
 constexpr int BUILD_WPC_SHARED = 2;
 
 static hipError_t build_knm_impl(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
                                  int64_t n_pad, const double* U, int64_t ldu, int64_t m,
                                  int64_t mp, double* K, const double* r, double* tslab,
-                                 int64_t shared_rb, hipStream_t s) {
+                                 int64_t shared_rb, int64_t* t_rows, hipStream_t s) {
   const int64_t nrb = n_pad / 64;
   if (shared_rb > nrb) shared_rb = nrb;
   if (shared_rb < 0) shared_rb = 0;
-  hipError_t e = build_knm_range(kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, 0, shared_rb,
+  int64_t s1 = 0, s2 = 0;
+  hipError_t e = build_knm_range(kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, 0, &s1, 0, shared_rb,
                                  BUILD_WPC_SHARED, s);
   if (e != hipSuccess) return e;
-  return build_knm_range(kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, shared_rb, nrb,
-                         BUILD_WPC_FULL, s);
+  // the VALU builder's partial rows are indexed by row block
+  const int64_t slot0 = kp.d <= 8 ? s1 : shared_rb;
+  e = build_knm_range(kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, slot0, &s2, shared_rb, nrb,
+                      BUILD_WPC_FULL, s);
+  if (t_rows) *t_rows = slot0 + s2;
+  return e;
 }
 
 // Row blocks built at shared occupancy beside the K22 chain: ~60 us per 64-wide Gauss-Jordan
@@ -474,15 +610,15 @@ hipError_t launch_build_knm(const KernParams& kp, const double* X, int64_t ldx, 
                             int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
                             double* K, hipStream_t s, bool beside_chain) {
   return build_knm_impl(kp, X, ldx, n, n_pad, U, ldu, m, mp, K, nullptr, nullptr,
-                        beside_chain ? chain_shared_rb(mp) : 0, s);
+                        beside_chain ? chain_shared_rb(mp) : 0, nullptr, s);
 }
 
 hipError_t launch_build_knm_t(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
                               int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
-                              double* K, const double* r, double* tslab, hipStream_t s,
-                              bool beside_chain) {
+                              double* K, const double* r, double* tslab, int64_t* t_rows,
+                              hipStream_t s, bool beside_chain) {
   return build_knm_impl(kp, X, ldx, n, n_pad, U, ldu, m, mp, K, r, tslab,
-                        beside_chain ? chain_shared_rb(mp) : 0, s);
+                        beside_chain ? chain_shared_rb(mp) : 0, t_rows, s);
 }
 
 hipError_t launch_build_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,

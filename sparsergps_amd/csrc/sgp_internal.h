@@ -53,7 +53,11 @@ struct KernParams {
   double l[SGP_MAXD];
   double rl[SGP_MAXD];   // 1/l_c (sqexp/exp: rl[0] = 1/l)
   double rl2[SGP_MAXD];  // 1/l_c^2
+  // Origin the K12 builder's GEMM-form exponent is centred on (the knots' mean; any point
+  // gives the same K up to rounding -- centring keeps |x~|^2 + |u~|^2 small, see k_cov.hip)
+  double ctr[SGP_MAXD];
 };
+
 
 // ---------------------------------------------------------------- k_cov.hip
 // Layer-1 fillers, column-major output (R layout).  x/xp are column-major on device.
@@ -63,12 +67,12 @@ hipError_t launch_fill_cov(const KernParams& kp, const double* x, int64_t n, int
 hipError_t launch_fill_dcov(const KernParams& kp, const double* x, int64_t n, int64_t ldx,
                             const double* xp, int64_t np, int64_t ldxp, bool sym, int param,
                             double* out, int64_t ldo, hipStream_t s);
-// t partials of the builder (VI): tslab[row block of 64][j] = sum_i K_ij r_i; reduce with
-// launch_knot_reduce(tslab, n_pad / 64, mp, 1, ...).
+// t partials of the builder (VI): *t_rows rows tslab[q][j] (q < t_rows <= n_pad / 64) whose
+// column sums are t_j = sum_i K_ij r_i; reduce with launch_knot_reduce(tslab, *t_rows, mp, 1, ...).
 hipError_t launch_build_knm_t(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
                               int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
-                              double* K, const double* r, double* tslab, hipStream_t s,
-                              bool beside_chain = true);
+                              double* K, const double* r, double* tslab, int64_t* t_rows,
+                              hipStream_t s, bool beside_chain = true);
 // K12 (n_pad x mp, row-major, ld = mp).  Rows >= n and columns >= m are written as 0.
 // beside_chain: the K22 chain runs concurrently on the aux stream (phase 1), so the first row
 // blocks are built at reduced occupancy to leave it room (launch_build_knm_t always does).
