@@ -85,8 +85,27 @@ int make_params(int kernel, int d, const double* theta, double delta, KernParams
   else kp->coef = -1.0 / theta[1];
   if (kernel != SGP_KERNEL_ARD)
     for (int c = 1; c < d; ++c) { kp->l[c] = kp->l[0]; kp->rl[c] = kp->rl[0]; kp->rl2[c] = kp->rl2[0]; }
+  kp->lsig2 = log(kp->sig2);
+  set_exp_consts(kp);
   return SGP_OK;
 }
+
+}  // namespace
+
+void set_exp_consts(KernParams* kp) {
+  kp->ec[0] = 1.4426950408889634074;
+  kp->ec[1] = 6.93147180369123816490e-01;
+  kp->ec[2] = 1.90821492927058770002e-10;
+  double f = 1.0;
+  for (int q = 2; q <= 13; ++q) f *= (double)q;   // 13!
+  for (int q = 13; q >= 2; --q) {                 // ec[3] = 1/13!, ..., ec[14] = 1/2!
+    kp->ec[3 + (13 - q)] = 1.0 / f;
+    f /= (double)q;
+  }
+  kp->ec[15] = 0.0;
+}
+
+namespace {
 
 // kp->ctr = column means of the m x d knot matrix U (column-major, ld ldu; host memory)
 void set_center(KernParams* kp, const double* U, int64_t m, int64_t ldu) {

@@ -206,12 +206,13 @@ __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* 
 }
 
 // K12 row-major (n_pad x mp) on the matrix cores, d <= 8, sqexp / ARD.
-// The exponent -1/2 |x~ - u~|^2 (x~ = (x - ctr) / l per coordinate, ctr = the knots' mean) is
-// one GEMM with inner dimension 12 over augmented coordinates
-//   A_i = [x~_i (8), -|x~_i|^2 / 2, 1, 0, 0]    B_j = [u~_j (8), 1, -|u~_j|^2 / 2, 0, 0]
+// The exponent log(sig2) - 1/2 |x~ - u~|^2 (x~ = (x - ctr) / l per coordinate, ctr = the
+// knots' mean) is one GEMM with inner dimension 12 over augmented coordinates
+//   A_i = [x~_i (8), -|x~_i|^2 / 2, 1, 1, 0]    B_j = [u~_j (8), 1, -|u~_j|^2 / 2, log sig2, 0]
 // i.e. three v_mfma_f64_16x16x4_f64 per 16 x 16 tile, so the VALU only evaluates exp (the
 // per-pair coordinate differences of k_build_knm cost ~40 % of its VALU work, which then
-// matched the store time).  The expansion's rounding is ~1e-16 (|x~|^2 + |u~|^2) absolute in the
+// matched the store time); padding rows / knots carry -1e300 in the |.|^2 slot, so the clamped
+// exponent gives exactly 0 there without a select.  The expansion's rounding is ~1e-16 (|x~|^2 + |u~|^2) absolute in the
 // exponent -- ~1e-14 relative in K at the configs' scales, centring keeps it there for data far
 // from the origin.  Block: 4 waves x 16 rows of a 64-row block, 128 knots; tile 2p (2p+1) holds
 // knots j0 + 32p + 2 l' (+1) in MFMA column l' = lane & 15, so each lane stores its two adjacent
@@ -219,7 +220,7 @@ __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* 
 // row blocks rb0 + blockIdx.y + k gridDim.y; with t, the workgroup's t = K^T r partial over all
 // its row blocks goes to slot slot0 + blockIdx.y of tslab (fixed order: deterministic).
 template <bool WITH_T>
-__global__ void __launch_bounds__(256) k_build_knm_mfma(KernParams kp, const double* __restrict__ X,
+__global__ void __launch_bounds__(256, WITH_T ? 3 : 4) k_build_knm_mfma(KernParams kp, const double* __restrict__ X,
                                                         int64_t ldx, int64_t n,
                                                         const double* __restrict__ U, int64_t ldu,
                                                         int64_t m, int64_t mp,
@@ -249,9 +250,11 @@ __global__ void __launch_bounds__(256) k_build_knm_mfma(KernParams kp, const dou
     u2 += __shfl_xor(u2, 32, 64);
     b0[tt] = u0;
     b1[tt] = u1;
-    b2[tt] = lq == 0 ? 1.0 : (lq == 1 ? -0.5 * u2 : 0.0);
+    // padding knots: an exponent of -1e300 (clamped to -746 below) gives K = 0 with no
+    // per-pair select
+    b2[tt] = lq == 0 ? 1.0 : (lq == 1 ? (jv[tt] ? -0.5 * u2 : -1e300) : (lq == 2 ? kp.lsig2 : 0.0));
   }
-  const double sig2 = kp.sig2;
+  const double ehi = kp.lsig2;
   double tacc[8];
 #pragma unroll
   for (int tt = 0; tt < 8; ++tt) tacc[tt] = 0.0;
@@ -264,15 +267,11 @@ __global__ void __launch_bounds__(256) k_build_knm_mfma(KernParams kp, const dou
     double x2 = fma(a0, a0, a1 * a1);
     x2 += __shfl_xor(x2, 16, 64);
     x2 += __shfl_xor(x2, 32, 64);
-    const double a2 = lq == 0 ? -0.5 * x2 : (lq == 1 ? 1.0 : 0.0);
-    bool iv[4];
+    // exponent = x~.u~ - |x~|^2 / 2 - |u~|^2 / 2 + log(sig2); padding rows as padding knots
+    const double a2 = lq == 0 ? (ia < n ? -0.5 * x2 : -1e300) : (lq <= 2 ? 1.0 : 0.0);
     double rr[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t i = ib + lq + 4 * r;
-      iv[r] = i < n;
-      rr[r] = WITH_T ? rvec[i] : 0.0;
-    }
+    for (int r = 0; r < 4; ++r) rr[r] = WITH_T ? rvec[ib + lq + 4 * r] : 0.0;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const d4 z = {0.0, 0.0, 0.0, 0.0};
@@ -284,8 +283,10 @@ __global__ void __launch_bounds__(256) k_build_knm_mfma(KernParams kp, const dou
       e1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2[2 * p + 1], e1, 0, 0, 0);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const double v0 = (iv[r] && jv[2 * p]) ? sig2 * sgp_exp_nonpos(fmin(e0[r], 0.0)) : 0.0;
-        const double v1 = (iv[r] && jv[2 * p + 1]) ? sig2 * sgp_exp_nonpos(fmin(e1[r], 0.0)) : 0.0;
+        // K = exp(exponent) <= sig2: clamp the rounding above log(sig2), and below at -746
+        // (where exp underflows to 0)
+        const double v0 = sgp_exp_kp(fmin(fmax(e0[r], -746.0), ehi), kp);
+        const double v1 = sgp_exp_kp(fmin(fmax(e1[r], -746.0), ehi), kp);
         const int64_t i = ib + lq + 4 * r;
         __builtin_nontemporal_store(nt2{v0, v1},
                                     reinterpret_cast<nt2*>(&K[i * mp + j0 + 32 * p + 2 * ln]));

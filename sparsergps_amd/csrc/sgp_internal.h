@@ -56,7 +56,28 @@ struct KernParams {
   // Origin the K12 builder's GEMM-form exponent is centred on (the knots' mean; any point
   // gives the same K up to rounding -- centring keeps |x~|^2 + |u~|^2 small, see k_cov.hip)
   double ctr[SGP_MAXD];
+  double lsig2;          // log(sig2): folded into the builder's GEMM-form exponent
+  // sgp_exp_kp's constants as kernel arguments, so they sit in SGPRs and each Horner step is
+  // one v_fma_f64 (as literals the compiler pairs every step with a v_mov_b64): log2(e),
+  // ln2 hi/lo, then the degree-13 Taylor coefficients 1/13! .. 1/2!
+  double ec[16];
 };
+void set_exp_consts(KernParams* kp);
+
+// exp(x) for x already clamped to [-746, log(DBL_MAX)]: the same reduction and polynomial as
+// sgp_exp_nonpos with the constants read from kp (SGPRs).  Below -745.13 ldexp underflows to
+// 0, as exp does.
+__device__ __forceinline__ double sgp_exp_kp(double x, const KernParams& kp) {
+  const double k = __builtin_rint(x * kp.ec[0]);
+  double r = __builtin_fma(-k, kp.ec[1], x);
+  r = __builtin_fma(-k, kp.ec[2], r);
+  double p = kp.ec[3];
+#pragma unroll
+  for (int q = 4; q < 15; ++q) p = __builtin_fma(p, r, kp.ec[q]);
+  p = __builtin_fma(p, r, 1.0);
+  p = __builtin_fma(p, r, 1.0);
+  return __builtin_ldexp(p, (int)k);
+}
 
 
 // ---------------------------------------------------------------- k_cov.hip
