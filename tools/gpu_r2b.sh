@@ -16,7 +16,8 @@ timeout -k 10 300 python3 bench.py --no-cpu-baseline > $O/bench_c3.json 2> $O/be
 timeout -k 10 300 python3 bench.py --config C2 --steps 20 --warmup 3 > $O/bench_c2.json 2> $O/bench_c2.err || { echo "bench C2 failed"; tail -n 20 $O/bench_c2.err; exit 1; }
 timeout -k 10 300 python3 bench.py --mode laplace --steps 10 --warmup 2 > $O/bench_c5.json 2> $O/bench_c5.err || { echo "bench C5 failed"; tail -n 20 $O/bench_c5.err; exit 1; }
 timeout -k 10 300 python3 bench.py --mode fitc > $O/bench_fitc.json 2> $O/bench_fitc.err || { echo "bench FITC failed"; tail -n 20 $O/bench_fitc.err; exit 1; }
-cat $O/bench_c3.json $O/bench_c2.json $O/bench_c5.json $O/bench_fitc.json | cut -c1-400
+timeout -k 10 300 python3 bench.py --n 125000 --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_rows125k.json 2> $O/bench_rows125k.err || { echo "bench rows failed"; tail -n 20 $O/bench_rows125k.err; exit 1; }
+cat $O/bench_c3.json $O/bench_c2.json $O/bench_c5.json $O/bench_fitc.json $O/bench_rows125k.json | cut -c1-300
 if [ "${SKIP_CPU_FULL:-0}" != 1 ]; then
   timeout -k 10 900 python3 bench.py --cpu-full $O/cpu_full.json > $O/cpu_full.out 2> $O/cpu_full.err || { echo "cpu-full failed"; tail -n 20 $O/cpu_full.err; exit 1; }
   tail -n 12 $O/cpu_full.err
