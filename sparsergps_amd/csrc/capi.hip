@@ -103,6 +103,15 @@ void set_exp_consts(KernParams* kp) {
     f /= (double)q;
   }
   kp->ec[15] = 0.0;
+  kp->xt[0] = 46.166241308446828384;                 // 32 / ln2
+  kp->xt[1] = 6.93147180369123816490e-01 / 32.0;      // fdlibm ln2_hi (low 21 bits zero) / 32
+  kp->xt[2] = 1.90821492927058770002e-10 / 32.0;      // ln2_lo / 32
+  kp->xt[3] = 1.0 / 720.0;
+  kp->xt[4] = 1.0 / 120.0;
+  kp->xt[5] = 1.0 / 24.0;
+  kp->xt[6] = 1.0 / 6.0;
+  kp->xt[7] = 0.5;
+  for (int j = 0; j < 32; ++j) kp->et[j] = (double)exp2l((long double)j / 32.0L);
 }
 
 namespace {

@@ -229,6 +229,9 @@ __global__ void __launch_bounds__(256, WITH_T ? 3 : 4) k_build_knm_mfma(KernPara
                                                         double* __restrict__ tslab, int64_t slot0,
                                                         int64_t rb0, int64_t rb1) {
   __shared__ double tsh[WITH_T ? 4 : 1][128];
+  __shared__ double etab[32];
+  if (threadIdx.x < 32) etab[threadIdx.x] = kp.et[threadIdx.x];
+  __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ln = lane & 15, lq = lane >> 4;
   const int d = kp.d;
@@ -259,19 +262,34 @@ __global__ void __launch_bounds__(256, WITH_T ? 3 : 4) k_build_knm_mfma(KernPara
 #pragma unroll
   for (int tt = 0; tt < 8; ++tt) tacc[tt] = 0.0;
   typedef double nt2 __attribute__((ext_vector_type(2)));
+  // The next row block's coordinates and r are loaded before this block's stores: vmcnt
+  // counts loads and stores in issue order, so loads issued after the stores would make every
+  // block wait for the previous block's 16 stores to drain.
+  double xn0 = 0.0, xn1 = 0.0, rn[4] = {0.0, 0.0, 0.0, 0.0};
+  auto load_rows = [&](int64_t rb) {
+    const int64_t ib = rb * 64 + 16 * w, ia = ib + ln;   // X is zero-padded to n_pad rows
+    xn0 = f0 ? X[ia + c0 * ldx] : 0.0;
+    xn1 = f1 ? X[ia + c1 * ldx] : 0.0;
+    if (WITH_T) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) rn[r] = rvec[ib + lq + 4 * r];
+    }
+  };
+  if (rb0 + (int64_t)blockIdx.y < rb1) load_rows(rb0 + blockIdx.y);
   for (int64_t rb = rb0 + blockIdx.y; rb < rb1; rb += gridDim.y) {
     const int64_t ib = rb * 64 + 16 * w;
-    const int64_t ia = ib + ln;                 // this lane's A row (X is zero-padded to n_pad)
-    const double a0 = f0 ? (X[ia + c0 * ldx] - ct0) * rl0 : 0.0;
-    const double a1 = f1 ? (X[ia + c1 * ldx] - ct1) * rl1 : 0.0;
+    const int64_t ia = ib + ln;                 // this lane's A row
+    const double a0 = f0 ? (xn0 - ct0) * rl0 : 0.0;
+    const double a1 = f1 ? (xn1 - ct1) * rl1 : 0.0;
+    double rr[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rr[r] = rn[r];
+    if (rb + gridDim.y < rb1) load_rows(rb + gridDim.y);
     double x2 = fma(a0, a0, a1 * a1);
     x2 += __shfl_xor(x2, 16, 64);
     x2 += __shfl_xor(x2, 32, 64);
     // exponent = x~.u~ - |x~|^2 / 2 - |u~|^2 / 2 + log(sig2); padding rows as padding knots
     const double a2 = lq == 0 ? (ia < n ? -0.5 * x2 : -1e300) : (lq <= 2 ? 1.0 : 0.0);
-    double rr[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) rr[r] = WITH_T ? rvec[ib + lq + 4 * r] : 0.0;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const d4 z = {0.0, 0.0, 0.0, 0.0};
@@ -285,8 +303,8 @@ __global__ void __launch_bounds__(256, WITH_T ? 3 : 4) k_build_knm_mfma(KernPara
       for (int r = 0; r < 4; ++r) {
         // K = exp(exponent) <= sig2: clamp the rounding above log(sig2), and below at -746
         // (where exp underflows to 0)
-        const double v0 = sgp_exp_kp(fmin(fmax(e0[r], -746.0), ehi), kp);
-        const double v1 = sgp_exp_kp(fmin(fmax(e1[r], -746.0), ehi), kp);
+        const double v0 = sgp_exp_tab(fmin(fmax(e0[r], -746.0), ehi), kp, etab);
+        const double v1 = sgp_exp_tab(fmin(fmax(e1[r], -746.0), ehi), kp, etab);
         const int64_t i = ib + lq + 4 * r;
         __builtin_nontemporal_store(nt2{v0, v1},
                                     reinterpret_cast<nt2*>(&K[i * mp + j0 + 32 * p + 2 * ln]));
@@ -295,6 +313,10 @@ __global__ void __launch_bounds__(256, WITH_T ? 3 : 4) k_build_knm_mfma(KernPara
           tacc[2 * p + 1] = fma(v1, rr[r], tacc[2 * p + 1]);
         }
       }
+      // keep each tile pair's four stores where they are: left to itself the scheduler sinks
+      // all 16 to the end of the block, so a wave alternates a store burst with a long
+      // store-free VALU stretch
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   if (WITH_T) {

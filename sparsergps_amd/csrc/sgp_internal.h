@@ -61,8 +61,32 @@ struct KernParams {
   // one v_fma_f64 (as literals the compiler pairs every step with a v_mov_b64): log2(e),
   // ln2 hi/lo, then the degree-13 Taylor coefficients 1/13! .. 1/2!
   double ec[16];
+  // sgp_exp_tab's constants: 32 log2(e), ln2/32 hi/lo, 1/6! .. 1/2!, and the table 2^(j/32)
+  double xt[8];
+  double et[32];
 };
 void set_exp_consts(KernParams* kp);
+
+// exp(x) for x already clamped to [-746, log(DBL_MAX)] by a 32-entry table: x = (32 e + j) ln2/32
+// + r, |r| <= ln2/64, exp(x) = 2^e T_j (1 + p(r)) with p the degree-6 Taylor polynomial of
+// e^r - 1 (truncation < 2e-18 relative).  etab = kp.et staged in LDS: 32 doubles span the 64
+// banks once, so a wave's lookups never conflict.  Below -745.13 ldexp underflows to 0.
+__device__ __forceinline__ double sgp_exp_tab(double x, const KernParams& kp,
+                                              const double* etab) {
+  const double k = __builtin_rint(x * kp.xt[0]);
+  double r = __builtin_fma(-k, kp.xt[1], x);
+  r = __builtin_fma(-k, kp.xt[2], r);
+  double p = kp.xt[3];
+  p = __builtin_fma(p, r, kp.xt[4]);
+  p = __builtin_fma(p, r, kp.xt[5]);
+  p = __builtin_fma(p, r, kp.xt[6]);
+  p = __builtin_fma(p, r, kp.xt[7]);
+  p = __builtin_fma(p, r, 1.0);
+  p = p * r;
+  const int ki = (int)k;
+  const double t = etab[ki & 31];
+  return __builtin_ldexp(__builtin_fma(t, p, t), ki >> 5);
+}
 
 // exp(x) for x already clamped to [-746, log(DBL_MAX)]: the same reduction and polynomial as
 // sgp_exp_nonpos with the constants read from kp (SGPRs).  Below -745.13 ldexp underflows to
