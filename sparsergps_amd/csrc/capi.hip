@@ -965,6 +965,11 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
     HIPCHK(launch_syrk_aug(c->K, c->n_pad, mpv, c->r, nullptr, c->slab_syrk, c->slab_syrk_cap,
                            red1, c->stream, 2, nullptr, 0));
   }
+  // K22's inverse (aux) is queued behind the SYRK here rather than in phase 2: it needs only
+  // theta and U, so with several ranks it runs while the first all-reduce is in flight (the
+  // caller issues it on the main stream between the phases); alone it starts where it did
+  st = k22_factor(c, true);
+  if (st) return st;
   c->phase = 1;
   return SGP_OK;
 }
@@ -1047,10 +1052,8 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
   const double* t = red1 + mm;
   c->n_global = n_global;
   c->flags = flags;
-  // K22's inverse on aux, concurrently with Bm's on the main stream: two latency-bound chains
-  // of 256-workgroup steps that fit one residency round together
-  int st = k22_factor(c, true);
-  if (st) return st;
+  // K22's inverse (queued on aux at the end of phase 1) runs concurrently with Bm's on the
+  // main stream: two latency-bound chains of 256-workgroup steps fit one residency round
   {
     // tr(K22inv S) and M3 = K22inv S K22inv need S and K22inv only: on aux_lo beside the Bm
     // inversion (T22 and K22inv are final once the K22 chain on `aux` has finished).  Beside
@@ -1069,7 +1072,7 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
       HIPCHK(hipEventRecord(c->ev_m3, c->aux_lo));
     }
   }
-  st = bm_stage(c, S, 1.0 / z);
+  int st = bm_stage(c, S, 1.0 / z);
   if (st) return st;
   {
     Scope tm(c, "mm_vectors");
@@ -2118,8 +2121,7 @@ int sgp_vi_candidates(sgp_ctx* c, int kernel, const double* theta, const double*
   const double z = kp.tau2 + delta;
   const double* S = c->red1;
   const double* t = c->red1 + mm;
-  st = k22_factor(c, true);   // K22's inverse (aux) beside Bm's, as in sgp_vi_phase2
-  if (st) return st;
+  // K22's inverse was queued on aux by sgp_vi_phase1; it runs beside Bm's
   st = bm_stage(c, S, 1.0 / z);
   if (st) return st;
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
