@@ -9,3 +9,4 @@ for v in cur prev; do
 done
 done
 cp sparsergps_amd/lib/libsgp_cur.so sparsergps_amd/lib/libsgp.so
+timeout -k 10 120 ./tools/micro/kloop > gpurun_out/ab/kloop.txt 2>&1 && cat gpurun_out/ab/kloop.txt

@@ -7,6 +7,7 @@
 //   MODE 2  no global loads, no LDS stores (fragment reads + barrier + MFMA)
 //   MODE 3  no barrier (fragment reads + MFMA only)
 //   MODE 4  MFMA only (fragments in registers)
+//   MODE 5  LDS-DMA staging (k_loop_dma)
 // k_loop8: the same tile with 8 waves per workgroup (64 x 32 per wave).  MI355X r1: MODE 2
 // 74.4 vs 73.1 TF/s, but the full loop 68.1 vs 69.2 (the 4-wave loop stays)
 //   build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -o kloop kloop.hip ; run: ./kloop
@@ -156,6 +157,81 @@ __global__ void __launch_bounds__(256, 1) k_loop32(const double* __restrict__ K,
   if (s == 1234.5) out[tid] = s;
 }
 
+// MODE 5: operands staged by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction =
+// one 128-column k-row of an image) straight into the other LDS buffer: no staging VGPRs, no
+// ds_write; each wave issues 8 DMAs per step for step + 1, waits for its own (vmcnt(0)) after
+// the MFMAs, then the barrier.
+__global__ void __launch_bounds__(256, 2) k_loop_dma(const double* __restrict__ K, int64_t mp,
+                                                     int nsteps, double* out) {
+  __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
+  __shared__ __attribute__((aligned(16))) double Kb[2][BK * SB];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int ta = blockIdx.x % 8, tb = (blockIdx.x / 8) % 8;
+  const int64_t rbeg = (int64_t)(blockIdx.x / 64) * nsteps * BK;
+  d4 acc[4][4];
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+  // wave wv stages k-rows 4 wv .. 4 wv + 3 of both images
+  auto dma = [&](int step, int buf) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int kr = 4 * wv + q;
+      const int64_t row = rbeg + (int64_t)step * BK + kr;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(K + row * mp + ta * 128 + 2 * lane),
+          (__attribute__((address_space(3))) void*)(&Ka[buf][kr * SB]), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(K + row * mp + tb * 128 + 2 * lane),
+          (__attribute__((address_space(3))) void*)(&Kb[buf][kr * SB]), 16, 0, 0);
+    }
+  };
+  dma(0, 0);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
+    if (step + 1 < nsteps) dma(step + 1, cur ^ 1);
+    const double* As = Ka[cur];
+    const double* Bs = Kb[cur];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int krow = kk * 4 + (lane >> 4);
+      double af[4], bf[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        af[f] = As[krow * SB + wr * 64 + f * 16 + (lane & 15)];
+        bf[f] = Bs[krow * SB + wc * 64 + f * 16 + (lane & 15)];
+      }
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0);   // this wave's DMAs for step + 1 have landed
+    __syncthreads();
+  }
+  double s = 0.0;
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b) s += acc[a][b][0] + acc[a][b][1] + acc[a][b][2] + acc[a][b][3];
+  if (s == 1234.5) out[tid] = s;
+}
+
+void run_dma(const double* K, int64_t mp, int nsteps, double* out) {
+  const int nwg = 512;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  hipLaunchKernelGGL(k_loop_dma, dim3(nwg), dim3(256), 0, 0, K, mp, nsteps / 4, out);
+  hipEventRecord(e0);
+  hipLaunchKernelGGL(k_loop_dma, dim3(nwg), dim3(256), 0, 0, K, mp, nsteps, out);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms; hipEventElapsedTime(&ms, e0, e1);
+  const double flops = 2.0 * 128 * 128 * 16 * (double)nsteps * nwg;
+  printf("MODE 5 (LDS-DMA): %.3f ms  %.2f TF/s\n", ms, flops / (ms * 1e-3) / 1e12);
+}
+
 template <int SBW>
 void run32(const double* K, int64_t mp, int nsteps16, double* out, int wgs) {
   hipEvent_t e0, e1;
@@ -283,6 +359,10 @@ int main() {
     free(h);
   }
   const int nsteps = 4000;
+  run<0>(K, mp, nsteps, out);
+  run_dma(K, mp, nsteps, out);
+  run<0>(K, mp, nsteps, out);
+  run_dma(K, mp, nsteps, out);
   run32<144>(K, mp, nsteps, out, 256);
   run32<144>(K, mp, nsteps, out, 512);
   run<0>(K, mp, nsteps, out);
