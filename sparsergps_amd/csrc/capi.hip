@@ -1076,19 +1076,21 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
   if (st) return st;
   {
     Scope tm(c, "mm_vectors");
-    HIPCHK(dense_gemv(c->Binv, mp, t, 1.0 / z, c->uvec, c->stream));         // u = Binv t / z
-    HIPCHK(launch_dot(t, c->uvec, mp, c->slab_small, c->sc + SC_TU, c->stream));
-    HIPCHK(hipMemcpyAsync(c->sc + SC_RR, red1 + mm + mp, sizeof(double), hipMemcpyDeviceToDevice,
-                          c->stream));
     if (flags & SGP_FLAG_OBJ_ONLY) {   // elbo_fun alone: no adjoint work
+      HIPCHK(dense_gemv(c->Binv, mp, t, 1.0 / z, c->uvec, c->stream));       // u = Binv t / z
+      HIPCHK(launch_dot(t, c->uvec, mp, c->slab_small, c->sc + SC_TU, c->stream));
+      HIPCHK(hipMemcpyAsync(c->sc + SC_RR, red1 + mm + mp, sizeof(double),
+                            hipMemcpyDeviceToDevice, c->stream));
       HIPCHK(hipStreamWaitEvent(c->stream, c->ev_m3, 0));
       c->phase = 2;
       return SGP_OK;
     }
-    HIPCHK(launch_dot(c->Binv, S, mm, c->slab_small, c->sc + SC_TRBS, c->stream));
-    // P = tau^-2 K22inv - z^-1 Binv (and cdiag = diag K22inv for the contraction)
+    // u = Binv t / z, P = tau^-2 K22inv - z^-1 Binv, t.u, tr(Binv S) and r^T r in two
+    // launches (they sit between the Bm chain and the contraction, on the critical path)
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
-    HIPCHK(dense_axpby(1.0 / kp.tau2, c->K22inv, -1.0 / z, c->Binv, c->Pm, mm, c->stream));
+    HIPCHK(launch_vi_mm_vectors(c->Binv, c->K22inv, S, t, red1 + mm + mp, mp, 1.0 / z,
+                                1.0 / kp.tau2, -1.0 / z, c->uvec, c->Pm, c->slab_small,
+                                c->sc + SC_TU, c->sc + SC_TRBS, c->sc + SC_RR, c->stream));
     HIPCHK(hipEventRecord(c->ev_bm, c->stream));
   }
   {

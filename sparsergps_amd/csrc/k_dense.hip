@@ -465,7 +465,71 @@ __global__ void __launch_bounds__(256) k_fitc_omega(const double* __restrict__ a
   if (threadIdx.x == 0) slab[blockIdx.x] = s;
 }
 
+// VI phase-2 row pass over the m x m operands, one wave per row j (replaces a GEMV, an axpby
+// and a dot-product pair):  u_j = invz (Binv t)_j,  P_j: = a K22inv_j: + b Binv_j:,
+// part_j = sum_k Binv_jk S_jk.  The GEMV keeps k_gemv's lane-strided summation order.
+__global__ void __launch_bounds__(256) k_vi_mm_rows(const double* __restrict__ Binv,
+                                                    const double* __restrict__ K22inv,
+                                                    const double* __restrict__ S,
+                                                    const double* __restrict__ t, int64_t mp,
+                                                    double invz, double a, double b,
+                                                    double* __restrict__ u,
+                                                    double* __restrict__ P,
+                                                    double* __restrict__ part) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= mp) return;
+  const int64_t o = row * mp;
+  double su = 0.0, sp = 0.0;
+  for (int64_t j = lane; j < mp; j += 64) {
+    const double bv = Binv[o + j];
+    su = fma(bv, t[j], su);
+    sp = fma(bv, S[o + j], sp);
+    P[o + j] = a * K22inv[o + j] + b * bv;
+  }
+  su = wave_sum(su);
+  sp = wave_sum(sp);
+  if (lane == 0) {
+    u[row] = invz * su;
+    part[row] = sp;
+  }
+}
+
+// sc[0] = t . u, sc[1] = sum part (= tr(Binv S)), sc[2] = *rr; one block, fixed order
+__global__ void __launch_bounds__(256) k_vi_mm_scalars(const double* __restrict__ t,
+                                                       const double* __restrict__ u,
+                                                       const double* __restrict__ part,
+                                                       int64_t mp, const double* __restrict__ rr,
+                                                       double* __restrict__ tu_out,
+                                                       double* __restrict__ trbs_out,
+                                                       double* __restrict__ rr_out) {
+  __shared__ double sh[4];
+  double a = 0.0, c = 0.0;
+  for (int64_t j = threadIdx.x; j < mp; j += 256) {
+    a = fma(t[j], u[j], a);
+    c += part[j];
+  }
+  a = block_sum(a, sh);
+  c = block_sum(c, sh);
+  if (threadIdx.x == 0) {
+    *tu_out = a;
+    *trbs_out = c;
+    *rr_out = *rr;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_vi_mm_vectors(const double* Binv, const double* K22inv, const double* S,
+                                const double* t, const double* rr, int64_t mp, double invz,
+                                double a, double b, double* u, double* P, double* part,
+                                double* tu_out, double* trbs_out, double* rr_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_vi_mm_rows, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, s, Binv, K22inv,
+                     S, t, mp, invz, a, b, u, P, part);
+  hipLaunchKernelGGL(k_vi_mm_scalars, dim3(1), dim3(256), 0, s, t, u, part, mp, rr, tu_out,
+                     trbs_out, rr_out);
+  return hipGetLastError();
+}
 
 hipError_t launch_fitc_z(const double* q, int64_t n, int64_t n_pad, double c0, double* w,
                          double* slab, int* nblocks, hipStream_t s) {

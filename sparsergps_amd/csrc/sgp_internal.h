@@ -216,6 +216,12 @@ hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* Cb, doubl
 // C = a*A + b*B elementwise over mp x mp
 hipError_t dense_axpby(double a, const double* A, double b, const double* B, double* C,
                        int64_t count, hipStream_t s);
+// VI phase 2's m-vectors in two launches: u = invz Binv t, P = a K22inv + b Binv,
+// *tu_out = t.u, *trbs_out = tr(Binv S), *rr_out = *rr (part: mp doubles of scratch)
+hipError_t launch_vi_mm_vectors(const double* Binv, const double* K22inv, const double* S,
+                                const double* t, const double* rr, int64_t mp, double invz,
+                                double a, double b, double* u, double* P, double* part,
+                                double* tu_out, double* trbs_out, double* rr_out, hipStream_t s);
 // y = scale * A x  (A: mp x mp row-major)
 hipError_t dense_gemv(const double* A, int64_t mp, const double* x, double scale, double* y,
                       hipStream_t s);
