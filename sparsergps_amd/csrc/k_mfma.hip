@@ -29,6 +29,7 @@ constexpr int SB = 144;   // LDS row stride (doubles) of [k][128] operand images
 // 18 put rows r and r+8 on one bank (2-way conflicts on every A read); 17 is conflict-free for
 // ds_read2_b64 and ds_write_b64 alike (rows are then 8-byte aligned only: no b128 stores)
 constexpr int SA = 17;
+constexpr int SYRK_RGRP = 16;   // slabs summed per group by k_syrk_reduce_grp
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -289,8 +290,21 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
 
 // S (mp x mp full symmetric) from the per-split lower 64-blocks, fixed split order
 __global__ void __launch_bounds__(256)
+k_syrk_reduce_grp(double* __restrict__ slab, int splits, int64_t nblk) {
+  // first stage for many splits (small m): split group g = blockIdx.z sums its SYRK_RGRP
+  // slabs in order into the group's first slab (each element touched by one thread only)
+  const int64_t bid = blockIdx.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int s0 = blockIdx.z * SYRK_RGRP;
+  const int s1 = s0 + SYRK_RGRP < splits ? s0 + SYRK_RGRP : splits;
+  double v = 0.0;
+  for (int sp = s0; sp < s1; ++sp) v += slab[((int64_t)sp * nblk + bid) * 4096 + e];
+  slab[((int64_t)s0 * nblk + bid) * 4096 + e] = v;
+}
+
+__global__ void __launch_bounds__(256)
 k_syrk_reduce_blk(const double* __restrict__ slab, int splits, int64_t nblk, int64_t mp,
-                  double* __restrict__ red) {
+                  double* __restrict__ red, int stride) {
   const int64_t bid = blockIdx.y;
   const int e = blockIdx.x * 256 + threadIdx.x;   // element of the 64 x 64 block
   int rp = (int)((sqrtf(8.0f * (float)bid + 1.0f) - 1.0f) * 0.5f);
@@ -298,7 +312,7 @@ k_syrk_reduce_blk(const double* __restrict__ slab, int splits, int64_t nblk, int
   while ((int64_t)rp * (rp + 1) / 2 > bid) --rp;
   const int cp = (int)(bid - (int64_t)rp * (rp + 1) / 2);
   double v = 0.0;
-  for (int sp = 0; sp < splits; ++sp) v += slab[((int64_t)sp * nblk + bid) * 4096 + e];
+  for (int sp = 0; sp < splits; sp += stride) v += slab[((int64_t)sp * nblk + bid) * 4096 + e];
   const int64_t a = (int64_t)rp * 64 + e / 64, b = (int64_t)cp * 64 + e % 64;
   red[a * mp + b] = v;
   red[b * mp + a] = v;
@@ -1248,8 +1262,17 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
                            tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm);
     }
     if (part & 2) {
+      // many splits (small m): a first pass sums groups of SYRK_RGRP slabs in parallel, the
+      // final pass then sums the group totals (fixed order either way: deterministic)
+      int stride = 1;
+      if (q.splits > SYRK_RGRP) {
+        const unsigned ng = (unsigned)((q.splits + SYRK_RGRP - 1) / SYRK_RGRP);
+        hipLaunchKernelGGL(k_syrk_reduce_grp, dim3(4096 / 256, (unsigned)nblk, ng), dim3(256), 0,
+                           s, sl_s, q.splits, nblk);
+        stride = SYRK_RGRP;
+      }
       hipLaunchKernelGGL(k_syrk_reduce_blk, dim3(4096 / 256, (unsigned)nblk), dim3(256), 0, s,
-                         sl_s, q.splits, nblk, mp, red);
+                         sl_s, q.splits, nblk, mp, red, stride);
       if (with_t)
         hipLaunchKernelGGL(k_syrk_reduce_t, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s,
                            sl_t, sl_rr, q.splits, q.nb, mp, red);
