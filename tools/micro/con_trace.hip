@@ -1,4 +1,4 @@
-// Timeline probe of the K12 contraction kernel (k_contract<8, EPI_GRAD>): thread 0 of every
+// Timeline probe (stamps from the last launch: the normal 2-workgroups-per-CU grid) of the K12 contraction kernel (k_contract<8, EPI_GRAD>): thread 0 of every
 // workgroup records s_memtime at entry, after the k-loop and at the end, plus its CU / XCD, so
 // the per-tile fixed cost (prologue + epilogue) and the phase relation of the workgroups that
 // share a CU can be read off.  Synthetic operands; n = 131072 rows, m = 1024, d = 8 (ARD).
@@ -54,14 +54,6 @@ int main(int argc, char** argv) {
   int64_t nrec, nw;
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
-  for (int it = 0; it < 3; ++it) {
-    hipEventRecord(e0, 0);
-    launch_contract_args(kp, K, M, X, n_pad, n, n_pad, Uu, mp, m, mp, ca, slab, &nrec, &nw, 0);
-    hipEventRecord(e1, 0);
-    hipEventSynchronize(e1);
-    float ms; hipEventElapsedTime(&ms, e0, e1);
-    printf("run %d: %.3f ms  %.2f TF/s\n", it, ms, 2.0 * n * m * m / (ms * 1e-3) / 1e12);
-  }
   // one workgroup per CU: pad the launch with dynamic LDS so a second one cannot fit
   for (int it = 0; it < 3; ++it) {
     hipEventRecord(e0, 0);
@@ -72,6 +64,14 @@ int main(int argc, char** argv) {
     hipEventSynchronize(e1);
     float ms; hipEventElapsedTime(&ms, e0, e1);
     printf("1 WG/CU run %d: %.3f ms  %.2f TF/s\n", it, ms, 2.0 * n * m * m / (ms * 1e-3) / 1e12);
+  }
+  for (int it = 0; it < 3; ++it) {
+    hipEventRecord(e0, 0);
+    launch_contract_args(kp, K, M, X, n_pad, n, n_pad, Uu, mp, m, mp, ca, slab, &nrec, &nw, 0);
+    hipEventRecord(e1, 0);
+    hipEventSynchronize(e1);
+    float ms; hipEventElapsedTime(&ms, e0, e1);
+    printf("run %d: %.3f ms  %.2f TF/s\n", it, ms, 2.0 * n * m * m / (ms * 1e-3) / 1e12);
   }
   std::vector<unsigned long long> ht(nwg * 8);
   hipMemcpy(ht.data(), tr, ht.size() * 8, hipMemcpyDeviceToHost);
