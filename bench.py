@@ -154,6 +154,30 @@ def cpu_baseline_full(n_target=1_000_000, m=1024):
             "adjoint_direct": adjoint_direct(n_target, m)}
 
 
+def kernel_rooflines(mode, phase_avg, n_loc, m):
+    """The other hot kernels of the step against their own bounds (same HIP-event phase
+    timings as roofline.achieved): the K12 builder writes 8 B per (row, knot) pair of the
+    padded n_pad x m_p matrix (HBM-write bound); the SYRK does n m^2 algorithmic flops
+    (fp64 MFMA bound)."""
+    n_pad = -(-n_loc // 128) * 128
+    m_p = -(-m // 128) * 128
+    out = []
+    t = phase_avg.get("build_knm", 0.0) * 1e-3
+    if t > 0:
+        gbs = 8.0 * n_pad * m_p / t / 1e9
+        out.append({"kernel": "build_knm (k_build_knm_mfma)", "bound": "hbm", "achieved": gbs,
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                    "bytes_per_launch": 8.0 * n_pad * m_p})
+    key = {"vi": "syrk", "fitc": "syrk", "laplace": "syrk_z"}.get(mode)
+    t = phase_avg.get(key, 0.0) * 1e-3
+    if t > 0:
+        tf = float(n_loc) * m * m / t / 1e12
+        out.append({"kernel": key + " (k_syrk_blk)", "bound": "mfma", "achieved": tf,
+                    "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": tf / FP64_MFMA_PEAK_TFLOPS, "flops_per_launch": float(n_loc) * m * m})
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -322,6 +346,7 @@ def main():
                          "traffic": traffic if args.mode == "vi" else None,
                          "kernel": con_key + " (k_contract<8>)",
                          "flops_per_launch": flops},
+            "kernel_rooflines": kernel_rooflines(args.mode, phase_avg, n_loc, m),
             "phases_ms": {k: round(v, 4) for k, v in phase_avg.items()},
             "objective": obj,
         }

@@ -127,3 +127,18 @@ def test_c5_own_knot_count_against_adjoint_model(sgp):
     assert abs(obj - o) / abs(o) < 1e-9
     assert np.max(np.abs(fg - f)) < 1e-8
     assert _rel(grad, g) < 1e-7
+
+
+def test_c3_headline_shape_against_chunked_adjoint_model(sgp):
+    """configs[2] exactly (the bench workload): n = 1e6, m = 1024, d = 8, ARD -- the product
+    path against the row-chunked CPU model of the same adjoint algebra (~15-40 s of host
+    BLAS), i.e. parity at the headline size, not only at reduced n."""
+    from oracle import adjoint_chunked as AC
+    from sparsergps_amd.workloads import make_gaussian_problem
+    P = make_gaussian_problem("C3")
+    assert P["X"].shape == (1_000_000, 8) and P["U"].shape == (1024, 8)
+    th = np.array(list(P["cov_par"].values()))
+    obj, grad = sgp.vi_eval(P["cov_par"], "ard", P["U"], P["X"], P["y"], P["mu"], P["delta"])
+    o, g = AC.eval_vi("ard", th, P["X"], P["y"], P["mu"], P["U"], P["delta"])
+    assert abs(obj - o) / abs(o) < 1e-9
+    assert _rel(list(grad.values()), g) < 1e-7
