@@ -273,6 +273,13 @@ __global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
   double* S1 = lds + 64 * GJ_LS;
   const int i = blockIdx.y, j = blockIdx.x;
   const int64_t oi = (int64_t)i * 64, oj = (int64_t)j * 64, ok = (int64_t)k * 64;
+#ifdef SGP_GJ_TRACE   // timing probe only (tools/micro/gj_trace.hip): look-ahead WG stamps
+  const bool gj_tr = (i == k + 1) && (j == k + 1) && threadIdx.x == 0;
+#define GJ_STAMP(p_) do { if (gj_tr) SGP_GJ_TRACE(k, p_); } while (0)
+#else
+#define GJ_STAMP(p_) do { } while (0)
+#endif
+  GJ_STAMP(0);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   d4 acc[2][2];
@@ -336,8 +343,10 @@ __global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
   gj_st(S0, v0);
   gj_st(S1, v1);
   __syncthreads();
+  GJ_STAMP(1);
   gj_mm64(S0, S1, acc);                          // C_i P_k
   __syncthreads();                               // everyone is done reading S0 / S1
+  GJ_STAMP(2);
 #pragma unroll
   for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
@@ -367,8 +376,11 @@ __global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
       }
   if (look_ahead) {
     __syncthreads();
+    GJ_STAMP(3);
     gj_pivot_body(S0, GJ_LS, (int64_t)(k + 1) * 64, Pn, logd + k + 1, status, S1);
+    GJ_STAMP(4);
   }
+#undef GJ_STAMP
 }
 
 __global__ void __launch_bounds__(256) k_axpby(double a, const double* __restrict__ A, double b,
