@@ -7,6 +7,8 @@
 // Cholesky factor's squared diagonal, so log-determinants and R's chol() failure order come
 // out of the same pass.
 // Reductions are two-stage with fixed order (deterministic, run-to-run bit-identical).
+#include <stdlib.h>
+
 #include "sgp_internal.h"
 
 namespace {
@@ -562,6 +564,20 @@ hipError_t launch_fitc_omega(const double* alpha, const double* w, const double*
   return hipGetLastError();
 }
 
+// Dynamic LDS added to each step's workgroup so that only one fits per CU (71.7 KB static +
+// this > 80 KB).  Two chains run side by side (VI phase 2: K22's and Bm's inverses); with two
+// workgroups per CU a step's look-ahead workgroup (the chain's critical path: next pivot)
+// shared its CU with the other chain's tile updates.  One per CU, the other chain's step
+// fills the CUs the short tile updates free.  SGP_GJ_PAD_KB overrides (0 = off).
+static size_t gj_step_pad() {
+  static long pad = -1;
+  if (pad < 0) {
+    const char* e = getenv("SGP_GJ_PAD_KB");
+    pad = e ? atol(e) * 1024 : 24 * 1024;
+  }
+  return (size_t)pad;
+}
+
 hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* Cb, double* P,
                              double* logd, int* status, hipStream_t s) {
   // R: mp x mp ping-pong buffer; P: nb 64x64 pivot inverses (mp * 64 doubles); Cb unused.
@@ -572,7 +588,7 @@ hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* Cb, doubl
   double* dst = R;
   for (int k = 0; k < nb; ++k) {
     double* Pn = (k + 1 < nb) ? P + (int64_t)(k + 1) * 4096 : P;
-    hipLaunchKernelGGL(k_gj_step, dim3(nb, nb), dim3(256), 0, s, src, dst, mp, k, nb,
+    hipLaunchKernelGGL(k_gj_step, dim3(nb, nb), dim3(256), gj_step_pad(), s, src, dst, mp, k, nb,
                        P + (int64_t)k * 4096, Pn, logd, status);
     double* t = src;
     src = dst;
