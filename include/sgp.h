@@ -256,6 +256,9 @@ int sgp_lap_candidates(sgp_ctx* ctx, int kernel, const double* theta, const doub
  * over those sgp_ctx_timing_evals() evaluations (names: '\n'-separated phase names; ms: their
  * total durations, max n entries).  Nothing is read back while evaluations run. */
 int sgp_ctx_enable_timing(sgp_ctx* ctx, int enable);
+/* record only the phase called `name` (NULL: every phase) -- bench.py times its dominant
+ * kernel inside the timed region this way, with no other event records in the stream */
+int sgp_ctx_timing_filter(sgp_ctx* ctx, const char* name);
 int64_t sgp_ctx_timing_evals(const sgp_ctx* ctx);
 int sgp_ctx_timings(sgp_ctx* ctx, char* names, int64_t names_len, double* ms, int max_n, int* count);
 

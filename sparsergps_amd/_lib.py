@@ -95,6 +95,7 @@ PROTOTYPES = {
                                      C.c_int64, C.c_double, C.c_double, C.c_double, C.c_int,
                                      c_double_p, C.c_int64, C.c_int64, c_double_p]),
     "sgp_ctx_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
+    "sgp_ctx_timing_filter": (C.c_int, [C.c_void_p, C.c_char_p]),
     "sgp_ctx_timing_evals": (C.c_int64, [C.c_void_p]),
     "sgp_ctx_timings": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64, c_double_p, C.c_int, c_int_p]),
 }

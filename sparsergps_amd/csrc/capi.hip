@@ -210,6 +210,7 @@ struct sgp_ctx {
   std::vector<double> lap_objs;           // objective_function_values of the last NR run
   // timing
   bool timing = false;
+  std::string timing_only;                // record only the scopes of this name ("" = all)
   int64_t timing_evals = 0;               // evaluations recorded since timing was enabled
   std::vector<Timer> timers;
   std::vector<hipEvent_t> pool;
@@ -269,6 +270,7 @@ struct Scope {
   Scope(sgp_ctx* ctx, const char* name, hipStream_t st = nullptr)
       : c(ctx), s(st ? st : ctx->stream), idx((size_t)-1) {
     if (!c->timing) return;
+    if (!c->timing_only.empty() && c->timing_only != name) return;
     Timer t;
     t.name = name;
     t.a = pool_event(c);
@@ -744,6 +746,12 @@ int sgp_ctx_enable_timing(sgp_ctx* c, int enable) {
     c->pool_used = 0;
     c->timing_evals = 0;
   }
+  return SGP_OK;
+}
+
+int sgp_ctx_timing_filter(sgp_ctx* c, const char* name) {
+  if (!c) return SGP_EINVAL;
+  c->timing_only = name ? name : "";
   return SGP_OK;
 }
 

@@ -74,6 +74,11 @@ class SparseGPContext:
     def enable_timing(self, on=True):
         _lib.check(self._lib.sgp_ctx_enable_timing(self.handle, 1 if on else 0))
 
+    def timing_filter(self, name=None):
+        """Record only the phase `name` (None: all phases) while timing is enabled."""
+        _lib.check(self._lib.sgp_ctx_timing_filter(self.handle,
+                                                   None if name is None else name.encode()))
+
     def timing_evals(self):
         """Evaluations recorded since enable_timing(True)."""
         return int(self._lib.sgp_ctx_timing_evals(self.handle))

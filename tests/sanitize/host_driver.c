@@ -135,6 +135,7 @@ static void einval_checks(void) {
   EINVAL_(sgp_fitc_candidates(NULL, 1, th, buf, 1, 1, 1e-6, 0u, x, 1, 1, buf));
   EINVAL_(sgp_lap_candidates(NULL, 1, th, buf, 1, 1, 1e-6, 1.0, 1e-5, 10, x, 1, 1, buf));
   EINVAL_(sgp_ctx_enable_timing(NULL, 1));
+  EINVAL_(sgp_ctx_timing_filter(NULL, "contract_knm"));
   EINVAL_(sgp_ctx_timings(NULL, names, sizeof names, buf, 4, &ci));
   CHECK(sgp_ctx_rows(NULL) < 0, "sgp_ctx_rows(NULL)");
   CHECK(sgp_ctx_timing_evals(NULL) < 0 || sgp_ctx_timing_evals(NULL) == 0, "timing_evals(NULL)");
