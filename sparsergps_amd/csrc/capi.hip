@@ -940,19 +940,22 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   c->delta = delta;
   st = upload_knots(c, U, m, ldu);
   if (st) return st;
-  HIPCHK(hipMemsetAsync(c->status, 0, sizeof(int) * 4, c->stream));
-  HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->stream));
-  st = k22_sync(c);
+  st = k22_sync(c);   // aux may build K22 from here on
   if (st) return st;
   const int64_t mpv = c->mp, mmv = mpv * mpv;
   int64_t t_rows = 0;
   {
     // K12, and t = K^T r riding along in the memory-bound builder (keeps the SYRK's
-    // diagonal tiles as cheap as the others)
+    // diagonal tiles as cheap as the others); launched before anything else of the
+    // evaluation so the GPU starts on it as soon as the knots are up
     Scope t(c, "build_knm");
     HIPCHK(launch_build_knm_t(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, mpv, m, mpv, c->K, c->r,
                               c->tslab, &t_rows, c->stream, false));
   }
+  // status / scalar resets: first written by the K22 chain (queued after the SYRK below, aux
+  // waiting on the main stream) and by phase 2
+  HIPCHK(hipMemsetAsync(c->status, 0, sizeof(int) * 4, c->stream));
+  HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->stream));
   // K22 itself only (aux); its inverse runs in phase 2 beside the Bm inverse -- nothing in
   // phase 1 needs it, and the latency-bound chain no longer gates the one-round SYRK or shares
   // the CUs with the builder
