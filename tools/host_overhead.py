@@ -1,7 +1,12 @@
-#!/usr/bin/env python
-"""Host-side cost of one VI evaluation at C3 on one GPU: wall time of each API call of the
-phase protocol (the GPU runs asynchronously except in finish), to find host gaps between
-evaluations.  usage: python tools/host_overhead.py [steps] [rows]"""
+"""Host-side cost of one VI evaluation on the GPU (no profiler attached).
+
+Times, per evaluation of the bench's loop (RowShardedVI over one HipRowBackend, as bench.py
+runs it at N = 1): the host time inside sgp_vi_phase1 / sgp_vi_phase2 (launch issue only),
+inside sgp_vi_finish (waits for the GPU, then the readback), and the Python time between
+evaluations.  With the GPU the bottleneck, phase1 + phase2 issue time overlaps the previous
+kernels; what the GPU sees as idle is finish's tail + the Python gap + phase 1's issue up to
+its first launch.  usage: python3 tools/host_overhead.py [C2|C3] [n] [evals]
+"""
 import os
 import sys
 import time
@@ -15,39 +20,46 @@ def main():
     import torch
 
     import sparsergps_amd as S
-    from sparsergps_amd.workloads import make_gaussian_problem
-    from sparsergps_amd.dist import HipRowBackend
-    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-    rows = int(sys.argv[2]) if len(sys.argv) > 2 else None
-    P = make_gaussian_problem("C3", n=rows)
-    n, m = P["X"].shape[0], P["U"].shape[0]
-    names = S.param_names("ard", 8)
-    th0 = np.array([P["cov_par"][k] for k in names])
-    b = HipRowBackend(P["X"], P["y"], P["mu"], m, 0, "ard", "vi")
-    U = np.asfortranarray(P["U"])
-    tt = {"pre": 0.0, "phase1": 0.0, "phase2": 0.0, "finish": 0.0, "ctx": 0.0}
-    for k in range(steps + 2):
-        t0 = time.perf_counter()
-        th = th0 * np.exp(1e-3 * np.sin(np.arange(th0.size) + k))
-        t1 = time.perf_counter()
-        with b.stream_context():
-            t2 = time.perf_counter()
-            r1 = b.phase1(th, U, P["delta"])
-            t3 = time.perf_counter()
-            r2 = b.phase2(r1, n)
-            t4 = time.perf_counter()
-            obj, g = b.finish(r2)
-            t5 = time.perf_counter()
-        t6 = time.perf_counter()
-        if k >= 2:
-            tt["pre"] += t1 - t0
-            tt["ctx"] += (t2 - t1) + (t6 - t5)
-            tt["phase1"] += t3 - t2
-            tt["phase2"] += t4 - t3
-            tt["finish"] += t5 - t4
-    for k, v in tt.items():
-        print(f"{k:8s} {v / steps * 1e6:10.1f} us/eval")
+    from bench import make_problem
+    from sparsergps_amd.dist import HipRowBackend, RowShardedVI
+
+    config = sys.argv[1] if len(sys.argv) > 1 else "C2"
+    n = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2] != "-" else None
+    evals = int(sys.argv[3]) if len(sys.argv) > 3 else 40
+    P = make_problem(config, n=n)
+    names = S.param_names(P["cov_fun"], P["X"].shape[1])
+    theta0 = np.array([P["cov_par"][k] for k in names])
+    b = HipRowBackend(P["X"], P["y"], P["mu"], P["U"].shape[0], 0, P["cov_fun"], "vi")
+    vi = RowShardedVI(b, P["X"].shape[0], None, force_collectives=False)
+    U, delta = P["U"], P["delta"]
+
+    t_p1, t_p2, t_fin, t_gap, t_all = [], [], [], [], []
+    prev_end = None
+    for k in range(evals + 5):
+        th = theta0 * np.exp(1e-3 * np.sin(np.arange(theta0.size) + k))
+        a = time.perf_counter()
+        red1 = b.phase1(th, U, delta)
+        c1 = time.perf_counter()
+        red2 = b.phase2(red1, vi.n_global)
+        c2 = time.perf_counter()
+        b.finish(red2)
+        e = time.perf_counter()
+        if k >= 5:
+            t_p1.append(c1 - a)
+            t_p2.append(c2 - c1)
+            t_fin.append(e - c2)
+            t_all.append(e - a)
+            if prev_end is not None:
+                t_gap.append(a - prev_end)
+        prev_end = e
     torch.cuda.synchronize()
+    us = lambda v: f"{np.median(v) * 1e6:8.1f} us"
+    print(f"{config} n={P['X'].shape[0]} m={U.shape[0]}: per evaluation (median of {evals})")
+    print(f"  phase1 issue  {us(t_p1)}")
+    print(f"  phase2 issue  {us(t_p2)}")
+    print(f"  finish (wait + readback) {us(t_fin)}")
+    print(f"  python gap between evaluations {us(t_gap)}")
+    print(f"  eval wall     {us(t_all)}")
     b.close()
 
 
