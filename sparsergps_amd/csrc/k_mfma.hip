@@ -105,6 +105,26 @@ struct SyrkTMap {
   int S;                // slices per panel
 };
 
+// Every DESYNC_STEPS k-steps each wave of a long MFMA k-loop waits for its accumulators and
+// runs a short burst of fp32 FMAs on dead values (~1k VALU instructions, no memory traffic).
+// The two workgroups sharing a CU otherwise stay phase-locked -- their global loads, LDS
+// stores and barriers land on the same cycles -- and the burst, whose length depends on what
+// the partner is issuing, keeps them apart: tools/micro/kloop.hip (KLOOP_EPI=1) measures
+// MFMA busy 0.898 -> 0.930 of SIMD cycles at the same 2.38 GHz clock (70.0 -> 72.6 TF/s).
+constexpr int DESYNC_STEPS = 64;
+__device__ __forceinline__ void mfma_desync(double seed, double* sink) {
+  float v[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) v[c] = (float)seed + (float)c;   // waits for the accumulators
+  for (int e = 0; e < 128; ++e)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = fmaf(v[c], 0.999f, 1e-3f);
+  float t = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) t += v[c];
+  if (t == 1234.5f) sink[threadIdx.x] = (double)t;   // never true: keeps the burst alive
+}
+
 // WEIGHTED: rows scaled by w (FITC / Laplace); compiled out for the unweighted VI SYRK, whose
 // k-loop otherwise multiplies every A fragment by 1.0 (16 fp64 VALU ops per 64 MFMAs).
 template <bool WITH_T, bool WEIGHTED>
@@ -249,6 +269,8 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
     }
     if (step + 1 < nsteps) SYRKB_SSTORE(cur ^ 1);
     __syncthreads();
+    if (DESYNC_STEPS > 0 && (step % DESYNC_STEPS) == DESYNC_STEPS - 1)
+      mfma_desync(acc[0][0][0] + acc[3][3][3], slab);
   }
 #undef SYRKB_GLOAD
 #undef SYRKB_SSTORE
@@ -698,7 +720,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
       }
       // chunk ch of the coordinates: s_xs = [x~ | x~^2] (128 x 16), s_us = u~ (128 x sus)
 #define CON_XSTAGE(ch_)                                                                  \
-      for (int e = tid; e < T128 * 8; e += 256) {                                        \
+      _Pragma("unroll") for (int e = tid; e < T128 * 8; e += 256) {                      \
         const int rr = e % T128, c = e / T128, cg = 8 * (ch_) + c;                       \
         const int64_t i = i0 + rr, j = j0 + rr;                                          \
         double xv = 0.0;                                                                 \

@@ -18,7 +18,38 @@
 typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int BK = 16, SB = 144;
 
-template <int MODE>
+// EPI > 0: a stand-in for the contraction's per-tile epilogue every 64 steps (one m = 1024 tile):
+// the waves wait for their accumulators, then sleep EPI x s_sleep(127) (~8k cycles each) without
+// issuing anything -- how much of a latency-bound epilogue do the co-resident waves hide?
+// EPI >= 100: instead of sleeping, (EPI - 100) x 256 fp64 FMAs in 8 independent chains per wave
+// (EPI >= 200: the same count of fp32 FMAs) -- does VALU arithmetic beside a partner's MFMA
+// stream cost more than its issue slots?
+__device__ __forceinline__ void fake_epilogue(int epi, double a, double* out) {
+  if (a == 1234.5) out[threadIdx.x] = a;   // waits for the accumulator chain
+  if (epi >= 200) {
+    float v[8];
+    for (int c = 0; c < 8; ++c) v[c] = (float)a + c;
+    for (int e = 0; e < (epi - 200) * 32; ++e)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) v[c] = fmaf(v[c], 0.999f, 1e-3f);
+    float t = 0.f;
+    for (int c = 0; c < 8; ++c) t += v[c];
+    if (t == 1234.5f) out[threadIdx.x] = t;
+  } else if (epi >= 100) {
+    double v[8];
+    for (int c = 0; c < 8; ++c) v[c] = a + c;
+    for (int e = 0; e < (epi - 100) * 32; ++e)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) v[c] = fma(v[c], 0.999, 1e-3);
+    double t = 0.0;
+    for (int c = 0; c < 8; ++c) t += v[c];
+    if (t == 1234.5) out[threadIdx.x] = t;
+  } else {
+    for (int e = 0; e < epi; ++e) __builtin_amdgcn_s_sleep(127);
+  }
+}
+
+template <int MODE, int EPI = 0>
 __global__ void __launch_bounds__(256, 2) k_loop(const double* __restrict__ K, int64_t mp,
                                                  int nsteps, double* out) {
   __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
@@ -79,11 +110,103 @@ __global__ void __launch_bounds__(256, 2) k_loop(const double* __restrict__ K, i
     }
     if (MODE <= 1 && step + 1 < nsteps) sstore(cur ^ 1);
     if (MODE <= 2) __syncthreads();
+    if (EPI > 0 && (step & 63) == 63) fake_epilogue(EPI, acc[0][0][0] + acc[3][3][3], out);
   }
   double s = 0.0;
   for (int a = 0; a < 4; ++a)
     for (int b = 0; b < 4; ++b) s += acc[a][b][0] + acc[a][b][1] + acc[a][b][2] + acc[a][b][3];
   if (s == 1234.5) out[tid] = s;
+}
+
+// Prefetch distance 2: global loads for step + 2 are issued at the top of step (two staging
+// register sets), so one wave per SIMD (its partner in an epilogue) still covers an HBM round
+// trip with two steps of MFMAs instead of one.
+template <int EPI>
+__global__ void __launch_bounds__(256, 2) k_loop_pf2(const double* __restrict__ K, int64_t mp,
+                                                     int nsteps, double* out) {
+  __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
+  __shared__ __attribute__((aligned(16))) double Kb[2][BK * SB];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int ta = blockIdx.x % 8, tb = (blockIdx.x / 8) % 8;
+  const int64_t rbeg = (int64_t)(blockIdx.x / 64) * nsteps * BK;
+  d4 acc[4][4];
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+  const int lrow = tid >> 4, lc = tid & 15;
+  const double2* gA = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + ta * 128) + lc;
+  const double2* gB = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + tb * 128) + lc;
+  const int64_t gstep = BK * mp / 2;
+  double2 a0, a1, a2, a3, b0, b1, b2, b3;   // staging set of the even steps
+  double2 c0, c1, c2, c3, d0, d1, d2, d3;   // and of the odd steps
+#define PF_LOAD(step_, A0, A1, A2, A3, B0, B1, B2, B3)                                   \
+  {                                                                                     \
+    const int64_t o_ = (int64_t)(step_) * gstep;                                        \
+    A0 = gA[o_]; A1 = gA[o_ + 16]; A2 = gA[o_ + 32]; A3 = gA[o_ + 48];                  \
+    B0 = gB[o_]; B1 = gB[o_ + 16]; B2 = gB[o_ + 32]; B3 = gB[o_ + 48];                  \
+  }
+#define PF_STORE(buf_, A0, A1, A2, A3, B0, B1, B2, B3)                                  \
+  {                                                                                     \
+    double2* pa_ = reinterpret_cast<double2*>(&Ka[buf_][lrow * SB]) + lc;               \
+    double2* pb_ = reinterpret_cast<double2*>(&Kb[buf_][lrow * SB]) + lc;               \
+    pa_[0] = A0; pa_[16] = A1; pa_[32] = A2; pa_[48] = A3;                              \
+    pb_[0] = B0; pb_[16] = B1; pb_[32] = B2; pb_[48] = B3;                              \
+  }
+  auto compute = [&](int cur) {
+    const double* As = Ka[cur];
+    const double* Bs = Kb[cur];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int krow = kk * 4 + (lane >> 4);
+      double af[4], bf[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        af[f] = As[krow * SB + wr * 64 + f * 16 + (lane & 15)];
+        bf[f] = Bs[krow * SB + wc * 64 + f * 16 + (lane & 15)];
+      }
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
+    }
+  };
+  PF_LOAD(0, a0, a1, a2, a3, b0, b1, b2, b3);
+  PF_LOAD(1, c0, c1, c2, c3, d0, d1, d2, d3);
+  PF_STORE(0, a0, a1, a2, a3, b0, b1, b2, b3);
+  __syncthreads();
+  for (int step = 0; step < nsteps; step += 2) {   // nsteps even
+    // even step: its operands are in LDS buffer 0; refill the even set with step + 2
+    if (step + 2 < nsteps) PF_LOAD(step + 2, a0, a1, a2, a3, b0, b1, b2, b3);
+    compute(0);
+    PF_STORE(1, c0, c1, c2, c3, d0, d1, d2, d3);
+    __syncthreads();
+    // odd step: buffer 1; refill the odd set with step + 3
+    if (step + 3 < nsteps) PF_LOAD(step + 3, c0, c1, c2, c3, d0, d1, d2, d3);
+    compute(1);
+    if (step + 2 < nsteps) PF_STORE(0, a0, a1, a2, a3, b0, b1, b2, b3);
+    __syncthreads();
+    if (EPI > 0 && ((step + 1) & 63) == 63) fake_epilogue(EPI, acc[0][0][0] + acc[3][3][3], out);
+  }
+  double s = 0.0;
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b) s += acc[a][b][0] + acc[a][b][1] + acc[a][b][2] + acc[a][b][3];
+  if (s == 1234.5) out[tid] = s;
+}
+
+template <int EPI>
+void run_pf2(const double* K, int64_t mp, int nsteps, double* out) {
+  const int nwg = 512;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  hipLaunchKernelGGL(k_loop_pf2<EPI>, dim3(nwg), dim3(256), 0, 0, K, mp, nsteps / 4, out);
+  hipEventRecord(e0);
+  hipLaunchKernelGGL(k_loop_pf2<EPI>, dim3(nwg), dim3(256), 0, 0, K, mp, nsteps, out);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms; hipEventElapsedTime(&ms, e0, e1);
+  const double flops = 2.0 * 128 * 128 * 16 * (double)nsteps * nwg;
+  printf("PF2 EPI %2d: %.3f ms  %.2f TF/s\n", EPI, ms, flops / (ms * 1e-3) / 1e12);
 }
 
 // BK = 32 per step, double-buffered, one workgroup per CU (launch_bounds(256, 1): up to 512
@@ -247,26 +370,26 @@ void run32(const double* K, int64_t mp, int nsteps16, double* out, int wgs) {
   printf("BK32 SB=%d wgs=%d: %.3f ms  %.2f TF/s\n", SBW, wgs, ms, flops / (ms * 1e-3) / 1e12);
 }
 
-template <int MODE>
+template <int MODE, int EPI = 0>
 void run(const double* K, int64_t mp, int nsteps, double* out) {
   const int nwg = 512;
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
-  hipLaunchKernelGGL(k_loop<MODE>, dim3(nwg), dim3(256), 0, 0, K, mp, nsteps / 4, out);
+  hipLaunchKernelGGL((k_loop<MODE, EPI>), dim3(nwg), dim3(256), 0, 0, K, mp, nsteps / 4, out);
   hipEventRecord(e0);
-  hipLaunchKernelGGL(k_loop<MODE>, dim3(nwg), dim3(256), 0, 0, K, mp, nsteps, out);
+  hipLaunchKernelGGL((k_loop<MODE, EPI>), dim3(nwg), dim3(256), 0, 0, K, mp, nsteps, out);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms; hipEventElapsedTime(&ms, e0, e1);
   const double flops = 2.0 * 128 * 128 * 16 * (double)nsteps * nwg;
-  printf("MODE %d: %.3f ms  %.2f TF/s\n", MODE, ms, flops / (ms * 1e-3) / 1e12);
+  printf("MODE %d EPI %2d: %.3f ms  %.2f TF/s\n", MODE, EPI, ms, flops / (ms * 1e-3) / 1e12);
 }
 
 
 // 8 waves per 128x128 workgroup (2 x 4, 64 x 32 per wave: 4 x 2 fragments, 64 accumulator
 // VGPRs), 2 WGs per CU = 4 waves per SIMD: more waves to hide LDS / barrier latency at 1.5x
 // the fragment reads per MFMA.  MODE as k_loop (0 full, 2 no global loads / LDS stores).
-template <int MODE>
+template <int MODE, int EPI = 0>
 __global__ void __launch_bounds__(512, 2) k_loop8(const double* __restrict__ K, int64_t mp,
                                                   int nsteps, double* out) {
   __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
@@ -320,6 +443,7 @@ __global__ void __launch_bounds__(512, 2) k_loop8(const double* __restrict__ K, 
     }
     if (MODE <= 1 && step + 1 < nsteps) sstore(cur ^ 1);
     __syncthreads();
+    if (EPI > 0 && (step & 63) == 63) fake_epilogue(EPI, acc[0][0][0] + acc[3][1][3], out);
   }
   double s = 0.0;
   for (int a = 0; a < 4; ++a)
@@ -327,19 +451,19 @@ __global__ void __launch_bounds__(512, 2) k_loop8(const double* __restrict__ K, 
   if (s == 1234.5) out[tid] = s;
 }
 
-template <int MODE>
+template <int MODE, int EPI = 0>
 void run8(const double* K, int64_t mp, int nsteps, double* out) {
   const int nwg = 512;
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
-  hipLaunchKernelGGL(k_loop8<MODE>, dim3(nwg), dim3(512), 0, 0, K, mp, nsteps / 4, out);
+  hipLaunchKernelGGL((k_loop8<MODE, EPI>), dim3(nwg), dim3(512), 0, 0, K, mp, nsteps / 4, out);
   hipEventRecord(e0);
-  hipLaunchKernelGGL(k_loop8<MODE>, dim3(nwg), dim3(512), 0, 0, K, mp, nsteps, out);
+  hipLaunchKernelGGL((k_loop8<MODE, EPI>), dim3(nwg), dim3(512), 0, 0, K, mp, nsteps, out);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms; hipEventElapsedTime(&ms, e0, e1);
   const double flops = 2.0 * 128 * 128 * 16 * (double)nsteps * nwg;
-  printf("8-wave MODE %d: %.3f ms  %.2f TF/s\n", MODE, ms, flops / (ms * 1e-3) / 1e12);
+  printf("8-wave MODE %d EPI %2d: %.3f ms  %.2f TF/s\n", MODE, EPI, ms, flops / (ms * 1e-3) / 1e12);
 }
 
 int main() {
@@ -359,6 +483,23 @@ int main() {
     free(h);
   }
   const int nsteps = 4000;
+  if (getenv("KLOOP_EPI")) {   // epilogue-hiding comparison only
+    for (int rep = 0; rep < 2; ++rep) {
+      run<0>(K, mp, nsteps, out);
+      run<0, 6>(K, mp, nsteps, out);
+      run<0, 12>(K, mp, nsteps, out);
+      run_pf2<0>(K, mp, nsteps, out);
+      run_pf2<6>(K, mp, nsteps, out);
+      run_pf2<12>(K, mp, nsteps, out);
+      run<0, 200>(K, mp, nsteps, out);
+      run<0, 201>(K, mp, nsteps, out);
+      run<0, 204>(K, mp, nsteps, out);
+      run<0, 208>(K, mp, nsteps, out);
+      run<0, 216>(K, mp, nsteps, out);
+      run_pf2<204>(K, mp, nsteps, out);
+    }
+    return 0;
+  }
   run<0>(K, mp, nsteps, out);
   run_dma(K, mp, nsteps, out);
   run<0>(K, mp, nsteps, out);
