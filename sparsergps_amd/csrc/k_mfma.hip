@@ -112,7 +112,8 @@ struct SyrkTMap {
 // the partner is issuing, keeps them apart: tools/micro/kloop.hip (KLOOP_EPI=1) measures
 // MFMA busy 0.898 -> 0.930 of SIMD cycles at the same 2.38 GHz clock (70.0 -> 72.6 TF/s).
 constexpr int DESYNC_STEPS = 64;
-__device__ __forceinline__ void mfma_desync(double seed, double* sink) {
+__device__ double g_desync_sink[256];   // written only if the burst's dead value hits 1234.5f
+__device__ __forceinline__ void mfma_desync(double seed) {
   float v[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) v[c] = (float)seed + (float)c;   // waits for the accumulators
@@ -122,7 +123,8 @@ __device__ __forceinline__ void mfma_desync(double seed, double* sink) {
   float t = 0.f;
 #pragma unroll
   for (int c = 0; c < 8; ++c) t += v[c];
-  if (t == 1234.5f) sink[threadIdx.x] = (double)t;   // never true: keeps the burst alive
+  // keeps the burst alive; the sink is never read, so the (rare) hit is harmless
+  if (t == 1234.5f) g_desync_sink[threadIdx.x & 255] = (double)t;
 }
 
 // WEIGHTED: rows scaled by w (FITC / Laplace); compiled out for the unweighted VI SYRK, whose
@@ -270,7 +272,7 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
     if (step + 1 < nsteps) SYRKB_SSTORE(cur ^ 1);
     __syncthreads();
     if (DESYNC_STEPS > 0 && (step % DESYNC_STEPS) == DESYNC_STEPS - 1)
-      mfma_desync(acc[0][0][0] + acc[3][3][3], slab);
+      mfma_desync(acc[0][0][0] + acc[3][3][3]);
   }
 #undef SYRKB_GLOAD
 #undef SYRKB_SSTORE

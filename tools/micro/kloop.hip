@@ -78,14 +78,14 @@ __global__ void __launch_bounds__(256, 2) k_loop(const double* __restrict__ K, i
     pa[0] = va0; pa[16] = va1; pa[32] = va2; pa[48] = va3;
     pb[0] = vb0; pb[16] = vb1; pb[32] = vb2; pb[48] = vb3;
   };
-  if (MODE == 0) gload(0);
+  if (MODE == 0 || MODE >= 6) gload(0);
   sstore(0);
   sstore(1);
   __syncthreads();
   double rf[4] = {1.0 + lane * 1e-7, 1.0, 1.0, 1.0};
   for (int step = 0; step < nsteps; ++step) {
     const int cur = step & 1;
-    if (MODE == 0 && step + 1 < nsteps) gload(step + 1);
+    if ((MODE == 0 || MODE >= 6) && step + 1 < nsteps) gload(step + 1);
     const double* As = Ka[cur];
     const double* Bs = Kb[cur];
 #pragma unroll
@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(256, 2) k_loop(const double* __restrict__ K, i
       double af[4], bf[4];
 #pragma unroll
       for (int f = 0; f < 4; ++f) {
-        if (MODE <= 3) {
+        if (MODE <= 3 || MODE >= 6) {
           af[f] = As[krow * SB + wr * 64 + f * 16 + (lane & 15)];
           bf[f] = Bs[krow * SB + wc * 64 + f * 16 + (lane & 15)];
         } else {
@@ -107,9 +107,13 @@ __global__ void __launch_bounds__(256, 2) k_loop(const double* __restrict__ K, i
 #pragma unroll
         for (int fn = 0; fn < 4; ++fn)
           acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
+      // MODE 6 / 7: the next step's LDS stores between the MFMAs of sub-step 1 / 2 instead of
+      // after the last one (the buffer is free since the previous barrier)
+      if ((MODE == 6 && kk == 1) || (MODE == 7 && kk == 2))
+        if (step + 1 < nsteps) sstore(cur ^ 1);
     }
     if (MODE <= 1 && step + 1 < nsteps) sstore(cur ^ 1);
-    if (MODE <= 2) __syncthreads();
+    if (MODE <= 2 || MODE >= 6) __syncthreads();
     if (EPI > 0 && (step & 63) == 63) fake_epilogue(EPI, acc[0][0][0] + acc[3][3][3], out);
   }
   double s = 0.0;
@@ -371,8 +375,7 @@ void run32(const double* K, int64_t mp, int nsteps16, double* out, int wgs) {
 }
 
 template <int MODE, int EPI = 0>
-void run(const double* K, int64_t mp, int nsteps, double* out) {
-  const int nwg = 512;
+void run(const double* K, int64_t mp, int nsteps, double* out, int nwg = 512) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
   hipLaunchKernelGGL((k_loop<MODE, EPI>), dim3(nwg), dim3(256), 0, 0, K, mp, nsteps / 4, out);
@@ -382,7 +385,7 @@ void run(const double* K, int64_t mp, int nsteps, double* out) {
   hipEventSynchronize(e1);
   float ms; hipEventElapsedTime(&ms, e0, e1);
   const double flops = 2.0 * 128 * 128 * 16 * (double)nsteps * nwg;
-  printf("MODE %d EPI %2d: %.3f ms  %.2f TF/s\n", MODE, EPI, ms, flops / (ms * 1e-3) / 1e12);
+  printf("MODE %d EPI %2d wgs %d: %.3f ms  %.2f TF/s\n", MODE, EPI, nwg, ms, flops / (ms * 1e-3) / 1e12);
 }
 
 
@@ -483,6 +486,26 @@ int main() {
     free(h);
   }
   const int nsteps = 4000;
+  if (getenv("KLOOP_ALONE")) {   // one workgroup per CU (one wave per SIMD) vs two
+    for (int rep = 0; rep < 2; ++rep) {
+      run<6>(K, mp, nsteps, out, 512);
+      run<6>(K, mp, nsteps, out, 256);
+      run<7>(K, mp, nsteps, out, 512);
+      run<7>(K, mp, nsteps, out, 256);
+      run<6, 204>(K, mp, nsteps, out, 512);
+      run<0, 204>(K, mp, nsteps, out, 512);
+      run<6, 12>(K, mp, nsteps, out, 512);
+      run<4>(K, mp, nsteps, out, 512);
+      run<4>(K, mp, nsteps, out, 256);
+      run<3>(K, mp, nsteps, out, 512);
+      run<3>(K, mp, nsteps, out, 256);
+      run<2>(K, mp, nsteps, out, 512);
+      run<2>(K, mp, nsteps, out, 256);
+      run<0>(K, mp, nsteps, out, 512);
+      run<0>(K, mp, nsteps, out, 256);
+    }
+    return 0;
+  }
   if (getenv("KLOOP_EPI")) {   // epilogue-hiding comparison only
     for (int rep = 0; rep < 2; ++rep) {
       run<0>(K, mp, nsteps, out);
