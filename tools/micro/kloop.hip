@@ -345,8 +345,7 @@ __global__ void __launch_bounds__(256, 2) k_loop_dma(const double* __restrict__ 
   if (s == 1234.5) out[tid] = s;
 }
 
-void run_dma(const double* K, int64_t mp, int nsteps, double* out) {
-  const int nwg = 512;
+void run_dma(const double* K, int64_t mp, int nsteps, double* out, int nwg = 512) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
   hipLaunchKernelGGL(k_loop_dma, dim3(nwg), dim3(256), 0, 0, K, mp, nsteps / 4, out);
@@ -356,7 +355,7 @@ void run_dma(const double* K, int64_t mp, int nsteps, double* out) {
   hipEventSynchronize(e1);
   float ms; hipEventElapsedTime(&ms, e0, e1);
   const double flops = 2.0 * 128 * 128 * 16 * (double)nsteps * nwg;
-  printf("MODE 5 (LDS-DMA): %.3f ms  %.2f TF/s\n", ms, flops / (ms * 1e-3) / 1e12);
+  printf("MODE 5 (LDS-DMA) wgs %d: %.3f ms  %.2f TF/s\n", nwg, ms, flops / (ms * 1e-3) / 1e12);
 }
 
 template <int SBW>
@@ -488,13 +487,8 @@ int main() {
   const int nsteps = 4000;
   if (getenv("KLOOP_ALONE")) {   // one workgroup per CU (one wave per SIMD) vs two
     for (int rep = 0; rep < 2; ++rep) {
-      run<6>(K, mp, nsteps, out, 512);
-      run<6>(K, mp, nsteps, out, 256);
-      run<7>(K, mp, nsteps, out, 512);
-      run<7>(K, mp, nsteps, out, 256);
-      run<6, 204>(K, mp, nsteps, out, 512);
-      run<0, 204>(K, mp, nsteps, out, 512);
-      run<6, 12>(K, mp, nsteps, out, 512);
+      run_dma(K, mp, nsteps, out, 512);
+      run_dma(K, mp, nsteps, out, 256);
       run<4>(K, mp, nsteps, out, 512);
       run<4>(K, mp, nsteps, out, 256);
       run<3>(K, mp, nsteps, out, 512);
