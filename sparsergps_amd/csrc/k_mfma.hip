@@ -1402,6 +1402,11 @@ hipError_t launch_rowsum(const double* slab, int64_t nrow, int64_t len, double* 
   return hipGetLastError();
 }
 
+// dynamic LDS of the gradient-contraction launches: 0 in the product; tools/micro/con_trace.hip
+// builds with a pad that leaves one workgroup per CU (the k-loop without a co-resident partner)
+#ifndef SGP_CON_SHMEM
+#define SGP_CON_SHMEM 0
+#endif
 template <int DT, bool KNOT = false>
 static void launch_con_grad(bool v2, const KernParams& kp, const double* K, const double* M,
                             const double* X, int64_t ldx, int64_t n, int64_t n_pad,
@@ -1409,11 +1414,11 @@ static void launch_con_grad(bool v2, const KernParams& kp, const double* K, cons
                             const ConArgs& ca, double* slab, int nrec, int64_t nwg,
                             hipStream_t s) {
   if (v2)
-    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, true, KNOT>), dim3((unsigned)nwg), dim3(256), 0,
+    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, true, KNOT>), dim3((unsigned)nwg), dim3(256), SGP_CON_SHMEM,
                        s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec,
                        (double*)nullptr);
   else
-    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, false, KNOT>), dim3((unsigned)nwg), dim3(256), 0,
+    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, false, KNOT>), dim3((unsigned)nwg), dim3(256), SGP_CON_SHMEM,
                        s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec,
                        (double*)nullptr);
 }

@@ -199,8 +199,7 @@ __global__ void __launch_bounds__(256, 2) k_loop_pf2(const double* __restrict__ 
 }
 
 template <int EPI>
-void run_pf2(const double* K, int64_t mp, int nsteps, double* out) {
-  const int nwg = 512;
+void run_pf2(const double* K, int64_t mp, int nsteps, double* out, int nwg = 512) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
   hipLaunchKernelGGL(k_loop_pf2<EPI>, dim3(nwg), dim3(256), 0, 0, K, mp, nsteps / 4, out);
@@ -210,7 +209,109 @@ void run_pf2(const double* K, int64_t mp, int nsteps, double* out) {
   hipEventSynchronize(e1);
   float ms; hipEventElapsedTime(&ms, e0, e1);
   const double flops = 2.0 * 128 * 128 * 16 * (double)nsteps * nwg;
-  printf("PF2 EPI %2d: %.3f ms  %.2f TF/s\n", EPI, ms, flops / (ms * 1e-3) / 1e12);
+  printf("PF2 EPI %2d wgs %d: %.3f ms  %.2f TF/s\n", EPI, nwg, ms, flops / (ms * 1e-3) / 1e12);
+}
+
+// Intra-wave interleaving (MODE 0's work): loads and stores unconditional (clamped on the last
+// step) so a step is one basic block, and sched_group_barrier asks the scheduler for one
+// MFMA, then one LDS read, ... with the eight global loads and eight LDS stores spread over
+// the step -- the other instructions issue in the shadow of the MFMAs already in the pipe,
+// which matters when a wave has its SIMD to itself.  IL: 0 = no pattern (control).
+template <int IL>
+__global__ void __launch_bounds__(256, 2) k_loop_il(const double* __restrict__ K, int64_t mp,
+                                                    int nsteps, double* out) {
+  __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
+  __shared__ __attribute__((aligned(16))) double Kb[2][BK * SB];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int ta = blockIdx.x % 8, tb = (blockIdx.x / 8) % 8;
+  const int64_t rbeg = (int64_t)(blockIdx.x / 64) * nsteps * BK;
+  d4 acc[4][4];
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+  const int lrow = tid >> 4, lc = tid & 15;
+  const double2* gA = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + ta * 128) + lc;
+  const double2* gB = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + tb * 128) + lc;
+  const int64_t gstep = BK * mp / 2;
+  double2 va0, va1, va2, va3, vb0, vb1, vb2, vb3;
+  {
+    va0 = gA[0]; va1 = gA[16]; va2 = gA[32]; va3 = gA[48];
+    vb0 = gB[0]; vb1 = gB[16]; vb2 = gB[32]; vb3 = gB[48];
+    double2* pa = reinterpret_cast<double2*>(&Ka[0][lrow * SB]) + lc;
+    double2* pb = reinterpret_cast<double2*>(&Kb[0][lrow * SB]) + lc;
+    pa[0] = va0; pa[16] = va1; pa[32] = va2; pa[48] = va3;
+    pb[0] = vb0; pb[16] = vb1; pb[32] = vb2; pb[48] = vb3;
+  }
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
+    const int nx = step + 1 < nsteps ? step + 1 : step;   // clamped: one basic block per step
+    const int64_t o = (int64_t)nx * gstep;
+    va0 = gA[o]; va1 = gA[o + 16]; va2 = gA[o + 32]; va3 = gA[o + 48];
+    vb0 = gB[o]; vb1 = gB[o + 16]; vb2 = gB[o + 32]; vb3 = gB[o + 48];
+    const double* As = Ka[cur];
+    const double* Bs = Kb[cur];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int krow = kk * 4 + (lane >> 4);
+      double af[4], bf[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        af[f] = As[krow * SB + wr * 64 + f * 16 + (lane & 15)];
+        bf[f] = Bs[krow * SB + wc * 64 + f * 16 + (lane & 15)];
+      }
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
+    }
+    {
+      double2* pa = reinterpret_cast<double2*>(&Ka[cur ^ 1][lrow * SB]) + lc;
+      double2* pb = reinterpret_cast<double2*>(&Kb[cur ^ 1][lrow * SB]) + lc;
+      pa[0] = va0; pa[16] = va1; pa[32] = va2; pa[48] = va3;
+      pb[0] = vb0; pb[16] = vb1; pb[32] = vb2; pb[48] = vb3;
+    }
+    if (IL == 1) {
+      // 8 VMEM reads first (one per MFMA), LDS reads one per MFMA, LDS writes in the last
+      // quarter, one per MFMA
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);          // MFMA
+        if (i < 8) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+        if (i < 32) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0); // DS read
+        if (i >= 48 && i < 56) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+      }
+    } else if (IL == 2) {
+      // DS reads two per MFMA slot in the first half, writes spread over the second half
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (i < 8) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        if ((i & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        if (i >= 32 && (i & 3) == 0) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+      }
+    }
+    __syncthreads();
+  }
+  double s = 0.0;
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b) s += acc[a][b][0] + acc[a][b][1] + acc[a][b][2] + acc[a][b][3];
+  if (s == 1234.5) out[tid] = s;
+}
+
+template <int IL>
+void run_il(const double* K, int64_t mp, int nsteps, double* out, int nwg) {
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  hipLaunchKernelGGL(k_loop_il<IL>, dim3(nwg), dim3(256), 0, 0, K, mp, nsteps / 4, out);
+  hipEventRecord(e0);
+  hipLaunchKernelGGL(k_loop_il<IL>, dim3(nwg), dim3(256), 0, 0, K, mp, nsteps, out);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms; hipEventElapsedTime(&ms, e0, e1);
+  const double flops = 2.0 * 128 * 128 * 16 * (double)nsteps * nwg;
+  printf("IL %d wgs %d: %.3f ms  %.2f TF/s\n", IL, nwg, ms, flops / (ms * 1e-3) / 1e12);
 }
 
 // BK = 32 per step, double-buffered, one workgroup per CU (launch_bounds(256, 1): up to 512
@@ -487,8 +588,12 @@ int main() {
   const int nsteps = 4000;
   if (getenv("KLOOP_ALONE")) {   // one workgroup per CU (one wave per SIMD) vs two
     for (int rep = 0; rep < 2; ++rep) {
-      run_dma(K, mp, nsteps, out, 512);
-      run_dma(K, mp, nsteps, out, 256);
+      run_il<0>(K, mp, nsteps, out, 512);
+      run_il<0>(K, mp, nsteps, out, 256);
+      run_il<1>(K, mp, nsteps, out, 512);
+      run_il<1>(K, mp, nsteps, out, 256);
+      run_il<2>(K, mp, nsteps, out, 512);
+      run_il<2>(K, mp, nsteps, out, 256);
       run<4>(K, mp, nsteps, out, 512);
       run<4>(K, mp, nsteps, out, 256);
       run<3>(K, mp, nsteps, out, 512);
