@@ -135,12 +135,16 @@ __device__ __forceinline__ void mfma_desync(double seed) {
 // matrix pipe idle for the load latency; interleaved, the other instructions issue while the
 // MFMAs already queued execute.  tools/micro/kloop.hip (IL 1): 68.4 -> 73.9 TF/s with two
 // workgroups per CU, 60.3 -> 70.0 with one.  Needs the step to be a single basic block.
+// SPREAD: one LDS read per two MFMAs over the whole step (fragments read one sub-step ahead:
+// fewer live registers, for kernels whose epilogue shares the register budget).
+template <bool SPREAD = false>
 __device__ __forceinline__ void mfma_interleave() {
 #pragma unroll
   for (int i = 0; i < 64; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                      // MFMA
     if (i < 8) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);           // VMEM read
-    if (i < 32) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);          // DS read
+    if (SPREAD ? (i & 1) == 0 : i < 32)
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                    // DS read
     if (i >= 48 && i < 56) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
   }
 }
@@ -218,7 +222,9 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
     const int64_t o_ = (int64_t)(step) * gstep;                                 \
     va0 = gA[o_]; va1 = gA[o_ + 16]; va2 = gA[o_ + 32]; va3 = gA[o_ + 48];      \
     vb0 = gB[o_]; vb1 = gB[o_ + 16]; vb2 = gB[o_ + 32]; vb3 = gB[o_ + 48];      \
-    if (tid < BK) {                                                             \
+    if constexpr (!WITH_T) {  /* one block: every lane, 16 per weight */      \
+      if constexpr (WEIGHTED) vw = w[rbeg + (int64_t)(step) * BK + (tid & (BK - 1))]; \
+    } else if (tid < BK) {                                                      \
       const int64_t rr_ = rbeg + (int64_t)(step) * BK + tid;                    \
       if (WEIGHTED) vw = w[rr_];                                                \
       if (with_t) {                                                             \
@@ -233,7 +239,9 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
     double2* pb_ = reinterpret_cast<double2*>(&Kb[buf][lrow * SB]) + lc;        \
     pa_[0] = va0; pa_[16] = va1; pa_[32] = va2; pa_[48] = va3;                  \
     pb_[0] = vb0; pb_[16] = vb1; pb_[32] = vb2; pb_[48] = vb3;                  \
-    if (tid < BK) {                                                             \
+    if constexpr (!WITH_T) {                                                    \
+      ws[buf][tid & (BK - 1)] = vw;                                             \
+    } else if (tid < BK) {                                                      \
       ws[buf][tid] = vw;                                                        \
       if (with_t) {                                                             \
         const double rw_ = (tv != nullptr) ? vr : vr * vrr; /* (w r)_i or tv_i */ \
@@ -250,11 +258,11 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
   __syncthreads();
   for (int step = 0; step < nsteps; ++step) {
     const int cur = step & 1;
-    // VI (no t, no weights): one basic block per step, which the interleaved schedule below
-    // needs -- the last step reloads its own rows and stores them into the idle buffer.  (The
+    // Without t: one basic block per step, which the interleaved schedule below needs -- the
+    // last step reloads its own rows (and weights) and stores them into the idle buffer.  (The
     // t variants fold each staged row into rr as they store it, so they keep the guards.)
     // There inactive waves run their MFMAs on valid LDS operands (results never written).
-    constexpr bool one_block = !WITH_T && !WEIGHTED;
+    constexpr bool one_block = !WITH_T;
     if constexpr (one_block) {
       SYRKB_GLOAD(step + 1 < nsteps ? step + 1 : step);
     } else if (step + 1 < nsteps) {
@@ -548,6 +556,9 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   const int nsteps = (int)(mp / BK);
   // alpha folded into the k-loop: each thread dots the 8 K values it stages with u.
   double ku = 0.0, vuk = 0.0;
+  // the step is one basic block (mfma_interleave): the u slice is fetched, staged and folded
+  // unconditionally -- from M when there is no u (valid memory; ku is then never used)
+  const double* __restrict__ uk_src = with_u ? uvec : M;
 
   // The alpha dot products K_i . u ride on the A stream: 16 threads fetch the step's u slice
   // with the operands, it is staged in LDS with them, and each thread folds its 8 staged K
@@ -557,7 +568,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     const int64_t oa_ = (int64_t)(step) * (BK / 2), ob_ = (int64_t)(step) * bstep; \
     va0 = gA[oa_]; va1 = gA[oa_ + 1]; va2 = gA[oa_ + 2]; va3 = gA[oa_ + 3];      \
     vb0 = gB[ob_]; vb1 = gB[ob_ + 16]; vb2 = gB[ob_ + 32]; vb3 = gB[ob_ + 48];   \
-    if (with_u && tid < BK) vuk = uvec[(int64_t)(step) * BK + tid];              \
+    vuk = uk_src[(int64_t)(step) * BK + (tid & (BK - 1))];                       \
   }
 #define CON_SSTORE(buf)                                                          \
   {                                                                              \
@@ -567,10 +578,10 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     pa_[0] = va0.x; pa_[1] = va0.y; pa_[2] = va1.x; pa_[3] = va1.y;              \
     pa_[4] = va2.x; pa_[5] = va2.y; pa_[6] = va3.x; pa_[7] = va3.y;              \
     pb_[0] = vb0; pb_[16] = vb1; pb_[32] = vb2; pb_[48] = vb3;                   \
-    if (with_u && tid < BK) s_uk[buf][tid] = vuk;                                \
+    s_uk[buf][tid & (BK - 1)] = vuk;   /* 16 lanes per address, one value */     \
   }
 #define CON_KU(buf)                                                              \
-  if (with_u) {                                                                  \
+  {                                                                              \
     const double* u_ = &s_uk[buf][acol];                                         \
     ku = fma(va0.x, u_[0], ku); ku = fma(va0.y, u_[1], ku);                      \
     ku = fma(va1.x, u_[2], ku); ku = fma(va1.y, u_[3], ku);                      \
@@ -599,7 +610,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   for (int step = 0; step < nsteps; ++step) {
     const int cur = step & 1;
     CON_KU(cur);   // va still holds this step's staged K values
-    if (step + 1 < nsteps) CON_GLOAD(step + 1);
+    CON_GLOAD(step + 1 < nsteps ? step + 1 : step);   // the last step reloads its own slice
     const double* As = lds + cur * (A_SZ + B_SZ);
     const double* Bs = As + A_SZ;
 #pragma unroll
@@ -617,7 +628,8 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
         for (int fn = 0; fn < 4; ++fn)
           acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
     }
-    if (step + 1 < nsteps) CON_SSTORE(cur ^ 1);
+    CON_SSTORE(cur ^ 1);   // on the last step into the idle buffer
+    mfma_interleave<true>();
     __syncthreads();
   }
   }   // !FROM_T
