@@ -137,7 +137,9 @@ __device__ __forceinline__ void mfma_desync(double seed) {
 // workgroups per CU, 60.3 -> 70.0 with one.  Needs the step to be a single basic block.
 // SPREAD: one LDS read per two MFMAs over the whole step (fragments read one sub-step ahead:
 // fewer live registers, for kernels whose epilogue shares the register budget).
-template <bool SPREAD = false>
+// PAT (experiments, tools/micro/con_trace.hip): where the LDS stores go (0: MFMA slots 48-55,
+// 2: 56-63, 3: 32-39, 4: not grouped)
+template <bool SPREAD = false, int PAT = 0>
 __device__ __forceinline__ void mfma_interleave() {
 #pragma unroll
   for (int i = 0; i < 64; ++i) {
@@ -145,9 +147,17 @@ __device__ __forceinline__ void mfma_interleave() {
     if (i < 8) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);           // VMEM read
     if (SPREAD ? (i & 1) == 0 : i < 32)
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                    // DS read
-    if (i >= 48 && i < 56) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+    constexpr int w0 = PAT == 2 ? 56 : PAT == 3 ? 32 : 48;
+    if (PAT != 4 && i >= w0 && i < w0 + 8)
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);                    // DS write
   }
 }
+#ifndef SGP_CON_IL_PAT
+#define SGP_CON_IL_PAT 2   // contraction: stores in the last MFMA slots (65.5 vs 64.5 TF/s)
+#endif
+#ifndef SGP_SYRK_IL_PAT
+#define SGP_SYRK_IL_PAT 0
+#endif
 
 // WEIGHTED: rows scaled by w (FITC / Laplace); compiled out for the unweighted VI SYRK, whose
 // k-loop otherwise multiplies every A fragment by 1.0 (16 fp64 VALU ops per 64 MFMAs).
@@ -306,7 +316,7 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
     }
     if constexpr (one_block) {
       SYRKB_SSTORE(cur ^ 1);
-      mfma_interleave();
+      mfma_interleave<false, SGP_SYRK_IL_PAT>();
     } else if (step + 1 < nsteps) {
       SYRKB_SSTORE(cur ^ 1);
     }
@@ -629,7 +639,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
           acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
     }
     CON_SSTORE(cur ^ 1);   // on the last step into the idle buffer
-    mfma_interleave<true>();
+    mfma_interleave<true, SGP_CON_IL_PAT>();
     __syncthreads();
   }
   }   // !FROM_T
