@@ -105,28 +105,6 @@ struct SyrkTMap {
   int S;                // slices per panel
 };
 
-// Every DESYNC_STEPS k-steps each wave of a long MFMA k-loop waits for its accumulators and
-// runs a short burst of fp32 FMAs on dead values (~1k VALU instructions, no memory traffic).
-// The two workgroups sharing a CU otherwise stay phase-locked -- their global loads, LDS
-// stores and barriers land on the same cycles -- and the burst, whose length depends on what
-// the partner is issuing, keeps them apart: tools/micro/kloop.hip (KLOOP_EPI=1) measures
-// MFMA busy 0.898 -> 0.930 of SIMD cycles at the same 2.38 GHz clock (70.0 -> 72.6 TF/s).
-constexpr int DESYNC_STEPS = 64;
-__device__ double g_desync_sink[256];   // written only if the burst's dead value hits 1234.5f
-__device__ __forceinline__ void mfma_desync(double seed) {
-  float v[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) v[c] = (float)seed + (float)c;   // waits for the accumulators
-  for (int e = 0; e < 128; ++e)
-#pragma unroll
-    for (int c = 0; c < 8; ++c) v[c] = fmaf(v[c], 0.999f, 1e-3f);
-  float t = 0.f;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) t += v[c];
-  // keeps the burst alive; the sink is never read, so the (rare) hit is harmless
-  if (t == 1234.5f) g_desync_sink[threadIdx.x & 255] = (double)t;
-}
-
 // Issue order of one k-step (64 MFMAs, 32 LDS fragment reads, 8 global loads, 8 LDS stores)
 // as a scheduling request: each MFMA is followed by at most one LDS read (the first 32), one
 // global load (the first 8) and, late in the step, one LDS store.  The compiler's own order
@@ -325,8 +303,6 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
       SYRKB_SSTORE(cur ^ 1);
     }
     __syncthreads();
-    if (DESYNC_STEPS > 0 && (step % DESYNC_STEPS) == DESYNC_STEPS - 1)
-      mfma_desync(acc[0][0][0] + acc[3][3][3]);
   }
 #undef SYRKB_GLOAD
 #undef SYRKB_SSTORE
