@@ -18,11 +18,15 @@ HEADERS = ["sgp_internal.h", os.path.join("..", "..", "include", "sgp.h")]
 ARCH = os.environ.get("SGP_OFFLOAD_ARCH", "gfx950")
 
 
+class HipccMissing(RuntimeError):
+    """No hipcc on this machine (the only case in which an existing library may be reused)."""
+
+
 def hipcc():
     for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
         if cand and os.path.exists(cand):
             return cand
-    raise RuntimeError("hipcc not found: cannot build libsgp.so")
+    raise HipccMissing("hipcc not found: cannot build libsgp.so")
 
 
 def _stale():

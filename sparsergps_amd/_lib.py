@@ -9,7 +9,7 @@ import ctypes as C
 import os
 import threading
 
-from ._build import LIB, build
+from ._build import LIB, HipccMissing, build
 
 _lock = threading.Lock()
 _lib = None
@@ -119,10 +119,11 @@ def lib(auto_build: bool = True):
             return _lib
         if auto_build:
             # rebuilds only when a source is newer than the library (a stale .so would
-            # otherwise be loaded silently); without hipcc the existing library is used
+            # otherwise be loaded silently).  Only a missing hipcc lets the existing library
+            # be used; a compile or link error always propagates.
             try:
                 build()
-            except RuntimeError:
+            except HipccMissing:
                 if not os.path.exists(LIB):
                     raise
         if not os.path.exists(LIB):

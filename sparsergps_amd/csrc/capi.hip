@@ -116,12 +116,45 @@ void set_exp_consts(KernParams* kp) {
 
 namespace {
 
-// kp->ctr = column means of the m x d knot matrix U (column-major, ld ldu; host memory)
-void set_center(KernParams* kp, const double* U, int64_t m, int64_t ldu) {
+// kp->ctr = column means of the m x d knot matrix U (column-major, ld ldu; host memory), and
+// kp->span2 = a bound on |x~|^2 over the knots and the data box [xlo, xhi] (per coordinate;
+// NULL = knots only) that the matrix-core builder's accuracy guard reads (knm_mfma_ok).
+void set_center(KernParams* kp, const double* U, int64_t m, int64_t ldu, const double* xlo,
+                const double* xhi) {
+  double span2 = 0.0;
   for (int c = 0; c < kp->d; ++c) {
-    double s = 0.0;
-    for (int64_t j = 0; j < m; ++j) s += U[j + c * ldu];
+    double s = 0.0, lo = U[c * ldu], hi = U[c * ldu];
+    for (int64_t j = 0; j < m; ++j) {
+      const double v = U[j + c * ldu];
+      s += v;
+      lo = v < lo ? v : lo;
+      hi = v > hi ? v : hi;
+    }
     kp->ctr[c] = m > 0 ? s / (double)m : 0.0;
+    if (xlo && xhi) {
+      lo = xlo[c] < lo ? xlo[c] : lo;
+      hi = xhi[c] > hi ? xhi[c] : hi;
+    }
+    const double e = fmax(fabs(lo - kp->ctr[c]), fabs(hi - kp->ctr[c])) * kp->rl[c];
+    span2 += e * e;
+  }
+  kp->span2 = span2 == span2 ? span2 : INFINITY;   // NaN coordinates: the VALU form
+}
+
+// column ranges of an n x d column-major host matrix
+void col_range(const double* X, int64_t n, int64_t ldx, int d, std::vector<double>* lo,
+               std::vector<double>* hi) {
+  lo->assign((size_t)d, 0.0);
+  hi->assign((size_t)d, 0.0);
+  for (int c = 0; c < d; ++c) {
+    double a = n > 0 ? X[c * ldx] : 0.0, b = a;
+    for (int64_t i = 1; i < n; ++i) {
+      const double v = X[i + c * ldx];
+      a = v < a ? v : a;
+      b = v > b ? v : b;
+    }
+    (*lo)[(size_t)c] = a;
+    (*hi)[(size_t)c] = b;
   }
 }
 
@@ -380,6 +413,15 @@ uint64_t coord_hash_host(const double* x, int64_t stride, int d) {
 }
 
 int upload_knots(sgp_ctx* c, const double* U, int64_t m, int64_t ldu) {
+  // An evaluation that was begun but never finished (an error between the phases) can leave
+  // the K22 chain (aux: writes status[0], sc[SC_LD22], reads U) and aux_lo work queued.  The
+  // new evaluation's knot upload and status / scalar resets on the main stream must not
+  // overtake it.
+  if (c->phase != 0) {
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_m3, 0));
+    c->phase = 0;
+  }
   // optimizer iterations with fixed knots (xu_opt = "fixed") pass the same U every time: keep
   // the resident copy and its hash table
   if (c->knots_valid && c->knots_mp == c->mp && (int64_t)c->hU.size() == m * c->d) {
@@ -438,7 +480,7 @@ int check_eval_args(sgp_ctx* c, int kernel, const double* theta, const double* U
     set_err("sigma and tau must be positive");
     return SGP_EINVAL;
   }
-  set_center(kp, U, m, ldu);
+  set_center(kp, U, m, ldu, c->xmin.data(), c->xmax.data());
   return SGP_OK;
 }
 
@@ -1994,7 +2036,11 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
     set_err("invalid sgp_predict arguments");
     return SGP_EINVAL;
   }
-  set_center(&kp, U, m, ldu);
+  {
+    std::vector<double> plo, phi;
+    col_range(x_pred, np, ldxp, d, &plo, &phi);
+    set_center(&kp, U, m, ldu, plo.data(), phi.data());
+  }
   if (method != SGP_PRED_VI && method != SGP_PRED_LAPLACE && method != SGP_PRED_FULL) {
     set_err("invalid prediction method %d", method);
     return SGP_EINVAL;

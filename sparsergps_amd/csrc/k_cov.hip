@@ -566,7 +566,7 @@ static hipError_t build_knm_range(const KernParams& kp, const double* X, int64_t
   if (kp.kernel == 2) return hipErrorInvalidValue;
   const int64_t ncb = mp / 128;   // 128 knot columns per block
   const bool ard = kp.kernel == 1;
-  if (kp.d <= 8) {
+  if (knm_mfma_ok(kp)) {
     // persistent: one residency round of workgroups, each walking its share of row blocks
     const int occ = r ? occ_t : occ_n;
     const int per_cu = wpc < occ ? wpc : occ;
@@ -614,7 +614,7 @@ static hipError_t build_knm_impl(const KernParams& kp, const double* X, int64_t 
                                  BUILD_WPC_SHARED, s);
   if (e != hipSuccess) return e;
   // the VALU builder's partial rows are indexed by row block
-  const int64_t slot0 = kp.d <= 8 ? s1 : shared_rb;
+  const int64_t slot0 = knm_mfma_ok(kp) ? s1 : shared_rb;
   e = build_knm_range(kp, X, ldx, n, U, ldu, m, mp, K, r, tslab, slot0, &s2, shared_rb, nrb,
                       BUILD_WPC_FULL, s);
   if (t_rows) *t_rows = slot0 + s2;

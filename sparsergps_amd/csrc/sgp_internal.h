@@ -56,6 +56,10 @@ struct KernParams {
   // Origin the K12 builder's GEMM-form exponent is centred on (the knots' mean; any point
   // gives the same K up to rounding -- centring keeps |x~|^2 + |u~|^2 small, see k_cov.hip)
   double ctr[SGP_MAXD];
+  // Upper bound on |x~|^2 over the knots and the rows the builder sees (x~ = (x - ctr) * rl):
+  // the GEMM-form exponent's absolute rounding is ~eps (|x~|^2 + |u~|^2), so above
+  // SGP_MFMA_SPAN2_MAX the direct-difference VALU builder is used instead (knm_mfma_ok).
+  double span2;
   double lsig2;          // log(sig2): folded into the builder's GEMM-form exponent
   // sgp_exp_kp's constants as kernel arguments, so they sit in SGPRs and each Horner step is
   // one v_fma_f64 (as literals the compiler pairs every step with a v_mov_b64): log2(e),
@@ -66,6 +70,13 @@ struct KernParams {
   double et[32];
 };
 void set_exp_consts(KernParams* kp);
+
+// |x~|^2 bound below which the matrix-core K12 builder keeps K within ~1e-12 relative of the
+// direct-difference form (1e4 * 2^-52 * a few); the C2 / C3 / C5 workloads sit below 100.
+constexpr double SGP_MFMA_SPAN2_MAX = 1.0e4;
+inline bool knm_mfma_ok(const KernParams& kp) {
+  return kp.d <= 8 && kp.kernel != 2 && kp.span2 <= SGP_MFMA_SPAN2_MAX;
+}
 
 // exp(x) for x already clamped to [-746, log(DBL_MAX)] by a 32-entry table: x = (32 e + j) ln2/32
 // + r, |r| <= ln2/64, exp(x) = 2^e T_j (1 + p(r)) with p the degree-6 Taylor polynomial of

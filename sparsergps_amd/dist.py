@@ -58,7 +58,7 @@ class HipRowBackend:
     finish; mode "laplace" (sgp_lap_*): begin -> sum -> step -> sum -> ... -> done."""
 
     def __init__(self, X_local, y_local, mu_local, m_max, device_index, cov_fun, mode="vi",
-                 knots=False):
+                 knots=False, group=None):
         import torch
 
         from .vi import SparseGPContext
@@ -82,8 +82,9 @@ class HipRowBackend:
             n2 += self.ctx.knot_red_extra(m_max)
         self.knots = knots
         # knot bounds of the whole data set (quirk Q9, vi_functions.R:175-178): every rank
-        # must use the same ones, so the per-rank column ranges are combined once here
-        self.knot_bounds = global_knot_bounds(X_local) if knots else None
+        # must use the same ones, so the per-rank column ranges are combined once here, over
+        # the same process group the sharded driver reduces over
+        self.knot_bounds = global_knot_bounds(X_local, group) if knots else None
         self.red1 = torch.zeros(n1, dtype=torch.float64, device=self.dev)
         self.red2 = torch.zeros(n2, dtype=torch.float64, device=self.dev)
         # A dedicated (non-null) stream shared by libsgp's launches and torch.distributed:

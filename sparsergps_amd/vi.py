@@ -372,8 +372,14 @@ def _fingerprint(a):
 def _context_for(xy, y, mu, m, mu_vec=None):
     """Reuse one device context per (xy, y, mu), like the reference driver reuses xy across
     iterations.  Arrays are keyed by identity plus a sampled fingerprint; a scalar mu (the
-    mean(y) default, quirk Q14) is keyed by value.  mu_vec: the mean actually uploaded."""
-    mu_key = ("scalar", float(mu)) if np.ndim(mu) == 0 else ("array", id(mu), _fingerprint(mu))
+    mean(y) default, quirk Q14) is keyed by value, mu=None by the path's default.  mu_vec: the
+    mean actually uploaded."""
+    if mu is None:                       # the path's own default (mean(y) / log mean(y))
+        mu_key = ("default",)
+    elif np.ndim(mu) == 0:
+        mu_key = ("scalar", float(mu))
+    else:
+        mu_key = ("array", id(mu), _fingerprint(mu))
     key = (id(xy), id(y), mu_key, _fingerprint(xy), _fingerprint(y))
     ent = _CTX_CACHE.get(key)
     if ent is not None and ent[0] is xy and ent[1] is y and ent[2].m_max >= m:

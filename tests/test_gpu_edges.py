@@ -270,3 +270,33 @@ def test_newtrap_small_maxit(sgp, maxit):
     assert len(rv) == len(ov) == (2 if maxit <= 2 else 3)
     assert np.max(np.abs(rv - ov) / np.abs(ov)) < 1e-9
     assert np.max(np.abs(r["gp"] - nr["gp"])) < 1e-8
+
+
+@pytest.mark.parametrize("mode", ["vi", "fitc"])
+@pytest.mark.parametrize("layout", ["offset", "wide"])
+def test_data_far_from_origin_or_widely_spread(sgp, mode, layout):
+    """The matrix-core K12 builder forms the exponent as x~.u~ - |x~|^2/2 - |u~|^2/2 around
+    the knots' mean, whose rounding grows with |x~|^2 (k_cov.hip).  "offset": data 5e3 away
+    from the origin (centring keeps the matrix-core form exact to ~1e-14); "wide": data spread
+    over ~300 length scales (|x~|^2 ~ 1e5, past SGP_MFMA_SPAN2_MAX: the direct-difference
+    builder runs instead).  Knots are data rows plus a small jitter so K12 is not all zeros."""
+    g = np.random.Generator(np.random.PCG64(91 if layout == "offset" else 92))
+    n, m, d = 1500, 40, 3 if layout == "offset" else 2
+    if layout == "offset":
+        X = 5.0e3 + g.uniform(0.0, 10.0, size=(n, d))
+        cp = OrderedDict([("sigma", 1.2), ("l", 1.7), ("tau", 0.5)])
+    else:
+        X = g.uniform(0.0, 400.0, size=(n, d))
+        cp = OrderedDict([("sigma", 1.2), ("l", 0.7), ("tau", 0.5)])
+    U = X[g.choice(n, m, replace=False)] + g.normal(0.0, 0.3, size=(m, d))
+    y = np.sin(X / 7.0).sum(axis=1) + g.normal(0.0, 0.5, size=n)
+    mu = np.full(n, y.mean())
+    if mode == "vi":
+        obj, grad = sgp.vi_eval(cp, "sqexp", U, X, y, mu, 1e-6)
+        o = O.elbo_eval(cp, "sqexp", U, X, y, mu, 1e-6)
+        gr = O.delbo_dcov_par(cp, "sqexp", U, X, y, mu, 1e-6)["gradient"]
+    else:
+        obj, grad = sgp.fitc_eval(cp, "sqexp", U, X, y, mu, 1e-6)
+        o = O.fitc_obj_eval(cp, "sqexp", U, X, y, mu, 1e-6)
+        gr = O.dlogp_dcov_par(cp, "sqexp", U, X, y, mu, 1e-6)["gradient"]
+    _close(obj, grad, o, gr, cp)

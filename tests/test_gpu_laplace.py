@@ -109,3 +109,20 @@ def test_laplace_larger_against_adjoint_model(sgp):
     assert abs(obj - o) / abs(o) < 1e-10
     assert np.max(np.abs(fg - f)) < 1e-9
     assert np.max(np.abs(grad - g) / np.maximum(1, np.abs(g))) < 1e-8
+
+
+def test_dlogq_mu_omitted_defaults_to_log_mean(sgp):
+    """mu=None (no ctx): the Laplace entry points fall back to log(mean(y))
+    (poisson-regression-vignette.Rmd:92), cached under their own context key."""
+    P = _problem(310, 22)
+    ff = P["f0"] + 0.05 * np.cos(np.arange(310))
+    res = sgp.dlogq_dcov_par(P["cov_par"], "sqexp", True, None, None, P["U"], P["X"], P["y"], ff,
+                             None, P["a"], P["delta"])
+    g = O.dlogq_dcov_par(P["cov_par"], "sqexp", P["U"], P["X"], P["y"], ff,
+                         np.full(310, np.log(P["y"].mean())), P["a"], P["delta"])["gradient"]
+    for k in P["cov_par"]:
+        assert abs(res["gradient"][k] - g[k]) / max(1.0, abs(g[k])) < EVAL_RTOL
+    o = sgp.obj_fun_pois(ff, P["cov_par"], "sqexp", P["U"], P["X"], P["y"], None, P["a"], P["delta"])
+    s12, s22, Z = O.laplace_mats(P["cov_par"], "sqexp", P["U"], P["X"], P["delta"])
+    o_ref = O.obj_fun_pois(ff, np.full(310, np.log(P["y"].mean())), Z, s12, s22, P["y"], P["a"])
+    assert abs(o - o_ref) / abs(o_ref) < 1e-10
