@@ -127,17 +127,19 @@ SEXP _sparseRGPs_pos_to_real(SEXP x) {
   return out;
 }
 
-/* real_to_bounded: covariance_function_derivativesC.cpp:25-28, (ub e^x + lb) / (e^x + 1);
- * Rcpp sugar sizes the result by x; ub and lb are recycled */
+/* real_to_bounded: covariance_function_derivativesC.cpp:25-28, (ub e^x + lb) / (e^x + 1).
+ * Rcpp sugar does not recycle: the expression's length is its leftmost operand's, ub, and
+ * element i reads x[i] and lb[i] (past their end when they are shorter -- undefined there, an
+ * R error here). */
 static double bounded(double x, double ub, double lb) { return (ub * exp(x) + lb) / (exp(x) + 1.0); }
 
 SEXP _sparseRGPs_real_to_bounded(SEXP x, SEXP ub, SEXP lb) {
   SEXP xr = PROTECT(as_real(x)), ur = PROTECT(as_real(ub)), lr = PROTECT(as_real(lb));
-  const R_xlen_t n = XLENGTH(xr), nu = XLENGTH(ur), nl = XLENGTH(lr);
-  if (n > 0 && (nu == 0 || nl == 0)) Rf_error("ub and lb must not be empty");
+  const R_xlen_t n = XLENGTH(ur);
+  if (XLENGTH(xr) < n || XLENGTH(lr) < n)
+    Rf_error("x and lb need at least length(ub) = %ld values", (long)n);
   SEXP out = PROTECT(Rf_allocVector(REALSXP, n));
-  for (R_xlen_t i = 0; i < n; ++i)
-    REAL(out)[i] = bounded(REAL(xr)[i], REAL(ur)[i % nu], REAL(lr)[i % nl]);
+  for (R_xlen_t i = 0; i < n; ++i) REAL(out)[i] = bounded(REAL(xr)[i], REAL(ur)[i], REAL(lr)[i]);
   UNPROTECT(4);
   return out;
 }
@@ -227,13 +229,14 @@ SEXP _sparseRGPs_dexp_dtauC(SEXP x1, SEXP x2, SEXP cov_par) {
 /* knot derivatives, covariance_function_derivativesC.cpp:175-226: per coordinate c
  *   (x1_c - x2_c) / l_c^2 * k(x1, x2) * dx2/dtx2_c,  tx2 = log((x2 - lb) / (ub - x2)),
  *   dx2/dtx2 = e^tx2 (ub - lb) / (e^tx2 + 1)^2;  trans_par = tx2,
- *   inv_trans_par = real_to_bounded(x2, ub, lb) */
+ *   inv_trans_par = real_to_bounded(x2, ub, lb).  Every sugar expression there has x2's length
+ *   d and reads lb[c], ub[c] for c < d (no recycling): lb and ub need at least d values. */
 static SEXP knot_deriv(int kernel, SEXP x1, SEXP x2, SEXP cov_par, SEXP lb, SEXP ub, SEXP lnames) {
   Pair p = pair_of(x1, x2);
   SEXP lr = PROTECT(as_real(lb)), ur = PROTECT(as_real(ub));
   const int d = p.d, ard = kernel == SGP_KERNEL_ARD;
   if (d < 1 || d > 32) Rf_error("input dimension %d outside [1, 32]", d);
-  if (Rf_length(lr) < 1 || Rf_length(ur) < 1) Rf_error("lb and ub must not be empty");
+  if (Rf_length(lr) < d || Rf_length(ur) < d) Rf_error("lb and ub need at least %d values", d);
   double theta[40];
   theta_from(cov_par, ard, lnames, d, 0, theta);
   const double k = sgp_kernel_pair(kernel, REAL(p.a), REAL(p.b), d, theta);
@@ -241,9 +244,8 @@ static SEXP knot_deriv(int kernel, SEXP x1, SEXP x2, SEXP cov_par, SEXP lb, SEXP
   SEXP dv = PROTECT(Rf_allocVector(REALSXP, d));
   SEXP tr = PROTECT(Rf_allocVector(REALSXP, d));
   SEXP iv = PROTECT(Rf_allocVector(REALSXP, d));
-  const int nl = Rf_length(lr), nu = Rf_length(ur);
   for (int c = 0; c < d; ++c) {
-    const double x2c = REAL(p.b)[c], lbc = REAL(lr)[c % nl], ubc = REAL(ur)[c % nu];
+    const double x2c = REAL(p.b)[c], lbc = REAL(lr)[c], ubc = REAL(ur)[c];
     const double l = ard ? theta[1 + c] : theta[1];
     const double t = log((x2c - lbc) / (ubc - x2c));
     const double et = exp(t);

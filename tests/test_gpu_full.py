@@ -1,7 +1,8 @@
 """GPU parity for the full (non-sparse) Gaussian GP, config 1:
 sgp_eval_full vs obj_fun_norm_full / dlogp_dcov_par_full, predict_gp_full, and the
 norm_grad_ascent_full trajectory, against the oracle.  The boston.R data file is absent
-(SURVEY F-notes); the shapes follow it (n = 392 rows, d = 3) with synthetic values."""
+(SURVEY F-notes); two shapes with synthetic values: boston.R's real selection (n = 392 rows,
+d = 3, exec/boston.R:80) and the shape BASELINE.json configs[0] states (n = 506, d = 13)."""
 from collections import OrderedDict
 
 import numpy as np
@@ -31,11 +32,25 @@ def _data(n=392, d=3, seed=31, dup=True):
     return X, y, np.full(n, y.mean())
 
 
+def _cov_par(cov_fun, d):
+    if d == 3:
+        return (OrderedDict(sigma=1.3, l=1.7, tau=0.45) if cov_fun == "sqexp" else
+                OrderedDict(sigma=1.1, l1=1.2, l2=2.2, l3=0.9, tau=0.35))
+    # d = 13: length scales wide enough that K is far from its diagonal in 13 dimensions
+    if cov_fun == "sqexp":
+        return OrderedDict(sigma=1.3, l=5.5, tau=0.45)
+    cp = OrderedDict(sigma=1.1)
+    for c in range(d):
+        cp[f"l{c + 1}"] = 4.0 + 0.4 * c
+    cp["tau"] = 0.35
+    return cp
+
+
+@pytest.mark.parametrize("n,d", [(392, 3), (506, 13)])
 @pytest.mark.parametrize("cov_fun", ["sqexp", "ard"])
-def test_full_eval_matches_oracle(sgp, cov_fun):
-    X, y, mu = _data()
-    cp = (OrderedDict(sigma=1.3, l=1.7, tau=0.45) if cov_fun == "sqexp" else
-          OrderedDict(sigma=1.1, l1=1.2, l2=2.2, l3=0.9, tau=0.35))
+def test_full_eval_matches_oracle(sgp, cov_fun, n, d):
+    X, y, mu = _data(n=n, d=d)
+    cp = _cov_par(cov_fun, d)
     obj, g = sgp.full_eval(cp, cov_fun, X, y, mu)
     ro = O.full_obj_eval(cp, cov_fun, X, y, mu)
     rg = O.dlogp_dcov_par_full(cp, cov_fun, X, y, mu)["gradient"]
