@@ -62,7 +62,29 @@ def cpu_info():
     except OSError:
         pass
     return {"model": model, "logical_cpus": len(allowed),
-            "physical_cores": len(cores) or None}
+            "physical_cores": len(cores) or None, **cpu_quota()}
+
+
+def cpu_quota():
+    """The CPU share this process may use: the cgroup CPU quota (v2 cpu.max, or v1
+    cfs_quota_us / cfs_period_us) and OMP_NUM_THREADS, which the GPU boxes set to that share.
+    On those boxes affinity and /proc/cpuinfo show the whole host, not the share."""
+    raw, cpus = None, None
+    try:
+        raw = open("/sys/fs/cgroup/cpu.max").read().strip()
+        q, _, per = raw.partition(" ")
+        if q != "max":
+            cpus = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            raw = f"cfs_quota_us={q} cfs_period_us={per}"
+            cpus = q / per if q > 0 else None
+        except (OSError, ValueError):
+            pass
+    return {"cgroup_cpu_max": raw, "cgroup_quota_cpus": cpus,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def _blas_threads():
@@ -84,6 +106,9 @@ def _time_literal(ns, m, threads=None):
 
 
 def _fit(sizes, ts, n_target):
+    """Least squares t(n) = a + b n; with >= 3 sizes the residual tests the linear model."""
+    if len(sizes) < 3:
+        raise ValueError("the linear fit needs at least three sizes to have a residual")
     A = np.vstack([np.ones(len(sizes)), np.asarray(sizes, dtype=np.float64)]).T
     (a, b), *_ = np.linalg.lstsq(A, np.asarray(ts), rcond=None)
     resid = A @ np.array([a, b]) - np.asarray(ts)
@@ -122,8 +147,9 @@ def adjoint_direct(n=1_000_000, m=1024, chunk=8192):
                       f"(no extrapolation)"}
 
 
-def cpu_baseline(sizes=(4000, 8000), n_target=1_000_000, m=1024, full=None):
-    """cpu_baseline of the bench line (bounded: ~30-60 s of host time)."""
+def cpu_baseline(sizes=(2000, 5000, 8000), n_target=1_000_000, m=1024, full=None):
+    """cpu_baseline of the bench line (bounded: ~30-60 s of host time): a three-point fit of
+    the literal port plus the adjoint bar timed directly at the full n."""
     lit = literal_port(sizes, n_target, m)
     out = {
         "value": lit["value"],
@@ -145,12 +171,13 @@ def cpu_baseline(sizes=(4000, 8000), n_target=1_000_000, m=1024, full=None):
 
 
 def cpu_baseline_full(n_target=1_000_000, m=1024):
-    """SURVEY 8(d)'s whole CPU plan: the literal port on all cores at n in {1e4, 2e4, 5e4} and
-    on one core at n in {2500, 5000, 1e4}, plus the adjoint bar timed directly at n = 1e6
-    (several minutes of host time: `python bench.py --cpu-full`)."""
-    allc = literal_port((10_000, 20_000, 50_000), n_target, m)
+    """SURVEY 8(d)'s whole CPU plan: the literal port on every CPU of this process's quota
+    (BLAS threads = the share, see cpu_quota) at n in {1e4, 2e4, 5e4} and on one core at n in
+    {2500, 5000, 1e4}, plus the adjoint bar timed directly at n = 1e6 (several minutes of host
+    time: `python bench.py --cpu-full`)."""
+    share = literal_port((10_000, 20_000, 50_000), n_target, m)
     one = literal_port((2_500, 5_000, 10_000), n_target, m, threads=1)
-    return {"cpu": cpu_info(), "literal_all_cores": allc, "literal_one_core": one,
+    return {"cpu": cpu_info(), "literal_quota_cores": share, "literal_one_core": one,
             "adjoint_direct": adjoint_direct(n_target, m)}
 
 
@@ -368,14 +395,14 @@ def main():
         if (world == 1 and not args.no_cpu_baseline and args.mode == "vi"
                 and args.config == "C3" and n == 1_000_000):
             full = None
-            fp = os.path.join(ROOT, "profiles", "r2_cpu_baseline_full.json")
+            fp = os.path.join(ROOT, "profiles", "r3_cpu_baseline_full.json")
             if os.path.exists(fp):
                 rec = json.load(open(fp))
-                full = {"source": "profiles/r2_cpu_baseline_full.json (bench.py --cpu-full on a "
+                full = {"source": "profiles/r3_cpu_baseline_full.json (bench.py --cpu-full on a "
                                   "GPU box's host, committed; not re-measured by this run)",
                         "cpu": rec["cpu"],
-                        "literal_all_cores": {k: rec["literal_all_cores"][k] for k in
-                                              ("value", "sizes", "t_s", "fit", "threads")},
+                        "literal_quota_cores": {k: rec["literal_quota_cores"][k] for k in
+                                                ("value", "sizes", "t_s", "fit", "threads")},
                         "literal_one_core": {k: rec["literal_one_core"][k] for k in
                                              ("value", "sizes", "t_s", "fit", "threads")},
                         "adjoint_direct": rec["adjoint_direct"]["value"]}

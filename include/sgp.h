@@ -156,6 +156,11 @@ int sgp_fitc_finish(sgp_ctx* ctx, const double* red2, double* obj, double* grad)
  * maxit = 0 skips the NR loop: objective and dlogq_dcov_par at the resident f as given. */
 int sgp_lap_set_f(sgp_ctx* ctx, const double* f /* n host values, or NULL */, double fill);
 int sgp_lap_get_f(sgp_ctx* ctx, double* f /* n host values */);
+/* grad psi of the last Newton-Raphson step (n host values): the `gradient` element
+ * newtrap_sparseGP returns (R/newtrap_sparseGP.R:183-184) -- evaluated at the mode estimate
+ * that step started from, as the reference's loop leaves it.  SGP_EINVAL when no NR step has
+ * run since sgp_lap_set_f (or since OAT candidate scoring). */
+int sgp_lap_get_grad_psi(sgp_ctx* ctx, double* grad_psi);
 /* objective_function_values of the last NR run (first min(count, max_n) copied; *count = all) */
 int sgp_lap_objective_values(sgp_ctx* ctx, double* out, int max_n, int* count);
 int sgp_eval_laplace(sgp_ctx* ctx, int kernel, const double* theta, const double* U, int64_t m,

@@ -537,6 +537,15 @@ SEXP sgp_R_lap_get_f(SEXP ctx) {
   return f;
 }
 
+/* grad psi of the last NR step: newtrap_sparseGP's `gradient` (newtrap_sparseGP.R:183-184) */
+SEXP sgp_R_lap_get_grad_psi(SEXP ctx) {
+  sgp_ctx* c = ctx_of(ctx);
+  SEXP g = PROTECT(Rf_allocVector(REALSXP, (R_xlen_t)sgp_ctx_rows(c)));
+  check(sgp_lap_get_grad_psi(c, REAL(g)));
+  UNPROTECT(1);
+  return g;
+}
+
 /* objective_function_values of the last NR run */
 SEXP sgp_R_lap_objective_values(SEXP ctx) {
   sgp_ctx* c = ctx_of(ctx);
@@ -679,6 +688,7 @@ static const R_CallMethodDef CallEntries[] = {
     {"sgp_R_lap_set_f", (DL_FUNC)&sgp_R_lap_set_f, 2},
     {"sgp_R_lap_get_f", (DL_FUNC)&sgp_R_lap_get_f, 1},
     {"sgp_R_lap_objective_values", (DL_FUNC)&sgp_R_lap_objective_values, 1},
+    {"sgp_R_lap_get_grad_psi", (DL_FUNC)&sgp_R_lap_get_grad_psi, 1},
     {"sgp_R_enable_knot_grad", (DL_FUNC)&sgp_R_enable_knot_grad, 2},
     {"sgp_R_knot_gradient", (DL_FUNC)&sgp_R_knot_gradient, 4},
     {"sgp_R_posterior_u", (DL_FUNC)&sgp_R_posterior_u, 2},

@@ -62,6 +62,7 @@ PROTOTYPES = {
     "sgp_fitc_finish": (C.c_int, [C.c_void_p, C.c_void_p, c_double_p, c_double_p]),
     "sgp_lap_set_f": (C.c_int, [C.c_void_p, c_double_p, C.c_double]),
     "sgp_lap_get_f": (C.c_int, [C.c_void_p, c_double_p]),
+    "sgp_lap_get_grad_psi": (C.c_int, [C.c_void_p, c_double_p]),
     "sgp_lap_objective_values": (C.c_int, [C.c_void_p, c_double_p, C.c_int, c_int_p]),
     "sgp_eval_laplace": (C.c_int, [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_int64,
                                    C.c_int64, C.c_double, C.c_double, C.c_double, C.c_int,

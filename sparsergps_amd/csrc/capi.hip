@@ -233,6 +233,7 @@ struct sgp_ctx {
   // Poisson-Laplace state (row/knot vectors allocated on first use)
   double *y = nullptr, *mu = nullptr;     // per-row data (n_pad), kept for the Laplace path
   double* lv = nullptr;                   // LV_N x n_pad row vectors
+  bool lap_gpsi_valid = false;            // LV_GPSI holds the last NR step's grad psi
   double* lm = nullptr;                   // LM_N x mp_max knot vectors
   double* lslab = nullptr;                // K^T V row-chunk partials
   double* Cprev = nullptr;                // (K22 + S_B)^-1 of the previous NR iterate
@@ -1475,7 +1476,7 @@ int sgp_eval_fitc(sgp_ctx* c, int kernel, const double* theta, const double* U, 
 //   FIN     : G22 contraction, gradient
 enum { LS_NONE = 0, LS_OBJ0, LS_NRB, LS_OBJ, LS_GRADB, LS_FIN };
 enum { LV_F = 0, LV_Z, LV_ZI, LV_B, LV_RF, LV_TV, LV_OMZW, LV_Y1, LV_Y2, LV_DMT, LV_SV, LV_H,
-       LV_A, LV_V, LV_P, LV_C2, LV_G, LV_BSV, LV_N };   // C2, G, BSV adjacent (one K^T pass)
+       LV_A, LV_V, LV_P, LV_C2, LV_G, LV_BSV, LV_GPSI, LV_N };   // C2, G, BSV adjacent (one K^T pass)
 enum { LM_X1 = 0, LM_X2, LM_S, LM_GG, LM_NGG, LM_CW, LM_N };
 
 static double* lvec(sgp_ctx* c, int k) { return c->lv + (int64_t)k * c->n_pad; }
@@ -1515,6 +1516,19 @@ int sgp_lap_set_f(sgp_ctx* c, const double* f, double fill) {
   for (int64_t i = 0; i < c->n; ++i) h[(size_t)i] = f ? f[i] : fill;
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipMemcpy(lvec(c, LV_F), h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice));
+  c->lap_gpsi_valid = false;
+  return SGP_OK;
+}
+
+int sgp_lap_get_grad_psi(sgp_ctx* c, double* out) {
+  if (!c || !out) { set_err("invalid arguments"); return SGP_EINVAL; }
+  if (!c->lap_gpsi_valid) {
+    set_err("no Newton-Raphson step has run since the mode was last set");
+    return SGP_EINVAL;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(out, lvec(c, LV_GPSI), sizeof(double) * c->n, hipMemcpyDeviceToHost));
   return SGP_OK;
 }
 
@@ -1681,7 +1695,9 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
       int nb = 0;
       HIPCHK(launch_lap_nr_a(n, n_pad, lvec(c, LV_F), c->y, c->mu, lvec(c, LV_Z), lvec(c, LV_ZI),
                              c->lap_expo, lvec(c, LV_Y1), c->lap_tol, lvec(c, LV_G),
-                             lvec(c, LV_OMZW), lvec(c, LV_V), c->slab_small, &nb, c->stream));
+                             lvec(c, LV_OMZW), lvec(c, LV_V), lvec(c, LV_GPSI), c->slab_small,
+                             &nb, c->stream));
+      c->lap_gpsi_valid = true;
       HIPCHK(launch_gemv_cols(c->K, n_pad, mp, lvec(c, LV_V), n_pad, 1, c->lslab, c->lslab_cap,
                               red_out, c->stream));
       HIPCHK(launch_colsum(c->slab_small, nb, 1, red_out + mp, c->stream));
@@ -2360,6 +2376,7 @@ int sgp_lap_candidates(sgp_ctx* c, int kernel, const double* theta, const double
                         c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   c->last_mode = 0;   // the context's posterior state belongs to the last candidate
+  c->lap_gpsi_valid = false;
   return st;
 }
 

@@ -86,7 +86,8 @@ __global__ void __launch_bounds__(256) k_lap_obj(int64_t n, int64_t n_pad,
 
 // NR step, part a (grad_loglik_fn_pois + the first half of newtrap_sparseGP_update):
 //   g = y - a e^f, omzw = 1 - Z W, gpsi = g - (rf - y1)/Z   (y1 = K Bm_Z^-1 t_Z),
-//   v = gpsi / omzw (input of the K^T pass), slab = [#{|gpsi_i| > tol}].
+//   v = gpsi / omzw (input of the K^T pass), slab = [#{|gpsi_i| > tol}]; gpsi itself is kept
+//   (newtrap_sparseGP's returned `gradient`, R/newtrap_sparseGP.R:178-185).
 __global__ void __launch_bounds__(256) k_lap_nr_a(int64_t n, int64_t n_pad,
                                                   const double* __restrict__ f,
                                                   const double* __restrict__ y,
@@ -96,6 +97,7 @@ __global__ void __launch_bounds__(256) k_lap_nr_a(int64_t n, int64_t n_pad,
                                                   const double* __restrict__ y1, double tol,
                                                   double* __restrict__ g, double* __restrict__ omzw,
                                                   double* __restrict__ v,
+                                                  double* __restrict__ gpsi,
                                                   double* __restrict__ slab) {
   double acc[1] = {0.0};
   ROW_LOOP(i) {
@@ -109,11 +111,13 @@ __global__ void __launch_bounds__(256) k_lap_nr_a(int64_t n, int64_t n_pad,
       g[i] = gi;
       omzw[i] = om;
       v[i] = (1.0 / om) * gp;
+      gpsi[i] = gp;
       if (fabs(gp) > tol) acc[0] += 1.0;
     } else {
       g[i] = 0.0;
       omzw[i] = 1.0;
       v[i] = 0.0;
+      gpsi[i] = 0.0;
     }
   }
   block_store_sums<1>(acc, slab);
@@ -415,11 +419,11 @@ hipError_t launch_lap_obj(int64_t n, int64_t n_pad, const double* f, const doubl
 hipError_t launch_lap_nr_a(int64_t n, int64_t n_pad, const double* f, const double* y,
                            const double* mu, const double* Z, const double* zinv, double expo,
                            const double* y1, double tol, double* g, double* omzw, double* v,
-                           double* slab, int* nblocks, hipStream_t s) {
+                           double* gpsi, double* slab, int* nblocks, hipStream_t s) {
   const int nb = row_blocks(n_pad);
   *nblocks = nb;
   hipLaunchKernelGGL(k_lap_nr_a, dim3(nb), dim3(256), 0, s, n, n_pad, f, y, mu, Z, zinv, expo, y1,
-                     tol, g, omzw, v, slab);
+                     tol, g, omzw, v, gpsi, slab);
   return hipGetLastError();
 }
 

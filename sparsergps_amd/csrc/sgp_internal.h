@@ -277,7 +277,7 @@ hipError_t launch_lap_obj(int64_t n, int64_t n_pad, const double* f, const doubl
 hipError_t launch_lap_nr_a(int64_t n, int64_t n_pad, const double* f, const double* y,
                            const double* mu, const double* Z, const double* zinv, double expo,
                            const double* y1, double tol, double* g, double* omzw, double* v,
-                           double* slab, int* nblocks, hipStream_t s);
+                           double* gpsi, double* slab, int* nblocks, hipStream_t s);
 hipError_t launch_lap_nr_b(int64_t n, int64_t n_pad, double* f, const double* mu, const double* Z,
                            const double* g, const double* omzw, const double* y1,
                            const double* y2, hipStream_t s);

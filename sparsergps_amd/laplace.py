@@ -77,12 +77,14 @@ def _lap_ctx(cov_par, cov_fun, xu, xy, y, mu, ctx):
 def newtrap_sparseGP(start_vals, cov_par, cov_fun, xy, xu, y, mu, m=1.0, delta=1e-6,
                      maxit=1000, tol=1e-6, ctx=None):
     """R/newtrap_sparseGP.R:6-186 for the Poisson likelihood: {"gp",
-    "objective_function_values"} (sgp_lap_nr: the NR loop alone, no gradient work)."""
+    "objective_function_values", "gradient"} (sgp_lap_nr: the NR loop alone, no gradient work;
+    "gradient" is grad psi of the last NR step, as the reference returns it, l.183-184)."""
     ctx, theta, xu_m = _lap_ctx(cov_par, cov_fun, xu, xy, y, mu, ctx)
     if start_vals is not None:
         ctx.lap_set_f(start_vals)
     ctx.lap_nr(theta, cov_fun, xu_m, delta, m, tol, max(int(maxit), 1))   # first update always
-    return {"gp": ctx.lap_get_f(), "objective_function_values": ctx.lap_objective_values()}
+    return {"gp": ctx.lap_get_f(), "objective_function_values": ctx.lap_objective_values(),
+            "gradient": ctx.lap_get_grad_psi()}
 
 
 def dlogq_dcov_par(cov_par, cov_fun, dcov_fun_dtheta=True, dcov_fun_dknot=None, knot_opt=None,

@@ -206,6 +206,12 @@ class SparseGPContext:
         _lib.check(self._lib.sgp_lap_get_f(self.handle, _lib.dptr(f)))
         return f
 
+    def lap_get_grad_psi(self):
+        """grad psi of the last NR step (newtrap_sparseGP's `gradient`)."""
+        g = np.zeros(self.n, dtype=np.float64)
+        _lib.check(self._lib.sgp_lap_get_grad_psi(self.handle, _lib.dptr(g)))
+        return g
+
     def lap_objective_values(self):
         cnt = C.c_int(0)
         _lib.check(self._lib.sgp_lap_objective_values(self.handle, None, 0, C.byref(cnt)))

@@ -1,6 +1,6 @@
 """Generate tests/golden/rcpp_registry.json from the reference (run where /root/reference is
 present): the .Call registry of src/RcppExports.cpp (routine name, arity, in order) and the
-formals of the six R hot-path functions the R shim replaces.  Interface data only (names,
+formals of the R hot-path functions and drivers the R shim replaces.  Interface data only (names,
 arities, argument lists); tests/test_rshim.py checks rshim/ against it."""
 import json
 import os
@@ -17,6 +17,10 @@ FUNCS = {
     "dlogp_dcov_par": "R/laplace_approx_gradient.R",
     "newtrap_sparseGP": "R/newtrap_sparseGP.R",
     "dlogq_dcov_par": "R/laplace_approx_gradient.R",
+    "norm_grad_ascent_vi": "R/vi_functions.R",
+    "norm_grad_ascent": "R/laplace_gradient_ascent.R",
+    "laplace_grad_ascent": "R/laplace_gradient_ascent.R",
+    "predict_gp": "R/laplace_approx_prediction.R",
 }
 
 

@@ -58,6 +58,26 @@ def test_laplace_matches_oracle(sgp, n, m, cov_fun, coinc):
         assert abs(r["gradient"][k] - g[k]) / max(1.0, abs(g[k])) < EVAL_RTOL, (k, r["gradient"][k], g[k])
 
 
+@pytest.mark.parametrize("maxit", [2, 1000])
+def test_newtrap_returns_grad_psi(sgp, maxit):
+    """newtrap_sparseGP's `gradient` element: grad psi of the last NR step, i.e. at the f that
+    step started from (R/newtrap_sparseGP.R:97-104, 183-184).  maxit = 2 stops after the first
+    update (grad psi at f0, O(1) values); maxit = 1000 runs to the stop rule."""
+    P = _problem(300, 20)
+    nr = O.newtrap_sparseGP(P["f0"], P["cov_par"], "sqexp", P["X"], P["U"], P["y"], P["mu"],
+                            P["a"], P["delta"], maxit=maxit, tol=1e-5)
+    got = sgp.newtrap_sparseGP(P["f0"], P["cov_par"], "sqexp", P["X"], P["U"], P["y"], P["mu"],
+                               P["a"], P["delta"], maxit=maxit, tol=1e-5)
+    assert len(got["objective_function_values"]) == len(nr["objective_function_values"])
+    g_ref = nr["gradient"]
+    if maxit == 2:
+        assert np.max(np.abs(g_ref)) > 0.1
+        np.testing.assert_allclose(got["gradient"], g_ref, rtol=1e-9, atol=1e-12)
+    else:
+        # at the mode: |grad psi| <= tol, compared absolutely (f agrees to ~1e-9)
+        assert np.max(np.abs(got["gradient"] - g_ref)) < 1e-8
+
+
 def test_dlogq_and_obj_at_given_ff(sgp):
     """maxit = 0: no NR step, the gradient and objective at the supplied f (not a mode)."""
     P = _problem(320, 24)

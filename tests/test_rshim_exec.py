@@ -56,7 +56,7 @@ def _err(R, name, *args):
 # ------------------------------------------------------------------------------ CPU
 def test_registration(R):
     fix = json.load(open(os.path.join(GOLD, "rcpp_registry.json")))
-    assert R.n_routines == 34          # 20 reference routines + 14 fused
+    assert R.n_routines == 35          # 20 reference routines + 15 fused
     assert [tuple(e) for e in R.routines[:20]] == [tuple(e) for e in fix["call_entries"]]
     assert R.L.mock_dynamic_symbols() == 0             # R_useDynamicSymbols(dll, FALSE)
 
@@ -295,11 +295,18 @@ def test_laplace_routines(gR):
     np.testing.assert_allclose(out["gradient"], z["grad"], rtol=1e-6, atol=1e-8)
     np.testing.assert_allclose(R.call("sgp_R_lap_objective_values", ctx).py(), tr, rtol=1e-9)
     np.testing.assert_allclose(R.call("sgp_R_lap_get_f", ctx).py(), z["ff"], rtol=1e-7, atol=1e-9)
-    # NR alone (want_grad = FALSE) from a scalar start value
+    # NR alone (want_grad = FALSE) from a scalar start value; no grad psi before an NR step
     R.call("sgp_R_lap_set_f", ctx, float(z["f0"][0]))
+    assert "no Newton-Raphson step" in _err(R, "sgp_R_lap_get_grad_psi", ctx)
     nr = R.call("sgp_R_eval_laplace", ctx, "sqexp", th, U, delta, a, 1e-5, 1000.0,
                 R.lgl(False)).py()
     assert abs(nr["objective"][0] - tr[-1]) <= 1e-8 * abs(tr[-1])
+    # newtrap_sparseGP's `gradient`: grad psi of the last NR step, against the oracle's loop
+    nr_ref = O.newtrap_sparseGP(z["f0"], dict(zip([str(s) for s in z["names"]], th)), "sqexp",
+                                X, U, y, mu, a, delta, tol=1e-5)
+    gp = R.call("sgp_R_lap_get_grad_psi", ctx).py()
+    assert gp.shape == (X.shape[0],)
+    assert np.max(np.abs(gp - nr_ref["gradient"])) < 1e-8
     assert "length 1 or one value" in _err(R, "sgp_R_lap_set_f", ctx, z["f0"][:3])
     # Poisson OAT candidate scoring: newtrap at [U; cand_t] from the resident mode
     cand = np.random.default_rng(4).uniform(0, 10, (2, X.shape[1]))
@@ -360,12 +367,12 @@ def test_full_gp_routine(gR):
 @pytest.mark.gpu
 def test_every_device_routine_ran(gR):
     """Runs last in this module (pytest keeps file order): after the GPU tests above every
-    registered routine that needs the device -- the four matrix fillers and the 14 fused
+    registered routine that needs the device -- the four matrix fillers and the 15 fused
     routines -- has been called through mock_call (the 16 host-only per-pair / transform
     routines are covered by test_every_host_routine_ran on the CPU)."""
     if len(_GPU_DONE) < 5:
         pytest.skip("only a subset of this module's GPU tests ran")
     dev = [n for n, _ in gR.routines if n.startswith("sgp_R_") or "cov_mat" in n or "dsig_" in n]
-    assert len(dev) == 18
+    assert len(dev) == 19
     missing = [n for n in dev if n not in gR.called]
     assert not missing, missing
