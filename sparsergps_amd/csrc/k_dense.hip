@@ -10,6 +10,7 @@
 #include <stdlib.h>
 
 #include "sgp_internal.h"
+#include "sgp_probe.h"
 
 namespace {
 
@@ -275,12 +276,8 @@ __global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
   double* S1 = lds + 64 * GJ_LS;
   const int i = blockIdx.y, j = blockIdx.x;
   const int64_t oi = (int64_t)i * 64, oj = (int64_t)j * 64, ok = (int64_t)k * 64;
-#ifdef SGP_GJ_TRACE   // timing probe only (tools/micro/gj_trace.hip): look-ahead WG stamps
-  const bool gj_tr = (i == k + 1) && (j == k + 1) && threadIdx.x == 0;
-#define GJ_STAMP(p_) do { if (gj_tr) SGP_GJ_TRACE(k, p_); } while (0)
-#else
-#define GJ_STAMP(p_) do { } while (0)
-#endif
+  SGP_PROBE_GJ_DECL();   // timing probe hooks (sgp_probe.h): empty in the product
+#define GJ_STAMP(p_) SGP_PROBE_GJ_STAMP(p_)
   GJ_STAMP(0);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int wr = wv >> 1, wc = wv & 1;

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "sgp_internal.h"
+#include "sgp_probe.h"
 
 namespace {
 
@@ -579,9 +580,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     ku = fma(va3.x, u_[6], ku); ku = fma(va3.y, u_[7], ku);                      \
   }
 
-#ifdef SGP_CON_TRACE
-  if (tid == 0) SGP_CON_TRACE(0);
-#endif
+  SGP_PROBE_CON_STAMP(0);
   if constexpr (FROM_T) {
     // the product tile T = K M was stored by an earlier row-quadratic pass over the same K and
     // M (launch_rowquad_knm with tstore): read it instead of recomputing 2 n m^2 flops
@@ -630,20 +629,8 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
 #undef CON_SSTORE
 #undef CON_KU
 
-#ifdef SGP_CON_TRACE
-  if (tid == 0) SGP_CON_TRACE(1);
-#endif
-#ifdef SGP_CON_NO_EPILOGUE
-  if constexpr (EPI == EPI_GRAD) {   // timing probe only: k-loop cost without the epilogue
-    double v = 0.0;
-#pragma unroll
-    for (int fm = 0; fm < 4; ++fm)
-#pragma unroll
-      for (int fn = 0; fn < 4; ++fn) v += acc[fm][fn][0] + acc[fm][fn][3];
-    if (v == 1234.5) slab[tid] = v;
-    return;
-  }
-#endif
+  SGP_PROBE_CON_STAMP(1);
+  SGP_PROBE_CON_SKIP_EPILOGUE()   // timing probe hook (sgp_probe.h): empty in the product
   // ---------------- alpha (per row), shared by both epilogues ----------------
   double* s_alpha = lds;                    // 128
   double* s_rs = s_alpha + T128;            // 128
@@ -777,9 +764,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
       __syncthreads();
       s_kn = kst;                               // KNOT: [2 (wr)][128 cols][8] per chunk
                                                 // (aliases the K stage, after its last use)
-#ifdef SGP_CON_TRACE
-      if (tid == 0) SGP_CON_TRACE(4);
-#endif
+      SGP_PROBE_CON_STAMP(4);
 
       d4 P[4];
       double Cc[4], ucol[4], vcol[4];
@@ -828,16 +813,12 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
 #pragma unroll
           for (int fn = 0; fn < 4; ++fn)
             P[fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[fm][fn][r4], xb[r4], P[fn], 0, 0, 0);
-#ifdef SGP_CON_TRACE
-        if (fm == 0 && tid == 0) SGP_CON_TRACE(3);
-#endif
+        if (fm == 0) SGP_PROBE_CON_STAMP(3);
         __syncthreads();                        // everyone is done reading the stage
         if (fm < 3) { CON_KSTAGE(fm + 1); }
       }
 #undef CON_KSTAGE
-#ifdef SGP_CON_TRACE
-      if (tid == 0) SGP_CON_TRACE(5);
-#endif
+      SGP_PROBE_CON_STAMP(5);
       // D fragment fn: lane l, register q -> column wc*64 + fn*16 + (l>>4) + 4q, c' = l & 15
       const int cp = lane & 15, cc = cp & 7;
 #pragma unroll
@@ -909,9 +890,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
 #undef CON_XSTAGE
     }
 
-#ifdef SGP_CON_TRACE
-    if (tid == 0) SGP_CON_TRACE(6);
-#endif
+    SGP_PROBE_CON_STAMP(6);
     // record = [e_sig, e_l[0..L-1], c_sum, c_cnt, c_dg, alpha^T alpha]
     // (the coincidence fields stay zero here; k_coinc adds them)
     double v;
@@ -928,9 +907,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     __syncthreads();
     if (tid < nrec)   // field-major [nrec][nwg]: coalesced for the reduction (launch_rowsum)
       slab[tid * nwg + wgid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
-#ifdef SGP_CON_TRACE
-    if (tid == 0) SGP_CON_TRACE(2);
-#endif
+    SGP_PROBE_CON_STAMP(2);
   }
 }
 

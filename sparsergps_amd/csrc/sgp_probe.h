@@ -1,0 +1,59 @@
+// sgp_probe.h -- timing-probe hooks of the product kernels, compiled to nothing in the product.
+//
+// The micro-benchmarks under tools/micro/ include a product kernel source after defining one
+// of the probe macros below (and SGP_PROBE_BUILD); libsgp.so defines none of them, so every
+// hook is an empty statement there.  A probe that changes results (SGP_CON_NO_EPILOGUE drops
+// the gradient epilogue) refuses to build without SGP_PROBE_BUILD.
+//
+//   SGP_CON_TRACE(k)       s_memtime stamp k of a k_contract workgroup   (tools/micro/con_trace.hip)
+//   SGP_CON_NO_EPILOGUE    k_contract<.., EPI_GRAD> returns after the k-loop (timing only)
+//   SGP_GJ_TRACE(k, p)     stamp p of the GJ look-ahead workgroup at pivot k (tools/micro/gj_trace.hip)
+#pragma once
+
+#if (defined(SGP_CON_TRACE) || defined(SGP_CON_NO_EPILOGUE) || defined(SGP_GJ_TRACE)) && \
+    !defined(SGP_PROBE_BUILD)
+#error "timing probes are for tools/micro builds only (define SGP_PROBE_BUILD there)"
+#endif
+
+// k_contract: stamp k from thread 0 of the workgroup
+#ifdef SGP_CON_TRACE
+#define SGP_PROBE_CON_STAMP(k_)        \
+  do {                                 \
+    if (tid == 0) SGP_CON_TRACE(k_);   \
+  } while (0)
+#else
+#define SGP_PROBE_CON_STAMP(k_) \
+  do {                          \
+  } while (0)
+#endif
+
+// k_contract<.., EPI_GRAD>: leave after the k-loop, keeping the accumulators live
+#ifdef SGP_CON_NO_EPILOGUE
+#define SGP_PROBE_CON_SKIP_EPILOGUE()                                                   \
+  if constexpr (EPI == EPI_GRAD) {                                                      \
+    double v_ = 0.0;                                                                    \
+    _Pragma("unroll") for (int fm_ = 0; fm_ < 4; ++fm_)                                 \
+      _Pragma("unroll") for (int fn_ = 0; fn_ < 4; ++fn_)                               \
+        v_ += acc[fm_][fn_][0] + acc[fm_][fn_][3];                                      \
+    if (v_ == 1234.5) slab[tid] = v_;                                                   \
+    return;                                                                             \
+  }
+#else
+#define SGP_PROBE_CON_SKIP_EPILOGUE()
+#endif
+
+// k_gj_step: stamps of the workgroup that solves the next pivot
+#ifdef SGP_GJ_TRACE
+#define SGP_PROBE_GJ_DECL() const bool gj_tr_ = (i == k + 1) && (j == k + 1) && threadIdx.x == 0
+#define SGP_PROBE_GJ_STAMP(p_)          \
+  do {                                  \
+    if (gj_tr_) SGP_GJ_TRACE(k, p_);    \
+  } while (0)
+#else
+#define SGP_PROBE_GJ_DECL() \
+  do {                      \
+  } while (0)
+#define SGP_PROBE_GJ_STAMP(p_) \
+  do {                         \
+  } while (0)
+#endif

@@ -8,6 +8,7 @@
 #include <vector>
 #include <random>
 __device__ unsigned long long* g_trace;
+#define SGP_PROBE_BUILD 1
 #define SGP_CON_TRACE(k)                                                                   \
   do {                                                                                     \
     unsigned long long* t_ = g_trace + (int64_t)blockIdx.x * 8;                            \

@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <vector>
 __device__ unsigned long long g_gj[64][8];
+#define SGP_PROBE_BUILD 1
 #define SGP_GJ_TRACE(k_, p_) (g_gj[(k_)][(p_)] = __builtin_amdgcn_s_memtime())
 #include "../../sparsergps_amd/csrc/k_dense.hip"
 
