@@ -48,8 +48,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
     for src in SOURCES:
         obj = os.path.join(LIBDIR, src.replace(".hip", ".o"))
         objs.append(obj)
+        # SGP_HIPCC_DEFS: extra -D flags for A/B experiment builds (tools/ab_*.sh), never set
+        # for the product library
+        extra = os.environ.get("SGP_HIPCC_DEFS", "").split()
         cmd = [cc, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wno-unused-result",
-               "-c", os.path.join(CSRC, src), "-o", obj]
+               *extra, "-c", os.path.join(CSRC, src), "-o", obj]
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
     for cmd, p in procs:
         out, _ = p.communicate()

@@ -227,6 +227,7 @@ struct sgp_ctx {
   // phase 2's Bm-independent m x m work (K22inv S K22inv, tr(K22inv S)) also runs on `aux`,
   // concurrently with the latency-bound Bm inversion on the main stream
   hipEvent_t ev_s = nullptr, ev_m3 = nullptr, ev_bm = nullptr;
+  hipEvent_t ev_lo = nullptr;             // VI phase 1: builder done (main) / side work done (aux_lo)
   hipStream_t aux_lo = nullptr;           // ... at normal priority (the Bm chain keeps its CUs)
   double* slab_aux = nullptr;             // partials of the aux stream's small reductions
   // launch-bound Bm factorisation captured once per (mp, S pointer) and replayed
@@ -262,28 +263,52 @@ constexpr int SLAB_SMALL = 1024 * (SGP_MAXD + 2);
 constexpr int KNOT_PART_ROWS = 256;   // row groups of the knot / t column-sum first pass
 constexpr int RB_N = 256;             // pinned readback doubles at the end of c->pin
 
-// The end-of-evaluation D2H copies land in pinned memory (true async DMA, one synchronisation)
-// and are unpacked into the caller's host arrays afterwards.
+// The end-of-evaluation results are gathered by ONE small kernel straight into pinned host
+// memory (device-visible, hipHostMalloc) and unpacked into the caller's host arrays after one
+// synchronisation.  (Three hipMemcpyAsync D2H copies were three blit kernels plus their launch
+// gaps on the critical path of every evaluation: ~15 us at C2.)
+constexpr int RB_SEGS = 4;
+struct GatherSegs {
+  const double* src[RB_SEGS];
+  int off[RB_SEGS];   // destination offset (doubles)
+  int n[RB_SEGS];     // doubles
+  int count;
+};
+
+__global__ void __launch_bounds__(64) k_gather_host(GatherSegs g, double* __restrict__ dst) {
+  for (int q = 0; q < g.count; ++q)
+    for (int i = threadIdx.x; i < g.n[q]; i += 64) dst[g.off[q] + i] = g.src[q][i];
+  __threadfence_system();
+}
+
 struct Readback {
   sgp_ctx* c;
   double* base;
-  size_t off = 0;
+  size_t off = 0;   // doubles
   struct Item { void* host; size_t off, bytes; };
   std::vector<Item> items;
+  GatherSegs segs{};
   explicit Readback(sgp_ctx* ctx)
       : c(ctx), base(ctx->pin + ctx->mp_max * ctx->d + ctx->m_max + (ctx->m_max + 1) / 2 + 8) {}
+  // dev: device memory of `bytes` bytes, 8-byte aligned (copied as whole doubles)
   hipError_t add(void* host, const void* dev, size_t bytes) {
-    if (off + bytes > sizeof(double) * RB_N) return hipErrorInvalidValue;
+    const size_t nd = (bytes + 7) / 8;
+    if (off + nd > (size_t)RB_N || segs.count == RB_SEGS) return hipErrorInvalidValue;
     items.push_back({host, off, bytes});
-    hipError_t e = hipMemcpyAsync(reinterpret_cast<char*>(base) + off, dev, bytes,
-                                  hipMemcpyDeviceToHost, c->stream);
-    off += (bytes + 7) & ~size_t(7);
-    return e;
+    segs.src[segs.count] = reinterpret_cast<const double*>(dev);
+    segs.off[segs.count] = (int)off;
+    segs.n[segs.count] = (int)nd;
+    ++segs.count;
+    off += nd;
+    return hipSuccess;
   }
   hipError_t wait() {
-    hipError_t e = hipStreamSynchronize(c->stream);
+    hipLaunchKernelGGL(k_gather_host, dim3(1), dim3(64), 0, c->stream, segs, base);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    for (const Item& it : items) memcpy(it.host, reinterpret_cast<char*>(base) + it.off, it.bytes);
+    e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return e;
+    for (const Item& it : items) memcpy(it.host, base + it.off, it.bytes);
     return hipSuccess;
   }
 };
@@ -384,6 +409,7 @@ void ctx_free(sgp_ctx* c) {
   if (c->ev_s) hipEventDestroy(c->ev_s);
   if (c->ev_m3) hipEventDestroy(c->ev_m3);
   if (c->ev_bm) hipEventDestroy(c->ev_bm);
+  if (c->ev_lo) hipEventDestroy(c->ev_lo);
   if (c->aux) hipStreamDestroy(c->aux);
   if (c->aux_lo) hipStreamDestroy(c->aux_lo);
   for (hipEvent_t e : c->pool) hipEventDestroy(e);
@@ -653,7 +679,8 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
       hipEventCreateWithFlags(&c->ev_k22m, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_s, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_m3, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_bm, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_bm, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_lo, hipEventDisableTiming) != hipSuccess) {
     set_err("hipStream/hipEvent creation failed");
     ctx_free(c);
     delete c;
@@ -856,14 +883,14 @@ static int contract_pass(sgp_ctx* c, const double* M, ConArgs ca, double* rec_ou
   if (fused) ca.alpha_out = c->alpha;   // k_coinc needs the fused alpha_i
   HIPCHK(launch_contract_args(c->kp, c->K, M, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp, c->m,
                               c->mp, ca, c->slab_con, &nrec, &nwg, c->stream));
-  HIPCHK(launch_rowsum(c->slab_con, nrec, nwg, c->slab_small, c->slab_small_cap, rec_out, c->stream));
-  // tau's coincidence sums -> record fields 1+L .. 3+L
-  // the rows that equal some knot depend only on (X, knot set): found by hashing once per knot
-  // set (cflag written), later evaluations only revisit the flagged rows
+  // the per-tile records summed, and tau's coincidence sums added to record fields 1+L .. 3+L
+  // (two launches); the rows that equal some knot depend only on (X, knot set): found by
+  // hashing once per knot set (cflag written), later evaluations only revisit the flagged rows
   const bool flags_known = c->cflag_gen == c->knots_gen;
-  HIPCHK(launch_coinc(c->X, c->n_pad, c->n, c->kp.d, c->U, c->mp, c->m, c->khash, c->kidx, c->K,
-                      c->mp, M, ca, fused ? c->alpha : ca.alpha_in, c->slab_small,
-                      rec_out + 1 + c->kp.L, c->cflag, flags_known ? 2 : 1, c->stream));
+  HIPCHK(launch_records(c->slab_con, nrec, nwg, c->X, c->n_pad, c->n, c->kp.d, c->U, c->mp, c->m,
+                        c->khash, c->kidx, c->K, c->mp, M, ca, fused ? c->alpha : ca.alpha_in,
+                        c->slab_small, c->slab_small_cap, 1 + c->kp.L, rec_out, c->cflag,
+                        flags_known ? 2 : 1, c->stream));
   c->cflag_gen = c->knots_gen;
   if (c->knot_on)
     HIPCHK(launch_knot_reduce(c->knot_slab, c->n_pad / SGP_TILE, c->mp, c->kp.d, c->knot_part,
@@ -995,25 +1022,32 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
     HIPCHK(launch_build_knm_t(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, mpv, m, mpv, c->K, c->r,
                               c->tslab, &t_rows, c->stream, false));
   }
-  // status / scalar resets: first written by the K22 chain (queued after the SYRK below, aux
-  // waiting on the main stream) and by phase 2
-  HIPCHK(hipMemsetAsync(c->status, 0, sizeof(int) * 4, c->stream));
-  HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->stream));
-  // K22 itself only (aux); its inverse runs in phase 2 beside the Bm inverse -- nothing in
-  // phase 1 needs it, and the latency-bound chain no longer gates the one-round SYRK or shares
-  // the CUs with the builder
-  st = k22_build(c, kp.tau2);
-  if (st) return st;
-  HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_vi_red1_count(m), c->stream));
-  HIPCHK(launch_knot_reduce(c->tslab, t_rows, mpv, 1, c->T1, c->mp_max * c->mp_max,
-                            red1 + mmv, false,
-                            c->stream));
-  HIPCHK(launch_dot(c->r, c->r, c->n_pad, c->slab_small, red1 + mmv + mpv, c->stream));
+  // The SYRK goes right behind the builder (it needs only K12); the resets and the small t / rr
+  // reductions run on aux_lo beside it instead of between the two on the main stream, where at
+  // small n (C2) the GPU idled while the host issued them one by one
+  HIPCHK(hipEventRecord(c->ev_lo, c->stream));
   {
     Scope t(c, "syrk");
     HIPCHK(launch_syrk_aug(c->K, c->n_pad, mpv, c->r, nullptr, c->slab_syrk, c->slab_syrk_cap,
                            red1, c->stream, 1, nullptr, 0));
   }
+  // K22 itself only (aux); its inverse runs in phase 2 beside the Bm inverse -- nothing in
+  // phase 1 needs it, and the latency-bound chain no longer gates the one-round SYRK or shares
+  // the CUs with the builder
+  st = k22_build(c, kp.tau2);
+  if (st) return st;
+  // aux_lo, after the builder: status / scalar resets (first written by the K22 chain -- queued
+  // after the SYRK reduction, aux waiting on the main stream -- and by phase 2), red1's zeroing
+  // (before the SYRK reduction below writes S into it: the main stream waits for ev_lo), t and rr
+  HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_lo, 0));
+  HIPCHK(hipMemsetAsync(c->status, 0, sizeof(int) * 4, c->aux_lo));
+  HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->aux_lo));
+  HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_vi_red1_count(m), c->aux_lo));
+  HIPCHK(launch_knot_reduce(c->tslab, t_rows, mpv, 1, c->T1, c->mp_max * c->mp_max,
+                            red1 + mmv, false, c->aux_lo));
+  HIPCHK(launch_dot(c->r, c->r, c->n_pad, c->slab_aux, red1 + mmv + mpv, c->aux_lo));
+  HIPCHK(hipEventRecord(c->ev_lo, c->aux_lo));
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_lo, 0));
   {
     Scope t(c, "syrk_reduce");
     HIPCHK(launch_syrk_aug(c->K, c->n_pad, mpv, c->r, nullptr, c->slab_syrk, c->slab_syrk_cap,

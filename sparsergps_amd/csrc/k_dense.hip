@@ -222,7 +222,11 @@ __global__ void __launch_bounds__(256) k_gj_pivot(const double* __restrict__ A, 
 //   else    An_ij = Ao_ij - (Ao_ik P_k) Ao_kj                       (two 64^3 f64-MFMA products)
 // Look-ahead: the workgroup owning tile (k+1, k+1) factors its fresh tile right away and writes
 // the next pivot inverse P_{k+1}, so a step costs one launch instead of pivot + panel + update.
-constexpr int GJ_LS = 70;   // LDS row stride (doubles): conflict-free f64 fragment reads
+// LDS row stride (doubles).  The A-operand fragment reads of gj_mm64 are paired into
+// ds_read2_b64 (banks (a/4) mod 32, 16-lane groups): 16 rows per group need distinct double
+// slots mod 16, i.e. an odd stride (70 gave 2-way conflicts on every A read: 0.25 of the LDS
+// cycles in the r2 PMC pass).  The B reads are 16 contiguous columns at any stride.
+constexpr int GJ_LS = 65;
 
 __device__ __forceinline__ void gj_mm64(const double* As, const double* Bs, d4 (&acc)[2][2]) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -561,7 +565,7 @@ hipError_t launch_fitc_omega(const double* alpha, const double* w, const double*
   return hipGetLastError();
 }
 
-// Dynamic LDS added to each step's workgroup so that only one fits per CU (71.7 KB static +
+// Dynamic LDS added to each step's workgroup so that only one fits per CU (66.6 KB static +
 // this > 80 KB).  Two chains run side by side (VI phase 2: K22's and Bm's inverses); with two
 // workgroups per CU a step's look-ahead workgroup (the chain's critical path: next pivot)
 // shared its CU with the other chain's tile updates.  One per CU, the other chain's step

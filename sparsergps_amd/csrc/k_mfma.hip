@@ -118,7 +118,8 @@ struct SyrkTMap {
 // fewer live registers, for kernels whose epilogue shares the register budget).
 // PAT (experiments, tools/micro/con_trace.hip): where the LDS stores go (0: MFMA slots 48-55,
 // 2: 56-63, 3: 32-39, 4: not grouped)
-template <bool SPREAD = false, int PAT = 0>
+// NVMEM: global loads of the step placed one per MFMA slot (the 8 operand loads).
+template <bool SPREAD = false, int PAT = 0, int NVMEM = 8>
 __device__ __forceinline__ void mfma_interleave() {
 #pragma unroll
   for (int i = 0; i < 64; ++i) {
@@ -126,7 +127,7 @@ __device__ __forceinline__ void mfma_interleave() {
 #ifndef SGP_IL_VMEM0
 #define SGP_IL_VMEM0 0
 #endif
-    if (i >= SGP_IL_VMEM0 && i < SGP_IL_VMEM0 + 8)
+    if (i >= SGP_IL_VMEM0 && i < SGP_IL_VMEM0 + NVMEM)
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                    // VMEM read
     if (SPREAD ? (i & 1) == 0 : i < 32)
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                    // DS read
@@ -141,10 +142,17 @@ __device__ __forceinline__ void mfma_interleave() {
 #ifndef SGP_SYRK_IL_PAT
 #define SGP_SYRK_IL_PAT 0
 #endif
+#ifndef SGP_CON_KDB
+#define SGP_CON_KDB 0   // gradient epilogue: double-buffered half-height K stages (experiment)
+#endif
+#ifndef SGP_SYRK_T_EARLY
+#define SGP_SYRK_T_EARLY 0   // t slice accumulated before (1) or after (0) the step's MFMA block
+#endif
 
 // WEIGHTED: rows scaled by w (FITC / Laplace); compiled out for the unweighted VI SYRK, whose
 // k-loop otherwise multiplies every A fragment by 1.0 (16 fp64 VALU ops per 64 MFMAs).
-template <bool WITH_T, bool WEIGHTED>
+// TMODE: 0 no t; 1 t = K^T (w o r) with rr = sum w r^2; 2 t = K^T tv with rr = sum tv r
+template <int TMODE, bool WEIGHTED>
 __global__ void __launch_bounds__(256, 2)
 k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __restrict__ w,
            const double* __restrict__ r, const double* __restrict__ tv,
@@ -167,6 +175,7 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
   // (c_tmap); rr from diagonal group 0.
   const int64_t noff = (int64_t)nb * (nb - 1) / 2;
   const int dg = (gi >= noff) ? (int)(gi - noff) : -1;
+  constexpr bool WITH_T = TMODE != 0;
   constexpr bool with_t = WITH_T;
   // tm.S == 0 (more groups than the table holds, m > 1920): one whole-panel slice per panel,
   // panel a >= 1 on the strictly-lower group (a, 0) and panel 0 on diagonal group 0 -- distinct
@@ -201,6 +210,9 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
     for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
 
   const int lrow = tid >> 4, lc = tid & 15;
+  // with t: (w r)_i, or tv_i when the caller passes tv (Laplace); every lane stages the row
+  // tid % BK so the step has no lane-dependent branch
+  constexpr bool has_tv = TMODE == 2;
   const double2* gA = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + ta * (int64_t)T128) + lc;
   const double2* gB = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + tb * (int64_t)T128) + lc;
   const int64_t gstep = BK * mp / 2;
@@ -215,55 +227,58 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
     const int64_t o_ = (int64_t)(step) * gstep;                                 \
     va0 = gA[o_]; va1 = gA[o_ + 16]; va2 = gA[o_ + 32]; va3 = gA[o_ + 48];      \
     vb0 = gB[o_]; vb1 = gB[o_ + 16]; vb2 = gB[o_ + 32]; vb3 = gB[o_ + 48];      \
-    if constexpr (!WITH_T) {  /* one block: every lane, 16 per weight */      \
-      if constexpr (WEIGHTED) vw = w[rbeg + (int64_t)(step) * BK + (tid & (BK - 1))]; \
-    } else if (tid < BK) {                                                      \
-      const int64_t rr_ = rbeg + (int64_t)(step) * BK + tid;                    \
-      if (WEIGHTED) vw = w[rr_];                                                \
-      if (with_t) {                                                             \
-        vrr = r[rr_];                                                           \
-        vr = (tv != nullptr) ? tv[rr_] : ((w != nullptr) ? w[rr_] : 1.0);       \
-      }                                                                         \
+    /* one block: every lane stages row tid % BK (16 lanes per row) */          \
+    const int64_t rr_ = rbeg + (int64_t)(step) * BK + (tid & (BK - 1));        \
+    if constexpr (WEIGHTED) vw = w[rr_];                                        \
+    if constexpr (WITH_T) {                                                     \
+      vrr = r[rr_];                                                             \
+      if constexpr (has_tv) vr = tv[rr_];                                       \
     }                                                                           \
   }
-#define SYRKB_SSTORE(buf)                                                       \
+// fold: 1 when the staged rows are a new step's (rr counts each row once), 0 for the last
+// step's reload of its own rows
+#define SYRKB_SSTORE(buf, fold)                                                 \
   {                                                                             \
     double2* pa_ = reinterpret_cast<double2*>(&Ka[buf][lrow * SB]) + lc;        \
     double2* pb_ = reinterpret_cast<double2*>(&Kb[buf][lrow * SB]) + lc;        \
     pa_[0] = va0; pa_[16] = va1; pa_[32] = va2; pa_[48] = va3;                  \
     pb_[0] = vb0; pb_[16] = vb1; pb_[32] = vb2; pb_[48] = vb3;                  \
-    if constexpr (!WITH_T) {                                                    \
-      ws[buf][tid & (BK - 1)] = vw;                                             \
-    } else if (tid < BK) {                                                      \
-      ws[buf][tid] = vw;                                                        \
-      if (with_t) {                                                             \
-        const double rw_ = (tv != nullptr) ? vr : vr * vrr; /* (w r)_i or tv_i */ \
-        rw[buf][tid] = rw_;                                                     \
-        if (t_rr) rrp = fma(rw_, vrr, rrp);                                     \
-      }                                                                         \
+    ws[buf][tid & (BK - 1)] = vw;                                               \
+    if constexpr (WITH_T) {                                                     \
+      double rw_;                                  /* tv_i or (w r)_i */        \
+      if constexpr (has_tv) rw_ = vr;                                           \
+      else rw_ = vw * vrr;                                                      \
+      rw[buf][tid & (BK - 1)] = rw_;                                            \
+      rrp = fma(rw_ * (fold), vrr, rrp);   /* used by the t_rr lanes only */    \
     }                                                                           \
   }
 
   if (nsteps > 0) {
     SYRKB_GLOAD(0);
-    SYRKB_SSTORE(0);
+    SYRKB_SSTORE(0, 1.0);
   }
   __syncthreads();
   for (int step = 0; step < nsteps; ++step) {
     const int cur = step & 1;
-    // Without t: one basic block per step, which the interleaved schedule below needs -- the
-    // last step reloads its own rows (and weights) and stores them into the idle buffer.  (The
-    // t variants fold each staged row into rr as they store it, so they keep the guards.)
-    // There inactive waves run their MFMAs on valid LDS operands (results never written).
-    constexpr bool one_block = !WITH_T;
-    if constexpr (one_block) {
-      SYRKB_GLOAD(step + 1 < nsteps ? step + 1 : step);
-    } else if (step + 1 < nsteps) {
-      SYRKB_GLOAD(step + 1);
+    // One basic block per step, which the interleaved schedule below needs: the last step
+    // reloads its own rows (and weights) and stores them into the idle buffer (t variants: with
+    // fold = 0, so rr counts them once); inactive waves run their MFMAs on valid LDS operands
+    // (results never written).  The t slice is accumulated after the block.
+    const bool more = step + 1 < nsteps;
+    if constexpr (WITH_T && SGP_SYRK_T_EARLY) {   // experiment: t before the MFMA block
+      if (t_on) {
+        const double* img = (t_inb ? Kb[cur] : Ka[cur]) + tcol;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int q = trg + k * tng;
+          if (q < BK) tacc4[k & 3] = fma(rw[cur][q], img[q * SB], tacc4[k & 3]);
+        }
+      }
     }
+    SYRKB_GLOAD(more ? step + 1 : step);
     const double* As = (ra ? Kb[cur] : Ka[cur]) + ro;
     const double* Bs = (ca_ ? Kb[cur] : Ka[cur]) + co;
-    if (one_block || active) {
+    {
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         const int krow = kk * 4 + (lane >> 4);
@@ -285,23 +300,22 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
             acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
       }
     }
+    SYRKB_SSTORE(cur ^ 1, more ? 1.0 : 0.0);
+    // the operand loads take the first 8 MFMA slots (measured at C3 FITC: giving the row
+    // scalars slots of their own as well, ahead of the operands, was 3 % slower)
+    mfma_interleave<false, SGP_SYRK_IL_PAT>();
     // t: at most one W-column slice per workgroup, shared by all four waves (BK / (256 / W)
-    // rows per thread and step).  The with-t SYRK still runs ~1.3 ms (7 %) longer than the
-    // same weighted SYRK without t at C3 (19.2 vs 17.7-18.0 ms, FITC phase 1 vs 2); the cause is
-    // not the t arithmetic's placement (diagonal groups only, or spread: same time).
-    if (t_on) {
-      const double* img = (t_inb ? Kb[cur] : Ka[cur]) + tcol;
+    // rows per thread and step), from the current buffer (the stores above went to the other);
+    // after the MFMA block, as its own (workgroup-uniform) branch
+    if constexpr (WITH_T && !SGP_SYRK_T_EARLY) {
+      if (t_on) {
+        const double* img = (t_inb ? Kb[cur] : Ka[cur]) + tcol;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {           // 16 / tng rows per thread (tng = 2, 4 or 8)
-        const int q = trg + k * tng;
-        if (q < BK) tacc4[k & 3] = fma(rw[cur][q], img[q * SB], tacc4[k & 3]);
+        for (int k = 0; k < 8; ++k) {           // 16 / tng rows per thread (tng = 2, 4 or 8)
+          const int q = trg + k * tng;
+          if (q < BK) tacc4[k & 3] = fma(rw[cur][q], img[q * SB], tacc4[k & 3]);
+        }
       }
-    }
-    if constexpr (one_block) {
-      SYRKB_SSTORE(cur ^ 1);
-      mfma_interleave<false, SGP_SYRK_IL_PAT>();
-    } else if (step + 1 < nsteps) {
-      SYRKB_SSTORE(cur ^ 1);
     }
     __syncthreads();
   }
@@ -758,7 +772,25 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
         s_xs[rr * 16 + c] = xv;                                                          \
         s_xs[rr * 16 + 8 + c] = xv * xv;                                                 \
       }
-      CON_KSTAGE(0);
+      // SGP_CON_KDB (experiment): eight half-height stages (16 rows: the 8 rows a lane's q pair
+      // needs, of each 64-row half), double-buffered in the same LDS, each issued one half-stage
+      // ahead of its use, instead of four single-buffered 32-row stages
+#define CON_KHALF(s_)                                                                    \
+      _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_) {                                 \
+        const int rho_ = wv * 4 + q_;                                                    \
+        const int64_t row_ = i0 + (rho_ >> 3) * 64 + ((s_) >> 1) * 16 + ((s_) & 1) * 8 + \
+                             (rho_ & 7);                                                 \
+        __builtin_amdgcn_global_load_lds(                                                \
+            (const __attribute__((address_space(1))) void*)(K + row_ * mp + j0 + 2 * lane), \
+            (__attribute__((address_space(3))) void*)(kst + ((s_) & 1) * 16 * KST + rho_ * KST), \
+            16, 0, 0);                                                                   \
+      }
+      if constexpr (SGP_CON_KDB) {
+        CON_KHALF(0);
+        CON_KHALF(1);
+      } else {
+        CON_KSTAGE(0);
+      }
       CON_XSTAGE(0);
       __builtin_amdgcn_s_waitcnt(0);            // K stage 0 (LDS-DMA) landed
       __syncthreads();
@@ -778,6 +810,48 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
         ucol[fn] = s_u[col];
         vcol[fn] = with_v ? s_v[col] : 0.0;
       }
+      if constexpr (SGP_CON_KDB) {
+#pragma unroll
+        for (int hs = 0; hs < 8; ++hs) {
+          const int fm = hs >> 1, h = hs & 1;
+          if (hs > 0) {                         // half-stage hs landed (and is visible to all);
+            __builtin_amdgcn_s_waitcnt(0);      // everyone is done with hs - 1's buffer
+            __syncthreads();
+            if (hs < 7) { CON_KHALF(hs + 1); }
+          }
+          const double* kb = kst + h * 16 * KST;
+          double xb[2];
+#pragma unroll
+          for (int r2 = 0; r2 < 2; ++r2)
+            xb[r2] = s_xs[(wr * 64 + fm * 16 + 4 * (2 * h + r2) + (lane >> 4)) * 16 + (lane & 15)];
+#pragma unroll
+          for (int fn = 0; fn < 4; ++fn) {
+            const int col = wc * 64 + fn * 16 + (lane & 15);
+            double kv[2];
+#pragma unroll
+            for (int r2 = 0; r2 < 2; ++r2) kv[r2] = kb[(wr * 8 + (lane >> 4) + 4 * r2) * KST + col];
+#pragma unroll
+            for (int r2 = 0; r2 < 2; ++r2) {
+              const int q = 2 * h + r2;
+              const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
+              const bool valid = cval[fn] && ((i0 + row) < n);
+              double G = s_rs[row] * acc[fm][fn][q];
+              if constexpr (V2) G = fma(s_beta[row], vcol[fn], G);
+              G = fma(s_alpha[row], ucol[fn], G);
+              const double w = valid ? G * kv[r2] : 0.0;
+              Cc[fn] += w;
+              acc[fm][fn][q] = w;
+            }
+          }
+#pragma unroll
+          for (int r2 = 0; r2 < 2; ++r2)
+#pragma unroll
+            for (int fn = 0; fn < 4; ++fn)
+              P[fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[fm][fn][2 * h + r2], xb[r2], P[fn],
+                                                           0, 0, 0);
+        }
+        __syncthreads();                        // everyone is done reading the last stage
+      } else {
 #pragma unroll
       for (int fm = 0; fm < 4; ++fm) {
         if (fm > 0) {                           // stage fm landed (and is visible to all)
@@ -817,7 +891,9 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
         __syncthreads();                        // everyone is done reading the stage
         if (fm < 3) { CON_KSTAGE(fm + 1); }
       }
+      }   // !SGP_CON_KDB
 #undef CON_KSTAGE
+#undef CON_KHALF
       SGP_PROBE_CON_STAMP(5);
       // D fragment fn: lane l, register q -> column wc*64 + fn*16 + (l>>4) + 4q, c' = l & 15
       const int cp = lane & 15, cc = cp & 7;
@@ -977,18 +1053,35 @@ __device__ __forceinline__ uint64_t coord_hash(const double* x, int64_t stride, 
   return h;
 }
 
-__global__ void __launch_bounds__(256)
-k_coinc(const double* __restrict__ X, int64_t ldx, int64_t n, int d, const double* __restrict__ U,
-        int64_t ldu, int64_t m, const uint64_t* __restrict__ khash, const int* __restrict__ kidx,
-        const double* __restrict__ K, int64_t mp, const double* __restrict__ M,
-        const double* __restrict__ alpha, const double* __restrict__ uvec,
-        const double* __restrict__ beta, const double* __restrict__ vvec,
-        const double* __restrict__ rs_vec, double rs, const double* __restrict__ cdiag,
-        double* __restrict__ part, uint8_t* __restrict__ cflag, int flag_mode) {
+// Coincidence scan of block `bid` of `nblk` (tau's dK12/dtau = 2 tau^2 pairs)
+struct CoincArgs {
+  const double* X; int64_t ldx, n; int d;
+  const double* U; int64_t ldu, m;
+  const uint64_t* khash; const int* kidx;
+  const double* K; int64_t mp; const double* M;
+  const double* alpha; const double* uvec; const double* beta; const double* vvec;
+  const double* rs_vec; double rs; const double* cdiag;
+  uint8_t* cflag; int flag_mode;
+};
+
+__device__ __forceinline__ void coinc_body(const CoincArgs& ca, int64_t bid, int64_t nblk,
+                                           double* __restrict__ part) {
+  const double* __restrict__ X = ca.X;
+  const double* __restrict__ U = ca.U;
+  const double* __restrict__ K = ca.K;
+  const double* __restrict__ M = ca.M;
+  const int64_t ldx = ca.ldx, n = ca.n, ldu = ca.ldu, m = ca.m, mp = ca.mp;
+  const int d = ca.d, flag_mode = ca.flag_mode;
+  const uint64_t* __restrict__ khash = ca.khash;
+  const int* __restrict__ kidx = ca.kidx;
+  const double *alpha = ca.alpha, *uvec = ca.uvec, *beta = ca.beta, *vvec = ca.vvec;
+  const double *rs_vec = ca.rs_vec, *cdiag = ca.cdiag;
+  const double rs = ca.rs;
+  uint8_t* cflag = ca.cflag;
   // flag_mode 1: hash every row and record in cflag whether it equals some knot;
   //           2: cflag is current for this knot set -- only flagged rows are revisited
   double a[3] = {0.0, 0.0, 0.0};
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+  for (int64_t i = bid * 256 + threadIdx.x; i < n; i += nblk * 256) {
     if (flag_mode == 2 && !cflag[i]) continue;
     bool any = false;
     const uint64_t h = coord_hash(X + i, ldx, d);
@@ -1022,20 +1115,43 @@ k_coinc(const double* __restrict__ X, int64_t ldx, int64_t n, int d, const doubl
   }
   __syncthreads();
   if (threadIdx.x < 3)
-    part[blockIdx.x * 3 + threadIdx.x] =
+    part[bid * 3 + threadIdx.x] =
         sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
 }
 
-// rec[0..2] += sum_b part[b][0..2]  (one 256-thread block, fixed summation order)
-__global__ void __launch_bounds__(256) k_coinc_add(const double* __restrict__ part, int nb,
-                                                   double* __restrict__ rec) {
+// The contraction's record reduction, first pass, in one launch: blocks [0, nbc) run the
+// coincidence scan (partials part_c[b][3]); blocks [nbc, nbc + nrow * G) sum field c's
+// per-tile records over the tile range of group g (partials part_r[c][g]).
+__global__ void __launch_bounds__(256)
+k_rec_pass1(CoincArgs ca, int nbc, const double* __restrict__ slab, int64_t len, int G,
+            double* __restrict__ part_r, double* __restrict__ part_c) {
+  if ((int)blockIdx.x < nbc) {
+    coinc_body(ca, blockIdx.x, nbc, part_c);
+    return;
+  }
+  __shared__ double sh[4];
+  const int64_t bid = (int64_t)blockIdx.x - nbc, c = bid / G, g = bid % G;
+  const int64_t b = len * g / G, e = len * (g + 1) / G;
+  double v = 0.0;
+  for (int64_t k = b + threadIdx.x; k < e; k += 256) v += slab[c * len + k];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) part_r[c * G + g] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+// Second pass (one block, fixed summation orders): rec[c] = sum_g part_r[c][g] for c < nrow,
+// and the coincidence sums added to rec[coff + 0..2].
+__global__ void __launch_bounds__(256)
+k_rec_pass2(const double* __restrict__ part_r, int G, int nrow, const double* __restrict__ part_c,
+            int nbc, int coff, double* __restrict__ rec) {
   __shared__ double sh[3][4];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-  for (int b = tid; b < nb; b += 256) {
-    s0 += part[b * 3];
-    s1 += part[b * 3 + 1];
-    s2 += part[b * 3 + 2];
+  for (int b = tid; b < nbc; b += 256) {
+    s0 += part_c[b * 3];
+    s1 += part_c[b * 3 + 1];
+    s2 += part_c[b * 3 + 2];
   }
   s0 = wave_sum(s0);
   s1 = wave_sum(s1);
@@ -1046,7 +1162,13 @@ __global__ void __launch_bounds__(256) k_coinc_add(const double* __restrict__ pa
     sh[2][wv] = s2;
   }
   __syncthreads();
-  if (tid < 3) rec[tid] += sh[tid][0] + sh[tid][1] + sh[tid][2] + sh[tid][3];
+  if (tid < nrow) {
+    double v = 0.0;
+    for (int g = 0; g < G; ++g) v += part_r[tid * G + g];
+    const int q = tid - coff;
+    if (q >= 0 && q < 3) v += sh[q][0] + sh[q][1] + sh[q][2] + sh[q][3];
+    rec[tid] = v;
+  }
 }
 
 // rowq[tj][i] summed over the column tiles -> out[i] (deterministic order)
@@ -1061,7 +1183,10 @@ k_rowq_reduce(const double* __restrict__ rowq, int64_t ntj, int64_t n_pad,
 }
 
 // ============================================================================ generic 64x64 GEMM
-constexpr int GA = 18;   // [64][16] A image stride
+// [64][16] A image stride.  The compiler pairs the fragment reads into ds_read2_b64, which banks
+// (a/4) mod 32 in 16-lane groups: the 16 rows a group reads must fall on distinct double slots
+// mod 16, i.e. an odd stride (18 gave 2-way conflicts: 0.25 of the LDS cycles, r2 PMC pass)
+constexpr int GA = 17;
 constexpr int GB = 80;   // [16][64] B image stride: 2*80 % 64 == 32
 template <bool TA, bool TB>
 __global__ void __launch_bounds__(256)
@@ -1286,17 +1411,19 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
       }
     }
     if (part & 1) {
-      if (with_t && w)
-        hipLaunchKernelGGL((k_syrk_blk<true, true>), grid, dim3(256), 0, s, K, n_pad, mp, w, r, tv,
+      // with t: the weighted forms only (FITC phase 1: w = 1/Z; Laplace: w = B with tv)
+      if (with_t && !w) return hipErrorInvalidValue;
+      if (with_t && tv)
+        hipLaunchKernelGGL((k_syrk_blk<2, true>), grid, dim3(256), 0, s, K, n_pad, mp, w, r, tv,
                            q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm);
       else if (with_t)
-        hipLaunchKernelGGL((k_syrk_blk<true, false>), grid, dim3(256), 0, s, K, n_pad, mp, w, r,
-                           tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm);
+        hipLaunchKernelGGL((k_syrk_blk<1, true>), grid, dim3(256), 0, s, K, n_pad, mp, w, r, tv,
+                           q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm);
       else if (w)
-        hipLaunchKernelGGL((k_syrk_blk<false, true>), grid, dim3(256), 0, s, K, n_pad, mp, w, r,
+        hipLaunchKernelGGL((k_syrk_blk<0, true>), grid, dim3(256), 0, s, K, n_pad, mp, w, r,
                            tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm);
       else
-        hipLaunchKernelGGL((k_syrk_blk<false, false>), grid, dim3(256), 0, s, K, n_pad, mp, w, r,
+        hipLaunchKernelGGL((k_syrk_blk<0, false>), grid, dim3(256), 0, s, K, n_pad, mp, w, r,
                            tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm);
     }
     if (part & 2) {
@@ -1348,17 +1475,26 @@ hipError_t launch_gemm_tn(const double* A, int64_t lda, int64_t ma, const double
   return hipGetLastError();
 }
 
-hipError_t launch_coinc(const double* X, int64_t ldx, int64_t n, int d, const double* U,
-                        int64_t ldu, int64_t m, const uint64_t* khash, const int* kidx,
-                        const double* K, int64_t mp, const double* M, const ConArgs& ca,
-                        const double* alpha, double* part, double* rec, uint8_t* cflag,
-                        int flag_mode, hipStream_t s) {
-  int64_t nb = (n + 255) / 256;
-  if (nb > 1024) nb = 1024;
-  hipLaunchKernelGGL(k_coinc, dim3((unsigned)nb), dim3(256), 0, s, X, ldx, n, d, U, ldu, m, khash,
-                     kidx, K, mp, M, alpha, ca.uvec, ca.beta_in, ca.vvec, ca.rs_vec, ca.rs,
-                     ca.cdiag, part, cflag, flag_mode);
-  hipLaunchKernelGGL(k_coinc_add, dim3(1), dim3(256), 0, s, part, (int)nb, rec);
+hipError_t launch_records(const double* slab, int64_t nrow, int64_t len, const double* X,
+                          int64_t ldx, int64_t n, int d, const double* U, int64_t ldu, int64_t m,
+                          const uint64_t* khash, const int* kidx, const double* K, int64_t mp,
+                          const double* M, const ConArgs& cg, const double* alpha, double* part,
+                          int64_t part_cap, int coff, double* rec, uint8_t* cflag, int flag_mode,
+                          hipStream_t s) {
+  if (nrow <= 0 || nrow > 256 || coff < 0 || coff + 3 > nrow) return hipErrorInvalidValue;
+  const int G = 32;
+  int64_t nbc = (n + 255) / 256;
+  if (nbc > 1024) nbc = 1024;
+  if (nbc < 1) nbc = 1;
+  if (nrow * G + 3 * nbc > part_cap) return hipErrorInvalidValue;
+  double* part_r = part;
+  double* part_c = part + nrow * G;
+  CoincArgs ca{X, ldx, n, d, U, ldu, m, khash, kidx, K, mp, M, alpha, cg.uvec, cg.beta_in,
+               cg.vvec, cg.rs_vec, cg.rs, cg.cdiag, cflag, flag_mode};
+  hipLaunchKernelGGL(k_rec_pass1, dim3((unsigned)(nbc + nrow * G)), dim3(256), 0, s, ca,
+                     (int)nbc, slab, len, G, part_r, part_c);
+  hipLaunchKernelGGL(k_rec_pass2, dim3(1), dim3(256), 0, s, part_r, G, (int)nrow, part_c,
+                     (int)nbc, coff, rec);
   return hipGetLastError();
 }
 
@@ -1378,41 +1514,6 @@ hipError_t launch_knot_reduce(const double* knot_slab, int64_t ntiles, int64_t m
                      ncol, part);
   hipLaunchKernelGGL(k_knot_reduce2, dim3((unsigned)((ncol + 63) / 64)), dim3(256), 0, s, part,
                      (int)gy, ncol, out, accumulate ? 1 : 0);
-  return hipGetLastError();
-}
-
-// out[c] = sum_k slab[c * len + k] for c < nrow (field-major records), two deterministic passes
-// through part (nrow * 32 doubles)
-__global__ void __launch_bounds__(256) k_rowsum1(const double* __restrict__ slab, int64_t len,
-                                                 double* __restrict__ part) {
-  __shared__ double sh[4];
-  const int64_t c = blockIdx.x, g = blockIdx.y, G = gridDim.y;
-  const int64_t b = len * g / G, e = len * (g + 1) / G;
-  double v = 0.0;
-  for (int64_t k = b + threadIdx.x; k < e; k += 256) v += slab[c * len + k];
-  v = wave_sum(v);
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) part[c * G + g] = sh[0] + sh[1] + sh[2] + sh[3];
-}
-
-__global__ void k_rowsum2(const double* __restrict__ part, int G, int nrow,
-                          double* __restrict__ out) {
-  const int c = blockIdx.x * 64 + threadIdx.x;
-  if (c >= nrow) return;
-  double v = 0.0;
-  for (int g = 0; g < G; ++g) v += part[c * G + g];
-  out[c] = v;
-}
-
-hipError_t launch_rowsum(const double* slab, int64_t nrow, int64_t len, double* part,
-                         int64_t part_cap, double* out, hipStream_t s) {
-  if (nrow <= 0) return hipSuccess;
-  const int G = 32;
-  if (nrow * G > part_cap) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_rowsum1, dim3((unsigned)nrow, G), dim3(256), 0, s, slab, len, part);
-  hipLaunchKernelGGL(k_rowsum2, dim3((unsigned)((nrow + 63) / 64)), dim3(64), 0, s, part, G,
-                     (int)nrow, out);
   return hipGetLastError();
 }
 

@@ -296,10 +296,6 @@ hipError_t launch_lap_grad_b(int64_t n, int64_t n_pad, const double* B, const do
 hipError_t launch_knot_reduce(const double* knot_slab, int64_t ntiles, int64_t mp, int d,
                               double* part, int64_t part_cap, double* out, bool accumulate,
                               hipStream_t s);
-// out[c] = sum_k slab[c * len + k], c < nrow (field-major contraction records); part holds
-// nrow * 32 doubles
-hipError_t launch_rowsum(const double* slab, int64_t nrow, int64_t len, double* part,
-                         int64_t part_cap, double* out, hipStream_t s);
 // out[k*d + c] = 2 sum_l G22_kl K22_kl (u_lc - u_kc), G22 as in launch_contract_kmm
 hipError_t launch_knot_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,
                            int64_t mp, const double* uvec, const double* Ainv,
@@ -324,11 +320,14 @@ hipError_t launch_vi_cand_scalars(int64_t m, int64_t mp, int64_t T, int64_t Tp,
 hipError_t launch_colnorm2(const double* K, int64_t n_pad, int64_t mp, double* part,
                            int64_t part_cap, double* out, hipStream_t s);
 
-// tau coincidence sums of one contraction pass (k_mfma.hip k_coinc): rec[0..2] +=
-// {sum G_ij, #pairs, sum cdiag_j} over the pairs x_i == u_j; alpha = the pass's alpha_i
-// (alpha_in, or the fused alpha written through alpha_out); part: 1024 * 3 doubles.
-hipError_t launch_coinc(const double* X, int64_t ldx, int64_t n, int d, const double* U,
-                        int64_t ldu, int64_t m, const uint64_t* khash, const int* kidx,
-                        const double* K, int64_t mp, const double* M, const ConArgs& ca,
-                        const double* alpha, double* part, double* rec, uint8_t* cflag,
-                        int flag_mode, hipStream_t s);
+// One contraction pass's records, in two launches (k_mfma.hip k_rec_pass1 / k_rec_pass2):
+// rec[c] = sum_k slab[c * len + k] for c < nrow (field-major per-tile records), plus tau's
+// coincidence sums {sum G_ij, #pairs, sum cdiag_j} over the pairs x_i == u_j added to
+// rec[coff + 0..2]; alpha = the pass's alpha_i (alpha_in, or the fused alpha written through
+// alpha_out).  part: nrow * 32 + 3 * 1024 doubles (both passes' partials).
+hipError_t launch_records(const double* slab, int64_t nrow, int64_t len, const double* X,
+                          int64_t ldx, int64_t n, int d, const double* U, int64_t ldu, int64_t m,
+                          const uint64_t* khash, const int* kidx, const double* K, int64_t mp,
+                          const double* M, const ConArgs& cg, const double* alpha, double* part,
+                          int64_t part_cap, int coff, double* rec, uint8_t* cflag, int flag_mode,
+                          hipStream_t s);
