@@ -214,7 +214,9 @@ def main():
                     help="vi = the headline metric; fitc / laplace = secondary modes (SURVEY 8(d))")
     ap.add_argument("--config", default=None, choices=["C2", "C3", "C5"])
     ap.add_argument("--tol-nr", type=float, default=1e-5)
-    ap.add_argument("--n", type=int, default=None)
+    # --rows: the same, for torch.distributed.run command lines (it reads "--n" as an
+    # abbreviation of its own options)
+    ap.add_argument("--n", "--rows", dest="n", type=int, default=None)
     ap.add_argument("--m", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-full", default=None, metavar="OUT_JSON",

@@ -142,9 +142,6 @@ __device__ __forceinline__ void mfma_interleave() {
 #ifndef SGP_SYRK_IL_PAT
 #define SGP_SYRK_IL_PAT 0
 #endif
-#ifndef SGP_CON_KDB
-#define SGP_CON_KDB 0   // gradient epilogue: double-buffered half-height K stages (experiment)
-#endif
 #ifndef SGP_SYRK_T_EARLY
 #define SGP_SYRK_T_EARLY 0   // t slice accumulated before (1) or after (0) the step's MFMA block
 #endif
@@ -740,24 +737,16 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
       // The C fragment of K P is read directly as the A operand of v_mfma_f64_16x16x4 (its lane
       // map is that of W^T), so D costs 4 MFMAs per 16x16 fragment instead of ~3 d VALU ops
       // per pair.
-      // K_ij is read back through LDS: per 16-row fragment fm, the 32 tile rows the four waves
-      // need (fm-th 16 rows of each 64-row half) are copied global -> LDS by LDS-DMA (one
-      // 1 KiB row per wave-instruction, no VGPRs held), the first stage before the coordinate
-      // staging so its latency hides behind it.  (Fragment-shaped loads straight to VGPRs
+      // K_ij is read back through LDS: per half of a 16-row fragment fm, the 16 tile rows the
+      // four waves need are copied global -> LDS by LDS-DMA (one 1 KiB row per
+      // wave-instruction, no VGPRs held), double-buffered, the first two before the coordinate
+      // staging so their latency hides behind it.  (Fragment-shaped loads straight to VGPRs
       // serialised on one HBM round trip per fragment at this register pressure.)
       // Coordinates go through the D products in chunks of 8 (DT / 8 chunks): the first chunk
       // rides on the pass that forms W; each further chunk restages [x~ | x~^2] and u~ and adds
       // one 16-column MFMA product over the W kept in the accumulators.
       constexpr int KST = 136;                  // stage row stride (doubles)
-      double* kst = s_us + ((T128 * sus + 1) & ~1);   // 32 x KST, 16-byte aligned
-#define CON_KSTAGE(fm_)                                                                  \
-      _Pragma("unroll") for (int q_ = 0; q_ < 8; ++q_) {                                 \
-        const int rho_ = wv * 8 + q_;                                                    \
-        const int64_t row_ = i0 + (rho_ >> 4) * 64 + (fm_) * 16 + (rho_ & 15);           \
-        __builtin_amdgcn_global_load_lds(                                                \
-            (const __attribute__((address_space(1))) void*)(K + row_ * mp + j0 + 2 * lane), \
-            (__attribute__((address_space(3))) void*)(kst + rho_ * KST), 16, 0, 0);       \
-      }
+      double* kst = s_us + ((T128 * sus + 1) & ~1);   // 2 x 16 x KST, 16-byte aligned
       // chunk ch of the coordinates: s_xs = [x~ | x~^2] (128 x 16), s_us = u~ (128 x sus)
 #define CON_XSTAGE(ch_)                                                                  \
       _Pragma("unroll") for (int e = tid; e < T128 * 8; e += 256) {                      \
@@ -772,9 +761,10 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
         s_xs[rr * 16 + c] = xv;                                                          \
         s_xs[rr * 16 + 8 + c] = xv * xv;                                                 \
       }
-      // SGP_CON_KDB (experiment): eight half-height stages (16 rows: the 8 rows a lane's q pair
-      // needs, of each 64-row half), double-buffered in the same LDS, each issued one half-stage
-      // ahead of its use, instead of four single-buffered 32-row stages
+      // Eight half-height stages (16 rows: the 8 rows a lane's q pair needs, of each 64-row
+      // half), double-buffered in the LDS one 32-row stage took, each issued one half-stage
+      // ahead of its use (round 3; four single-buffered 32-row stages before: the same time at
+      // C3, 31.3-31.4 ms, and 1-3 % more at C2, profiles/r3/kdb_ab.txt)
 #define CON_KHALF(s_)                                                                    \
       _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_) {                                 \
         const int rho_ = wv * 4 + q_;                                                    \
@@ -785,12 +775,8 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
             (__attribute__((address_space(3))) void*)(kst + ((s_) & 1) * 16 * KST + rho_ * KST), \
             16, 0, 0);                                                                   \
       }
-      if constexpr (SGP_CON_KDB) {
-        CON_KHALF(0);
-        CON_KHALF(1);
-      } else {
-        CON_KSTAGE(0);
-      }
+      CON_KHALF(0);
+      CON_KHALF(1);
       CON_XSTAGE(0);
       __builtin_amdgcn_s_waitcnt(0);            // K stage 0 (LDS-DMA) landed
       __syncthreads();
@@ -810,7 +796,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
         ucol[fn] = s_u[col];
         vcol[fn] = with_v ? s_v[col] : 0.0;
       }
-      if constexpr (SGP_CON_KDB) {
+      {
 #pragma unroll
         for (int hs = 0; hs < 8; ++hs) {
           const int fm = hs >> 1, h = hs & 1;
@@ -849,50 +835,10 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
             for (int fn = 0; fn < 4; ++fn)
               P[fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[fm][fn][2 * h + r2], xb[r2], P[fn],
                                                            0, 0, 0);
+          if (hs == 1) SGP_PROBE_CON_STAMP(3);
         }
         __syncthreads();                        // everyone is done reading the last stage
-      } else {
-#pragma unroll
-      for (int fm = 0; fm < 4; ++fm) {
-        if (fm > 0) {                           // stage fm landed (and is visible to all)
-          __builtin_amdgcn_s_waitcnt(0);
-          __syncthreads();
-        }
-        double xb[4];
-#pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4)
-          xb[r4] = s_xs[(wr * 64 + fm * 16 + 4 * r4 + (lane >> 4)) * 16 + (lane & 15)];
-#pragma unroll
-        for (int fn = 0; fn < 4; ++fn) {
-          const int col = wc * 64 + fn * 16 + (lane & 15);
-          double kv[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) kv[q] = kst[(wr * 16 + (lane >> 4) + 4 * q) * KST + col];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
-            const bool valid = cval[fn] && ((i0 + row) < n);
-            double G = s_rs[row] * acc[fm][fn][q];
-            if constexpr (V2) G = fma(s_beta[row], vcol[fn], G);
-            G = fma(s_alpha[row], ucol[fn], G);
-            const double w = valid ? G * kv[q] : 0.0;
-            Cc[fn] += w;
-            acc[fm][fn][q] = w;
-          }
-        }
-        // r4-major: consecutive MFMAs go to the four independent accumulators P[fn] instead of
-        // four dependent ones into the same P[fn]
-#pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4)
-#pragma unroll
-          for (int fn = 0; fn < 4; ++fn)
-            P[fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[fm][fn][r4], xb[r4], P[fn], 0, 0, 0);
-        if (fm == 0) SGP_PROBE_CON_STAMP(3);
-        __syncthreads();                        // everyone is done reading the stage
-        if (fm < 3) { CON_KSTAGE(fm + 1); }
       }
-      }   // !SGP_CON_KDB
-#undef CON_KSTAGE
 #undef CON_KHALF
       SGP_PROBE_CON_STAMP(5);
       // D fragment fn: lane l, register q -> column wc*64 + fn*16 + (l>>4) + 4q, c' = l & 15
