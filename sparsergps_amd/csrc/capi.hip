@@ -1010,22 +1010,23 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   c->delta = delta;
   st = upload_knots(c, U, m, ldu);
   if (st) return st;
-  st = k22_sync(c);   // aux may build K22 from here on
-  if (st) return st;
   const int64_t mpv = c->mp, mmv = mpv * mpv;
   int64_t t_rows = 0;
   {
     // K12, and t = K^T r riding along in the memory-bound builder (keeps the SYRK's
-    // diagonal tiles as cheap as the others); launched before anything else of the
-    // evaluation so the GPU starts on it as soon as the knots are up
+    // diagonal tiles as cheap as the others); the first HIP call of the evaluation, so the
+    // GPU starts on it as soon as the host gets here
     Scope t(c, "build_knm");
     HIPCHK(launch_build_knm_t(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, mpv, m, mpv, c->K, c->r,
                               c->tslab, &t_rows, c->stream, false));
   }
-  // The SYRK goes right behind the builder (it needs only K12); the resets and the small t / rr
-  // reductions run on aux_lo beside it instead of between the two on the main stream, where at
-  // small n (C2) the GPU idled while the host issued them one by one
-  HIPCHK(hipEventRecord(c->ev_lo, c->stream));
+  // ev_knots after the builder: aux may build K22 from here on (first needed by phase 2), and
+  // aux_lo may reduce the builder's t partials.  The SYRK goes right behind the builder (it
+  // needs only K12); the resets and the small t / rr reductions run on aux_lo beside it
+  // instead of between the two on the main stream, where at small n (C2) the GPU idled while
+  // the host issued them one by one
+  st = k22_sync(c);
+  if (st) return st;
   {
     Scope t(c, "syrk");
     HIPCHK(launch_syrk_aug(c->K, c->n_pad, mpv, c->r, nullptr, c->slab_syrk, c->slab_syrk_cap,
@@ -1039,7 +1040,7 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   // aux_lo, after the builder: status / scalar resets (first written by the K22 chain -- queued
   // after the SYRK reduction, aux waiting on the main stream -- and by phase 2), red1's zeroing
   // (before the SYRK reduction below writes S into it: the main stream waits for ev_lo), t and rr
-  HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_lo, 0));
+  HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_knots, 0));
   HIPCHK(hipMemsetAsync(c->status, 0, sizeof(int) * 4, c->aux_lo));
   HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->aux_lo));
   HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_vi_red1_count(m), c->aux_lo));
