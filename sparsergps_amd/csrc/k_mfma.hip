@@ -142,14 +142,12 @@ __device__ __forceinline__ void mfma_interleave() {
 #ifndef SGP_SYRK_IL_PAT
 #define SGP_SYRK_IL_PAT 0
 #endif
-#ifndef SGP_SYRK_T_EARLY
-#define SGP_SYRK_T_EARLY 0   // t slice accumulated before (1) or after (0) the step's MFMA block
-#endif
 
 // WEIGHTED: rows scaled by w (FITC / Laplace); compiled out for the unweighted VI SYRK, whose
 // k-loop otherwise multiplies every A fragment by 1.0 (16 fp64 VALU ops per 64 MFMAs).
-// TMODE: 0 no t; 1 t = K^T (w o r) with rr = sum w r^2; 2 t = K^T tv with rr = sum tv r
-template <int TMODE, bool WEIGHTED>
+// TMODE: 0 no t; 1 t = K^T (w o r) with rr = sum w r^2; 2 t = K^T tv with rr = sum tv r.
+// TR: rows of the t slice per thread and step, 8 / S for S slices per panel (syrk_t_table)
+template <int TMODE, bool WEIGHTED, int TR = 2>
 __global__ void __launch_bounds__(256, 2)
 k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __restrict__ w,
            const double* __restrict__ r, const double* __restrict__ tv,
@@ -262,16 +260,6 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
     // fold = 0, so rr counts them once); inactive waves run their MFMAs on valid LDS operands
     // (results never written).  The t slice is accumulated after the block.
     const bool more = step + 1 < nsteps;
-    if constexpr (WITH_T && SGP_SYRK_T_EARLY) {   // experiment: t before the MFMA block
-      if (t_on) {
-        const double* img = (t_inb ? Kb[cur] : Ka[cur]) + tcol;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int q = trg + k * tng;
-          if (q < BK) tacc4[k & 3] = fma(rw[cur][q], img[q * SB], tacc4[k & 3]);
-        }
-      }
-    }
     SYRKB_GLOAD(more ? step + 1 : step);
     const double* As = (ra ? Kb[cur] : Ka[cur]) + ro;
     const double* Bs = (ca_ ? Kb[cur] : Ka[cur]) + co;
@@ -301,18 +289,23 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
     // the operand loads take the first 8 MFMA slots (measured at C3 FITC: giving the row
     // scalars slots of their own as well, ahead of the operands, was 3 % slower)
     mfma_interleave<false, SGP_SYRK_IL_PAT>();
-    // t: at most one W-column slice per workgroup, shared by all four waves (BK / (256 / W)
-    // rows per thread and step), from the current buffer (the stores above went to the other);
-    // after the MFMA block, as its own (workgroup-uniform) branch
-    if constexpr (WITH_T && !SGP_SYRK_T_EARLY) {
-      if (t_on) {
-        const double* img = (t_inb ? Kb[cur] : Ka[cur]) + tcol;
+    // t: at most one W-column slice per workgroup, shared by all four waves (TR = BK / (256 / W)
+    // rows per thread and step), from the current buffer (the stores above went to the other).
+    // Branch-free, so it stays inside the step's basic block and its LDS reads interleave with
+    // the MFMAs: workgroups without a slice read column 0 and never use the sums.  (Round 2-3:
+    // a branch after the block, its loop over rows waiting on each read in turn, cost the
+    // with-t SYRK 16 % against the same SYRK without t.)
+    if constexpr (WITH_T) {
+      const double* img = (t_inb ? Kb[cur] : Ka[cur]) + tcol;
+      double a_[TR], b_[TR];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {           // 16 / tng rows per thread (tng = 2, 4 or 8)
-          const int q = trg + k * tng;
-          if (q < BK) tacc4[k & 3] = fma(rw[cur][q], img[q * SB], tacc4[k & 3]);
-        }
+      for (int k = 0; k < TR; ++k) {
+        const int q = trg + k * (BK / TR);
+        a_[k] = rw[cur][q];
+        b_[k] = img[q * SB];
       }
+#pragma unroll
+      for (int k = 0; k < TR; ++k) tacc4[k & 3] = fma(a_[k], b_[k], tacc4[k & 3]);
     }
     __syncthreads();
   }
@@ -1359,12 +1352,21 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
     if (part & 1) {
       // with t: the weighted forms only (FITC phase 1: w = 1/Z; Laplace: w = B with tv)
       if (with_t && !w) return hipErrorInvalidValue;
-      if (with_t && tv)
-        hipLaunchKernelGGL((k_syrk_blk<2, true>), grid, dim3(256), 0, s, K, n_pad, mp, w, r, tv,
-                           q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm);
-      else if (with_t)
-        hipLaunchKernelGGL((k_syrk_blk<1, true>), grid, dim3(256), 0, s, K, n_pad, mp, w, r, tv,
-                           q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm);
+      // rows of the t slice per thread: 8 / S (tm.S == 0: one slice per panel)
+      const int tr = tm.S >= 4 ? 2 : tm.S == 2 ? 4 : 8;
+#define SYRK_T_LAUNCH(tmode_, tr_)                                                             \
+  hipLaunchKernelGGL((k_syrk_blk<tmode_, true, tr_>), grid, dim3(256), 0, s, K, n_pad, mp, w, r, \
+                     tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm)
+      if (with_t && tv) {
+        if (tr == 2) SYRK_T_LAUNCH(2, 2);
+        else if (tr == 4) SYRK_T_LAUNCH(2, 4);
+        else SYRK_T_LAUNCH(2, 8);
+      } else if (with_t) {
+        if (tr == 2) SYRK_T_LAUNCH(1, 2);
+        else if (tr == 4) SYRK_T_LAUNCH(1, 4);
+        else SYRK_T_LAUNCH(1, 8);
+      }
+#undef SYRK_T_LAUNCH
       else if (w)
         hipLaunchKernelGGL((k_syrk_blk<0, true>), grid, dim3(256), 0, s, K, n_pad, mp, w, r,
                            tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm);

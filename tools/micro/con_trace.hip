@@ -1,12 +1,15 @@
 // Timeline probe (stamps from the last launch: the normal 2-workgroups-per-CU grid) of the K12 contraction kernel (k_contract<8, EPI_GRAD>): thread 0 of every
 // workgroup records s_memtime at entry, after the k-loop and at the end, plus its CU / XCD, so
 // the per-tile fixed cost (prologue + epilogue) and the phase relation of the workgroups that
-// share a CU can be read off.  Synthetic operands; n = 131072 rows, m = 1024, d = 8 (ARD).
+// share a CU can be read off.  Synthetic operands; default n = 131072 rows, m = 1024, d = 8
+// (ARD); C2's shape is n = 100000, m = 256.
 //   build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -o con_trace con_trace.hip
-//   run:   ./con_trace out.csv
+//   run:   ./con_trace out.csv [n m]
 #include <cstdio>
 #include <vector>
 #include <random>
+#include <algorithm>
+#include <cstdlib>
 __device__ unsigned long long* g_trace;
 #define SGP_PROBE_BUILD 1
 #define SGP_CON_TRACE(k)                                                                   \
@@ -19,7 +22,8 @@ __device__ unsigned long long* g_trace;
 #include "../../sparsergps_amd/csrc/k_mfma.hip"
 
 int main(int argc, char** argv) {
-  const int64_t n = 131072, n_pad = n, m = 1024, mp = 1024;
+  const int64_t n = argc > 3 ? atoll(argv[2]) : 131072, n_pad = (n + 127) / 128 * 128;
+  const int64_t m = argc > 3 ? atoll(argv[3]) : 1024, mp = (m + 127) / 128 * 128;
   const int d = 8;
   std::mt19937_64 g(1);
   std::uniform_real_distribution<double> U01(0.0, 1.0);
@@ -84,5 +88,19 @@ int main(int argc, char** argv) {
             t[3], t[5], t[6], t[2], t[7] & 0xffffffffull, t[7] >> 32);
   }
   fclose(f);
+  // per-workgroup phases (s_memtime ticks: shader clock): k-loop = t1 - t0, epilogue = t2 - t1
+  std::vector<double> kl, ep;
+  unsigned long long tmin = ~0ull, tmax = 0;
+  for (int64_t w = 0; w < nwg; ++w) {
+    const unsigned long long* t = &ht[w * 8];
+    kl.push_back((double)(t[1] - t[0]));
+    ep.push_back((double)(t[2] - t[1]));
+    tmin = std::min(tmin, t[0]);
+    tmax = std::max(tmax, t[2]);
+  }
+  std::sort(kl.begin(), kl.end());
+  std::sort(ep.begin(), ep.end());
+  printf("n=%lld m=%lld nwg=%lld  median k-loop %.0f ticks, epilogue %.0f ticks, span %llu ticks\n",
+         (long long)n, (long long)m, (long long)nwg, kl[kl.size() / 2], ep[ep.size() / 2], tmax - tmin);
   return 0;
 }
