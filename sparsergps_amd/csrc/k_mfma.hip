@@ -142,6 +142,12 @@ __device__ __forceinline__ void mfma_interleave() {
 #ifndef SGP_SYRK_IL_PAT
 #define SGP_SYRK_IL_PAT 0
 #endif
+// With-t SYRK: the next k-step's operand loads pinned to the top of the step (a scheduling
+// barrier after them, no VMEM groups in the interleave).  The group-barrier request alone
+// leaves the loads at MFMA slots 16-54 of 64 with their vmcnt wait 4-30 slots later
+// (tools/isa_step.py); pinned, the t-carrying SYRK runs 1.7 % faster (FITC C3 17.95 -> 17.64
+// ms), but the same pin made the VI SYRK 10 % and the contraction 1.5 % slower and the omega
+// SYRK 5 % slower (profiles/r3/gload_pin_ab.txt), so only the t variants use it.
 
 // WEIGHTED: rows scaled by w (FITC / Laplace); compiled out for the unweighted VI SYRK, whose
 // k-loop otherwise multiplies every A fragment by 1.0 (16 fp64 VALU ops per 64 MFMAs).
@@ -258,9 +264,10 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
     // One basic block per step, which the interleaved schedule below needs: the last step
     // reloads its own rows (and weights) and stores them into the idle buffer (t variants: with
     // fold = 0, so rr counts them once); inactive waves run their MFMAs on valid LDS operands
-    // (results never written).  The t slice is accumulated after the block.
+    // (results never written).  The t slice is accumulated inside the block (below).
     const bool more = step + 1 < nsteps;
     SYRKB_GLOAD(more ? step + 1 : step);
+    if constexpr (WITH_T) __builtin_amdgcn_sched_barrier(0);
     const double* As = (ra ? Kb[cur] : Ka[cur]) + ro;
     const double* Bs = (ca_ ? Kb[cur] : Ka[cur]) + co;
     {
@@ -286,9 +293,10 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
       }
     }
     SYRKB_SSTORE(cur ^ 1, more ? 1.0 : 0.0);
-    // the operand loads take the first 8 MFMA slots (measured at C3 FITC: giving the row
-    // scalars slots of their own as well, ahead of the operands, was 3 % slower)
-    mfma_interleave<false, SGP_SYRK_IL_PAT>();
+    // VMEM groups for the operand loads in the first 8 MFMA slots (the compiler still places
+    // them at slots 16-54: tools/isa_step.py; giving the row scalars slots of their own as
+    // well, ahead of the operands, was 3 % slower at C3 FITC); the t variants pin them instead
+    mfma_interleave<false, SGP_SYRK_IL_PAT, WITH_T ? 0 : 8>();
     // t: at most one W-column slice per workgroup, shared by all four waves (TR = BK / (256 / W)
     // rows per thread and step), from the current buffer (the stores above went to the other).
     // Branch-free, so it stays inside the step's basic block and its LDS reads interleave with
