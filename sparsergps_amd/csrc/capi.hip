@@ -1725,17 +1725,26 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
                      (fabs(c->lap_obj - c->lap_obj_prev) > c->lap_tol || c->lap_cnt > 0.0));
     if (go) {   // NR part a: grad_psi and K^T (grad_psi / omzw)
       Scope t(c, "lap_nr_a");
-      HIPCHK(launch_gemv_rows(c->K, n_pad, mp, lmv(c, LM_X1), nullptr, lvec(c, LV_Y1), nullptr,
-                              c->stream));
-      int nb = 0;
-      HIPCHK(launch_lap_nr_a(n, n_pad, lvec(c, LV_F), c->y, c->mu, lvec(c, LV_Z), lvec(c, LV_ZI),
-                             c->lap_expo, lvec(c, LV_Y1), c->lap_tol, lvec(c, LV_G),
-                             lvec(c, LV_OMZW), lvec(c, LV_V), lvec(c, LV_GPSI), c->slab_small,
-                             &nb, c->stream));
+      if (mp <= 2048 && lap_nr_a_fused_slab(n_pad, mp) <= c->lslab_cap) {
+        // one pass over K12: y1 = K x1, the row update and K^T v from the same staged rows
+        HIPCHK(launch_lap_nr_a_fused(c->K, n, n_pad, mp, lmv(c, LM_X1), lvec(c, LV_F), c->y,
+                                     c->mu, lvec(c, LV_Z), lvec(c, LV_ZI), c->lap_expo,
+                                     c->lap_tol, lvec(c, LV_Y1), lvec(c, LV_G), lvec(c, LV_OMZW),
+                                     lvec(c, LV_V), lvec(c, LV_GPSI), c->lslab, c->lslab_cap,
+                                     red_out, red_out + mp, c->stream));
+      } else {
+        HIPCHK(launch_gemv_rows(c->K, n_pad, mp, lmv(c, LM_X1), nullptr, lvec(c, LV_Y1), nullptr,
+                                c->stream));
+        int nb = 0;
+        HIPCHK(launch_lap_nr_a(n, n_pad, lvec(c, LV_F), c->y, c->mu, lvec(c, LV_Z),
+                               lvec(c, LV_ZI), c->lap_expo, lvec(c, LV_Y1), c->lap_tol,
+                               lvec(c, LV_G), lvec(c, LV_OMZW), lvec(c, LV_V), lvec(c, LV_GPSI),
+                               c->slab_small, &nb, c->stream));
+        HIPCHK(launch_gemv_cols(c->K, n_pad, mp, lvec(c, LV_V), n_pad, 1, c->lslab, c->lslab_cap,
+                                red_out, c->stream));
+        HIPCHK(launch_colsum(c->slab_small, nb, 1, red_out + mp, c->stream));
+      }
       c->lap_gpsi_valid = true;
-      HIPCHK(launch_gemv_cols(c->K, n_pad, mp, lvec(c, LV_V), n_pad, 1, c->lslab, c->lslab_cap,
-                              red_out, c->stream));
-      HIPCHK(launch_colsum(c->slab_small, nb, 1, red_out + mp, c->stream));
       *count = mp + 1;
       c->lap_state = LS_NRB;
       return SGP_OK;
@@ -1752,13 +1761,13 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
     }
     // gradient part a (dlogq_dcov_par at the final f)
     Scope t(c, "lap_grad_a");
-    HIPCHK(launch_gemv_rows(c->K, n_pad, mp, lmv(c, LM_X1), nullptr, lvec(c, LV_Y1), nullptr,
-                            c->stream));
-    HIPCHK(launch_rowquad_knm(kp, c->K, c->Binv, n, n_pad, c->m, mp, c->r, 0.0, nullptr, nullptr,
-                              nullptr, c->rowq, lvec(c, LV_P), c->stream,
-                              tstore_ready(c) ? c->tp : nullptr));
+    // c2 = (rf - K x1) / Z rides in the row-quadratic pass's k-loop as its fused alpha (the
+    // K x1 dot products from the staged K values): no separate K x1 pass
+    HIPCHK(launch_rowquad_knm(kp, c->K, c->Binv, n, n_pad, c->m, mp, lvec(c, LV_RF), 0.0,
+                              lvec(c, LV_ZI), lmv(c, LM_X1), lvec(c, LV_C2), c->rowq,
+                              lvec(c, LV_P), c->stream, tstore_ready(c) ? c->tp : nullptr));
     HIPCHK(launch_lap_grad_a(n, n_pad, lvec(c, LV_F), c->y, c->mu, lvec(c, LV_Z), lvec(c, LV_ZI),
-                             c->lap_expo, lvec(c, LV_Y1), lvec(c, LV_P), lvec(c, LV_C2),
+                             c->lap_expo, nullptr, lvec(c, LV_P), lvec(c, LV_C2),
                              lvec(c, LV_G), lvec(c, LV_B), lvec(c, LV_DMT), lvec(c, LV_SV),
                              lvec(c, LV_BSV), c->stream));
     HIPCHK(launch_gemv_cols(c->K, n_pad, mp, lvec(c, LV_C2), n_pad, 3, c->lslab, c->lslab_cap,

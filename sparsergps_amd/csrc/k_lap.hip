@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(256) k_lap_nr_b(int64_t n, int64_t n_pad,
 }
 
 // Gradient rows, part a (laplace_approx_gradient.R:133-178): with p_i = k_i^T C k_i,
-//   c2 = rf/Z - y1/Z, B = 1/(Z - 1/W), dMt = B - B^2 p  (diag of Sigma~^-1),
+//   c2 = rf/Z - y1/Z (left as passed in when y1 == nullptr), B = 1/(Z - 1/W), dMt = B - B^2 p  (diag of Sigma~^-1),
 //   comp4 = -1/D + (1/(Z D))^2 p  (D = W - 1/Z),  sv = comp4 (-W3)(-1/W),  bsv = B sv.
 __global__ void __launch_bounds__(256) k_lap_grad_a(int64_t n, int64_t n_pad,
                                                     const double* __restrict__ f,
@@ -169,7 +169,7 @@ __global__ void __launch_bounds__(256) k_lap_grad_a(int64_t n, int64_t n_pad,
       const double zi = Z[i], iz = zinv[i];
       const double bi = 1.0 / (zi - 1.0 / W);
       const double pi = p[i];
-      c2[i] = iz * (f[i] - mu[i]) - iz * y1[i];
+      if (y1) c2[i] = iz * (f[i] - mu[i]) - iz * y1[i];   // else c2 came with p (fused alpha)
       g[i] = -expo * e + y[i];
       B[i] = bi;
       dMt[i] = bi - bi * bi * pi;
@@ -287,6 +287,146 @@ __global__ void __launch_bounds__(128) k_gemv_cols(const double* __restrict__ K,
   double* o = part + (ch * NV) * mp + j;
 #pragma unroll
   for (int v = 0; v < NV; ++v) o[v * mp] = acc[v];
+}
+
+// NR step, part a in one pass over K12 (replaces k_gemv_rows + k_lap_nr_a + k_gemv_cols<1>,
+// which read K twice): per row block of R = 8192 / mp rows staged in LDS (64 KB),
+//   y1_i = K_i x1 (one wave per row), the k_lap_nr_a row update (g, omzw, v, gpsi, the
+//   stop-rule count) by one thread per row, then part[ch][j] += sum_i K_ij v_i from the same
+//   LDS image.  The next block's rows and row vectors are loaded into registers while the
+//   current one is processed.  One workgroup per row chunk; part[ch][0..mp) and cnt[ch] are
+// reduced by launch_colsum (fixed order).  mp <= 2048 (x1 staged beside the rows).
+constexpr int NRA_LDS = 8192;                 // doubles of the row-block image
+constexpr int NRA_LD2 = NRA_LDS / 512;        // double2 loads per thread and block
+__global__ void __launch_bounds__(256) k_lap_nr_a_fused(const double* __restrict__ K,
+                                                        int64_t n, int64_t n_pad, int64_t mp,
+                                                        int64_t chunk,
+                                                        const double* __restrict__ x1,
+                                                        const double* __restrict__ f,
+                                                        const double* __restrict__ y,
+                                                        const double* __restrict__ mu,
+                                                        const double* __restrict__ Z,
+                                                        const double* __restrict__ zinv,
+                                                        double expo, double tol,
+                                                        double* __restrict__ y1,
+                                                        double* __restrict__ g,
+                                                        double* __restrict__ omzw,
+                                                        double* __restrict__ v,
+                                                        double* __restrict__ gpsi,
+                                                        double* __restrict__ part,
+                                                        double* __restrict__ cnt) {
+  extern __shared__ __attribute__((aligned(16))) double nra_lds[];
+  double* Ks = nra_lds;                 // [R][mp]
+  double* xs = nra_lds + NRA_LDS;       // [mp]
+  __shared__ double s_v[64], s_dot[64], s_rv[5][64];
+  __shared__ double s_cnt[4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int R = (int)(NRA_LDS / mp);
+  const int64_t ch = blockIdx.x;
+  const int64_t i0 = ch * chunk;
+  const int64_t i1 = (i0 + chunk < n_pad) ? i0 + chunk : n_pad;
+  for (int64_t j = tid; j < mp; j += 256) xs[j] = x1[j];
+  constexpr int NCOL = 8;               // columns per thread: mp <= 2048
+  double acc[NCOL];
+#pragma unroll
+  for (int q = 0; q < NCOL; ++q) acc[q] = 0.0;
+  double cacc = 0.0;
+  double2 t[NRA_LD2];
+  double rv[5];
+  // block b0's rows (guarded: the chunk's last block may be short) and, for thread r < rows,
+  // row b0 + r's vectors
+  auto load_block = [&](int64_t b0) {
+    const int rows = (int)((b0 + R <= i1) ? R : i1 - b0);
+    const double2* src = reinterpret_cast<const double2*>(K + b0 * mp);
+    const int64_t nv2 = (int64_t)rows * mp / 2;
+#pragma unroll
+    for (int q = 0; q < NRA_LD2; ++q) {
+      const int64_t e = tid + 256 * q;
+      t[q] = (e < nv2) ? src[e] : make_double2(0.0, 0.0);
+    }
+    if (tid < rows && b0 + tid < n) {   // rows past n: the vectors may end at n
+      const int64_t i = b0 + tid;
+      rv[0] = f[i]; rv[1] = y[i]; rv[2] = mu[i]; rv[3] = Z[i]; rv[4] = zinv[i];
+    }
+  };
+  if (i0 < i1) load_block(i0);
+  for (int64_t b0 = i0; b0 < i1; b0 += R) {
+    const int rows = (int)((b0 + R <= i1) ? R : i1 - b0);
+    __syncthreads();                    // the previous block's image and vectors are read
+    {
+      double2* dst = reinterpret_cast<double2*>(Ks);
+#pragma unroll
+      for (int q = 0; q < NRA_LD2; ++q) dst[tid + 256 * q] = t[q];
+      if (tid < rows) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) s_rv[k][tid] = rv[k];
+      }
+    }
+    __syncthreads();
+    if (b0 + R < i1) load_block(b0 + R);   // in flight while this block is processed
+    // y1, one wave per row
+    for (int r = wv; r < rows; r += 4) {
+      const double* kr = Ks + (int64_t)r * mp;
+      double s0 = 0.0, s1 = 0.0;
+      int64_t j = lane;
+      for (; j + 64 < mp; j += 128) {
+        s0 = fma(kr[j], xs[j], s0);
+        s1 = fma(kr[j + 64], xs[j + 64], s1);
+      }
+      if (j < mp) s0 = fma(kr[j], xs[j], s0);
+      const double sd = wave_sum(s0 + s1);
+      if (lane == 0) s_dot[r] = sd;
+    }
+    __syncthreads();
+    // the row update, one thread per row
+    if (tid < rows) {
+      const int64_t i = b0 + tid;
+      const double sd = s_dot[tid];
+      double vi = 0.0;
+      if (i < n) {
+        const double fi = s_rv[0][tid], yi = s_rv[1][tid], mui = s_rv[2][tid];
+        const double zi = s_rv[3][tid], iz = s_rv[4][tid];
+        const double e = exp(fi);
+        const double W = -expo * e;
+        const double gi = -expo * e + yi;
+        const double om = 1.0 - zi * W;
+        const double gp = gi + (-iz * (fi - mui) + iz * sd);
+        vi = (1.0 / om) * gp;
+        g[i] = gi;
+        omzw[i] = om;
+        gpsi[i] = gp;
+        if (fabs(gp) > tol) cacc += 1.0;
+      } else {
+        g[i] = 0.0;
+        omzw[i] = 1.0;
+        gpsi[i] = 0.0;
+      }
+      y1[i] = sd;
+      v[i] = vi;
+      s_v[tid] = vi;
+    }
+    __syncthreads();
+    // K^T v over the block's rows, in row order
+#pragma unroll
+    for (int q = 0; q < NCOL; ++q) {
+      const int64_t j = tid + 256 * q;
+      if (j < mp) {
+        double a = acc[q];
+        for (int r = 0; r < rows; ++r) a = fma(Ks[(int64_t)r * mp + j], s_v[r], a);
+        acc[q] = a;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NCOL; ++q) {
+    const int64_t j = tid + 256 * q;
+    if (j < mp) part[ch * mp + j] = acc[q];
+  }
+  // the count: threads 0..R-1 hold their rows' part (all in wave 0: R <= 64)
+  if (wv == 0) {
+    const double cw = wave_sum(cacc);
+    if (lane == 0) cnt[ch] = cw;
+  }
 }
 
 // part[ch][j] = sum_{i in chunk ch} K_ij^2
@@ -425,6 +565,40 @@ hipError_t launch_lap_nr_a(int64_t n, int64_t n_pad, const double* f, const doub
   hipLaunchKernelGGL(k_lap_nr_a, dim3(nb), dim3(256), 0, s, n, n_pad, f, y, mu, Z, zinv, expo, y1,
                      tol, g, omzw, v, gpsi, slab);
   return hipGetLastError();
+}
+
+int64_t lap_nr_a_fused_chunks(int64_t n_pad, int64_t mp) {
+  // ~8 row blocks per workgroup, at most LAP_NB x 4 workgroups
+  const int64_t R = NRA_LDS / mp;
+  int64_t nch = (n_pad + 8 * R - 1) / (8 * R);
+  if (nch > 4 * LAP_NB) nch = 4 * LAP_NB;
+  return nch < 1 ? 1 : nch;
+}
+
+int64_t lap_nr_a_fused_slab(int64_t n_pad, int64_t mp) {
+  const int64_t nch = lap_nr_a_fused_chunks(n_pad, mp);
+  return nch * mp + nch;
+}
+
+hipError_t launch_lap_nr_a_fused(const double* K, int64_t n, int64_t n_pad, int64_t mp,
+                                 const double* x1, const double* f, const double* y,
+                                 const double* mu, const double* Z, const double* zinv,
+                                 double expo, double tol, double* y1, double* g, double* omzw,
+                                 double* v, double* gpsi, double* part, int64_t part_cap,
+                                 double* out, double* out_cnt, hipStream_t s) {
+  if (mp < 128 || mp > 2048 || mp % 128 != 0) return hipErrorInvalidValue;
+  const int64_t nch = lap_nr_a_fused_chunks(n_pad, mp);
+  if (nch * mp + nch > part_cap) return hipErrorInvalidValue;
+  const int64_t chunk = (n_pad + nch - 1) / nch;
+  const size_t shmem = sizeof(double) * (size_t)(NRA_LDS + mp);
+  double* cnt = part + nch * mp;
+  hipLaunchKernelGGL(k_lap_nr_a_fused, dim3((unsigned)nch), dim3(256), shmem, s, K, n, n_pad, mp,
+                     chunk, x1, f, y, mu, Z, zinv, expo, tol, y1, g, omzw, v, gpsi, part, cnt);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = launch_colsum(part, nch, mp, out, s);
+  if (e != hipSuccess) return e;
+  return launch_colsum(cnt, nch, 1, out_cnt, s);
 }
 
 hipError_t launch_lap_nr_b(int64_t n, int64_t n_pad, double* f, const double* mu, const double* Z,
