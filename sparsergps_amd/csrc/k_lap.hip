@@ -296,7 +296,10 @@ __global__ void __launch_bounds__(128) k_gemv_cols(const double* __restrict__ K,
 //   LDS image.  The next block's rows and row vectors are loaded into registers while the
 //   current one is processed.  One workgroup per row chunk; part[ch][0..mp) and cnt[ch] are
 // reduced by launch_colsum (fixed order).  mp <= 2048 (x1 staged beside the rows).
-constexpr int NRA_LDS = 8192;                 // doubles of the row-block image
+#ifndef SGP_NRA_LDS
+#define SGP_NRA_LDS 8192
+#endif
+constexpr int NRA_LDS = SGP_NRA_LDS;          // doubles of the row-block image
 constexpr int NRA_LD2 = NRA_LDS / 512;        // double2 loads per thread and block
 __global__ void __launch_bounds__(256) k_lap_nr_a_fused(const double* __restrict__ K,
                                                         int64_t n, int64_t n_pad, int64_t mp,
@@ -318,7 +321,8 @@ __global__ void __launch_bounds__(256) k_lap_nr_a_fused(const double* __restrict
   extern __shared__ __attribute__((aligned(16))) double nra_lds[];
   double* Ks = nra_lds;                 // [R][mp]
   double* xs = nra_lds + NRA_LDS;       // [mp]
-  __shared__ double s_v[64], s_dot[64], s_rv[5][64];
+  constexpr int RMAX = NRA_LDS / 128;   // rows of a block at the smallest mp
+  __shared__ double s_v[RMAX], s_dot[RMAX], s_rv[5][RMAX];
   __shared__ double s_cnt[4];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int R = (int)(NRA_LDS / mp);
@@ -364,18 +368,20 @@ __global__ void __launch_bounds__(256) k_lap_nr_a_fused(const double* __restrict
     }
     __syncthreads();
     if (b0 + R < i1) load_block(b0 + R);   // in flight while this block is processed
-    // y1, one wave per row
-    for (int r = wv; r < rows; r += 4) {
-      const double* kr = Ks + (int64_t)r * mp;
-      double s0 = 0.0, s1 = 0.0;
-      int64_t j = lane;
-      for (; j + 64 < mp; j += 128) {
-        s0 = fma(kr[j], xs[j], s0);
-        s1 = fma(kr[j + 64], xs[j + 64], s1);
+    // y1, one wave per row, four rows of a wave at a time (independent dot chains)
+    for (int r0 = wv; r0 < rows; r0 += 16) {
+      double sd[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int64_t j = lane; j < mp; j += 64) {
+        const double xv = xs[j];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (r0 + 4 * k < rows) sd[k] = fma(Ks[(int64_t)(r0 + 4 * k) * mp + j], xv, sd[k]);
       }
-      if (j < mp) s0 = fma(kr[j], xs[j], s0);
-      const double sd = wave_sum(s0 + s1);
-      if (lane == 0) s_dot[r] = sd;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double w = wave_sum(sd[k]);
+        if (lane == 0 && r0 + 4 * k < rows) s_dot[r0 + 4 * k] = w;
+      }
     }
     __syncthreads();
     // the row update, one thread per row
@@ -412,7 +418,16 @@ __global__ void __launch_bounds__(256) k_lap_nr_a_fused(const double* __restrict
       const int64_t j = tid + 256 * q;
       if (j < mp) {
         double a = acc[q];
-        for (int r = 0; r < rows; ++r) a = fma(Ks[(int64_t)r * mp + j], s_v[r], a);
+        int r = 0;
+        for (; r + 4 <= rows; r += 4) {   // the four reads issued together, summed in row order
+          const double k0 = Ks[(int64_t)r * mp + j], k1 = Ks[(int64_t)(r + 1) * mp + j];
+          const double k2 = Ks[(int64_t)(r + 2) * mp + j], k3 = Ks[(int64_t)(r + 3) * mp + j];
+          a = fma(k0, s_v[r], a);
+          a = fma(k1, s_v[r + 1], a);
+          a = fma(k2, s_v[r + 2], a);
+          a = fma(k3, s_v[r + 3], a);
+        }
+        for (; r < rows; ++r) a = fma(Ks[(int64_t)r * mp + j], s_v[r], a);
         acc[q] = a;
       }
     }
@@ -422,10 +437,12 @@ __global__ void __launch_bounds__(256) k_lap_nr_a_fused(const double* __restrict
     const int64_t j = tid + 256 * q;
     if (j < mp) part[ch * mp + j] = acc[q];
   }
-  // the count: threads 0..R-1 hold their rows' part (all in wave 0: R <= 64)
-  if (wv == 0) {
+  // the count: threads 0..R-1 hold their rows' part
+  {
     const double cw = wave_sum(cacc);
-    if (lane == 0) cnt[ch] = cw;
+    if (lane == 0) s_cnt[wv] = cw;
+    __syncthreads();
+    if (tid == 0) cnt[ch] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
   }
 }
 
