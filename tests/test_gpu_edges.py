@@ -84,7 +84,9 @@ def test_fitc_edge_shapes(sgp, n, m, d, cov_fun):
     _close(obj, grad, o, g, cp)
 
 
-@pytest.mark.parametrize("n,m", [(60, 150), (1024, 128), (1025, 129)])
+# (777, 300) and (500, 1100): knot tiles (mp = 384, 1152) that do not divide the fused Newton
+# pass's 8192-double row image (k_lap_nr_a_fused: 21- and 7-row blocks, short last blocks)
+@pytest.mark.parametrize("n,m", [(60, 150), (1024, 128), (1025, 129), (777, 300), (500, 1100)])
 def test_laplace_edge_shapes(sgp, n, m):
     P = O.make_poisson_problem(n=n, m=m)
     cp = P["cov_par"]
