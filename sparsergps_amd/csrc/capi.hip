@@ -1688,6 +1688,7 @@ static int lap_consume_obj(sgp_ctx* c, const double* red, int64_t o, bool first,
                                                : "Sigma22 + t(Sigma12) %*% (B * Sigma12)"));
     return SGP_ENOTPD;
   }
+  if (!first) c->lap_cnt = sc[SC_RR + 3];   // the count of the step that led here (nr_b)
   const double ld22 = 2.0 * sc[SC_LD22], ldB = 2.0 * sc[SC_LDB];
   const double rr = sc[SC_RR], logpy = sc[SC_RR + 1], logz2 = sc[SC_RR + 2], tu = sc[SC_TU];
   // laplace_approx_obj_funs.R:158-172: quad + log p(y|f) + det_part_1 + det_part_2
@@ -1779,17 +1780,15 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
   if (st_in == LS_NRB) {
     {
       Scope t(c, "lap_nr_b");
+      // the stop-rule count rides to the host with the next objective's scalars (sc is read
+      // back by lap_consume_obj): no host round trip inside the Newton step
       HIPCHK(hipMemcpyAsync(c->sc + SC_RR + 3, red_in + mp, sizeof(double),
                             hipMemcpyDeviceToDevice, c->stream));
-      double cnt = 0.0;
-      HIPCHK(hipMemcpyAsync(&cnt, red_in + mp, sizeof(double), hipMemcpyDeviceToHost, c->stream));
       HIPCHK(dense_gemv(c->Binv, mp, red_in, 1.0, lmv(c, LM_X2), c->stream));
       HIPCHK(launch_gemv_rows(c->K, n_pad, mp, lmv(c, LM_X2), nullptr, lvec(c, LV_Y2), nullptr,
                               c->stream));
       HIPCHK(launch_lap_nr_b(n, n_pad, lvec(c, LV_F), c->mu, lvec(c, LV_Z), lvec(c, LV_G),
                              lvec(c, LV_OMZW), lvec(c, LV_Y1), lvec(c, LV_Y2), c->stream));
-      HIPCHK(hipStreamSynchronize(c->stream));
-      c->lap_cnt = cnt;
     }
     int st = lap_obj_partials(c, red_out, 0);
     if (st) return st;
