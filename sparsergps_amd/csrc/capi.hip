@@ -1726,7 +1726,7 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
                      (fabs(c->lap_obj - c->lap_obj_prev) > c->lap_tol || c->lap_cnt > 0.0));
     if (go) {   // NR part a: grad_psi and K^T (grad_psi / omzw)
       Scope t(c, "lap_nr_a");
-      if (mp <= 2048 && lap_nr_a_fused_slab(n_pad, mp) <= c->lslab_cap) {
+      if (mp <= 2048 && lap_rowpass_slab(n_pad, mp) <= c->lslab_cap) {
         // one pass over K12: y1 = K x1, the row update and K^T v from the same staged rows
         HIPCHK(launch_lap_nr_a_fused(c->K, n, n_pad, mp, lmv(c, LM_X1), lvec(c, LV_F), c->y,
                                      c->mu, lvec(c, LV_Z), lvec(c, LV_ZI), c->lap_expo,
@@ -1778,6 +1778,8 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
     return SGP_OK;
   }
   if (st_in == LS_NRB) {
+    // NR part b and the next objective's rows fused into one K pass where the knot count allows
+    const bool fused = mp <= 2048 && lap_rowpass_slab(n_pad, mp) <= c->lslab_cap;
     {
       Scope t(c, "lap_nr_b");
       // the stop-rule count rides to the host with the next objective's scalars (sc is read
@@ -1785,10 +1787,32 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
       HIPCHK(hipMemcpyAsync(c->sc + SC_RR + 3, red_in + mp, sizeof(double),
                             hipMemcpyDeviceToDevice, c->stream));
       HIPCHK(dense_gemv(c->Binv, mp, red_in, 1.0, lmv(c, LM_X2), c->stream));
-      HIPCHK(launch_gemv_rows(c->K, n_pad, mp, lmv(c, LM_X2), nullptr, lvec(c, LV_Y2), nullptr,
-                              c->stream));
-      HIPCHK(launch_lap_nr_b(n, n_pad, lvec(c, LV_F), c->mu, lvec(c, LV_Z), lvec(c, LV_G),
-                             lvec(c, LV_OMZW), lvec(c, LV_Y1), lvec(c, LV_Y2), c->stream));
+      if (!fused) {
+        HIPCHK(launch_gemv_rows(c->K, n_pad, mp, lmv(c, LM_X2), nullptr, lvec(c, LV_Y2),
+                                nullptr, c->stream));
+        HIPCHK(launch_lap_nr_b(n, n_pad, lvec(c, LV_F), c->mu, lvec(c, LV_Z), lvec(c, LV_G),
+                               lvec(c, LV_OMZW), lvec(c, LV_Y1), lvec(c, LV_Y2), c->stream));
+      }
+    }
+    if (fused) {
+      // one K pass: y2 = K x2, the f update and t = K^T tv at the new f (red_out + mm) with
+      // tv'(f - mu) (red_out + mm + mp); k_lap_obj's rows (B, rf, tv, the likelihood sums) and
+      // S_B by the weighted SYRK without t (red_out)
+      Scope t(c, "lap_obj");
+      HIPCHK(launch_lap_nr_b_t_fused(c->K, n, n_pad, mp, lmv(c, LM_X2), lvec(c, LV_F), c->y,
+                                     c->mu, lvec(c, LV_Z), lvec(c, LV_ZI), lvec(c, LV_G),
+                                     lvec(c, LV_OMZW), lvec(c, LV_Y1), c->lslab, c->lslab_cap,
+                                     red_out + mm, red_out + mm + mp, c->stream));
+      int nb = 0;
+      HIPCHK(launch_lap_obj(n, n_pad, lvec(c, LV_F), c->y, c->mu, lvec(c, LV_Z), lvec(c, LV_ZI),
+                            c->lap_expo, lvec(c, LV_B), lvec(c, LV_RF), lvec(c, LV_TV),
+                            c->slab_small, &nb, c->stream));
+      HIPCHK(launch_syrk_aug(c->K, n_pad, mp, lvec(c, LV_RF), lvec(c, LV_B), c->slab_syrk,
+                             c->slab_syrk_cap, red_out, c->stream, 3, nullptr, 0));
+      HIPCHK(launch_colsum(c->slab_small, nb, 2, red_out + mm + mp + 1, c->stream));
+      *count = mm + mp + 3;
+      c->lap_state = LS_OBJ;
+      return SGP_OK;
     }
     int st = lap_obj_partials(c, red_out, 0);
     if (st) return st;

@@ -289,54 +289,64 @@ __global__ void __launch_bounds__(128) k_gemv_cols(const double* __restrict__ K,
   for (int v = 0; v < NV; ++v) o[v * mp] = acc[v];
 }
 
-// NR step, part a in one pass over K12 (replaces k_gemv_rows + k_lap_nr_a + k_gemv_cols<1>,
-// which read K twice): per row block of R = 8192 / mp rows staged in LDS (64 KB),
-//   y1_i = K_i x1 (one wave per row), the k_lap_nr_a row update (g, omzw, v, gpsi, the
-//   stop-rule count) by one thread per row, then part[ch][j] += sum_i K_ij v_i from the same
-//   LDS image.  The next block's rows and row vectors are loaded into registers while the
-//   current one is processed.  One workgroup per row chunk; part[ch][0..mp) and cnt[ch] are
-// reduced by launch_colsum (fixed order).  mp <= 2048 (x1 staged beside the rows).
+// Newton-step passes over K12 that each replace a row GEMV, a per-row kernel and a column GEMV
+// (two K reads) by one read: per row block of R = 8192 / mp rows staged in LDS (64 KB; the next
+// block's rows and row vectors are loaded into registers while the current one is processed),
+//   d_i = K_i x (one wave per row, four rows of a wave at a time), a per-row update by one
+//   thread per row, then part[ch][j] += sum_i K_ij v_i from the same LDS image.
+// LAP_PASS_A (NR part a): x = x1, the k_lap_nr_a update (y1 = d, g, omzw, gpsi), v = gpsi/omzw,
+//   scalars = [stop-rule count].
+// LAP_PASS_B (NR part b + the next objective's t): x = x2, the k_lap_nr_b update of f
+//   (y2 = d), v = tv = (f - mu)/Z at the new f (t = K^T tv), scalars = [sum tv (f - mu)];
+//   k_lap_obj then forms B, rf, tv and the likelihood sums in its own (cheap, fully parallel)
+//   pass and S_B comes from the weighted SYRK without t.
+// One workgroup per row chunk; part[ch][0..mp) and the scalars sc[ch][..] are reduced by
+// launch_colsum (fixed order).  mp <= 2048 (x staged beside the rows).
 #ifndef SGP_NRA_LDS
 #define SGP_NRA_LDS 8192
 #endif
 constexpr int NRA_LDS = SGP_NRA_LDS;          // doubles of the row-block image
 constexpr int NRA_LD2 = NRA_LDS / 512;        // double2 loads per thread and block
-__global__ void __launch_bounds__(256) k_lap_nr_a_fused(const double* __restrict__ K,
-                                                        int64_t n, int64_t n_pad, int64_t mp,
-                                                        int64_t chunk,
-                                                        const double* __restrict__ x1,
-                                                        const double* __restrict__ f,
-                                                        const double* __restrict__ y,
-                                                        const double* __restrict__ mu,
-                                                        const double* __restrict__ Z,
-                                                        const double* __restrict__ zinv,
-                                                        double expo, double tol,
-                                                        double* __restrict__ y1,
-                                                        double* __restrict__ g,
-                                                        double* __restrict__ omzw,
-                                                        double* __restrict__ v,
-                                                        double* __restrict__ gpsi,
-                                                        double* __restrict__ part,
-                                                        double* __restrict__ cnt) {
+enum { LAP_PASS_A = 0, LAP_PASS_B = 1 };
+
+struct LapPassArgs {
+  const double* x;                            // x1 (A) / x2 (B), mp
+  double* f;                                  // A: read; B: updated
+  const double *y, *mu, *Z, *zinv;
+  const double *g_in, *omzw_in, *y1_in;       // B
+  double expo, tol;                           // A
+  double *y1, *g, *omzw, *v, *gpsi;           // A outputs
+  double* part;                               // [nch][mp]
+  double* sc;                                 // [nch][NS]
+};
+
+template <int MODE>
+__global__ void __launch_bounds__(256) k_lap_rowpass(const double* __restrict__ K, int64_t n,
+                                                     int64_t n_pad, int64_t mp, int64_t chunk,
+                                                     LapPassArgs pa) {
+  constexpr int NV = MODE == LAP_PASS_A ? 5 : 8;      // row vectors staged per row
+  constexpr int NS = 1;                                // scalar sums
   extern __shared__ __attribute__((aligned(16))) double nra_lds[];
   double* Ks = nra_lds;                 // [R][mp]
   double* xs = nra_lds + NRA_LDS;       // [mp]
   constexpr int RMAX = NRA_LDS / 128;   // rows of a block at the smallest mp
-  __shared__ double s_v[RMAX], s_dot[RMAX], s_rv[5][RMAX];
-  __shared__ double s_cnt[4];
+  __shared__ double s_v[RMAX], s_dot[RMAX], s_rv[NV][RMAX];
+  __shared__ double s_red[4][NS];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int R = (int)(NRA_LDS / mp);
   const int64_t ch = blockIdx.x;
   const int64_t i0 = ch * chunk;
   const int64_t i1 = (i0 + chunk < n_pad) ? i0 + chunk : n_pad;
-  for (int64_t j = tid; j < mp; j += 256) xs[j] = x1[j];
+  for (int64_t j = tid; j < mp; j += 256) xs[j] = pa.x[j];
   constexpr int NCOL = 8;               // columns per thread: mp <= 2048
   double acc[NCOL];
 #pragma unroll
   for (int q = 0; q < NCOL; ++q) acc[q] = 0.0;
-  double cacc = 0.0;
+  double sacc[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) sacc[k] = 0.0;
   double2 t[NRA_LD2];
-  double rv[5];
+  double rv[NV];
   // block b0's rows (guarded: the chunk's last block may be short) and, for thread r < rows,
   // row b0 + r's vectors
   auto load_block = [&](int64_t b0) {
@@ -350,7 +360,10 @@ __global__ void __launch_bounds__(256) k_lap_nr_a_fused(const double* __restrict
     }
     if (tid < rows && b0 + tid < n) {   // rows past n: the vectors may end at n
       const int64_t i = b0 + tid;
-      rv[0] = f[i]; rv[1] = y[i]; rv[2] = mu[i]; rv[3] = Z[i]; rv[4] = zinv[i];
+      rv[0] = pa.f[i]; rv[1] = pa.y[i]; rv[2] = pa.mu[i]; rv[3] = pa.Z[i]; rv[4] = pa.zinv[i];
+      if constexpr (MODE == LAP_PASS_B) {
+        rv[5] = pa.g_in[i]; rv[6] = pa.omzw_in[i]; rv[7] = pa.y1_in[i];
+      }
     }
   };
   if (i0 < i1) load_block(i0);
@@ -363,12 +376,12 @@ __global__ void __launch_bounds__(256) k_lap_nr_a_fused(const double* __restrict
       for (int q = 0; q < NRA_LD2; ++q) dst[tid + 256 * q] = t[q];
       if (tid < rows) {
 #pragma unroll
-        for (int k = 0; k < 5; ++k) s_rv[k][tid] = rv[k];
+        for (int k = 0; k < NV; ++k) s_rv[k][tid] = rv[k];
       }
     }
     __syncthreads();
     if (b0 + R < i1) load_block(b0 + R);   // in flight while this block is processed
-    // y1, one wave per row, four rows of a wave at a time (independent dot chains)
+    // d = K x, one wave per row, four rows of a wave at a time (independent dot chains)
     for (int r0 = wv; r0 < rows; r0 += 16) {
       double sd[4] = {0.0, 0.0, 0.0, 0.0};
       for (int64_t j = lane; j < mp; j += 64) {
@@ -389,26 +402,42 @@ __global__ void __launch_bounds__(256) k_lap_nr_a_fused(const double* __restrict
       const int64_t i = b0 + tid;
       const double sd = s_dot[tid];
       double vi = 0.0;
-      if (i < n) {
-        const double fi = s_rv[0][tid], yi = s_rv[1][tid], mui = s_rv[2][tid];
-        const double zi = s_rv[3][tid], iz = s_rv[4][tid];
-        const double e = exp(fi);
-        const double W = -expo * e;
-        const double gi = -expo * e + yi;
-        const double om = 1.0 - zi * W;
-        const double gp = gi + (-iz * (fi - mui) + iz * sd);
-        vi = (1.0 / om) * gp;
-        g[i] = gi;
-        omzw[i] = om;
-        gpsi[i] = gp;
-        if (fabs(gp) > tol) cacc += 1.0;
-      } else {
-        g[i] = 0.0;
-        omzw[i] = 1.0;
-        gpsi[i] = 0.0;
+      const double fi = s_rv[0][tid], yi = s_rv[1][tid], mui = s_rv[2][tid];
+      const double zi = s_rv[3][tid], iz = s_rv[4][tid];
+      if constexpr (MODE == LAP_PASS_A) {   // k_lap_nr_a
+        if (i < n) {
+          const double e = exp(fi);
+          const double W = -pa.expo * e;
+          const double gi = -pa.expo * e + yi;
+          const double om = 1.0 - zi * W;
+          const double gp = gi + (-iz * (fi - mui) + iz * sd);
+          vi = (1.0 / om) * gp;
+          pa.g[i] = gi;
+          pa.omzw[i] = om;
+          pa.gpsi[i] = gp;
+          if (fabs(gp) > pa.tol) sacc[0] += 1.0;
+        } else {
+          pa.g[i] = 0.0;
+          pa.omzw[i] = 1.0;
+          pa.gpsi[i] = 0.0;
+        }
+        pa.y1[i] = sd;
+        pa.v[i] = vi;
+      } else {                              // k_lap_nr_b; tv = (f - mu)/Z at the new f
+        (void)yi;
+        if (i < n) {
+          const double gi = s_rv[5][tid], om = s_rv[6][tid], y1i = s_rv[7][tid];
+          const double a11 = (zi / om) * gi;
+          const double a12 = (1.0 / om) * (fi - mui);
+          const double a13 = y1i / om;
+          const double a2 = sd / om;
+          const double fn = fi + (a11 - a12 + a13 + a2);
+          pa.f[i] = fn;
+          const double r = fn - mui;
+          vi = iz * r;
+          sacc[0] = fma(vi, r, sacc[0]);
+        }
       }
-      y1[i] = sd;
-      v[i] = vi;
       s_v[tid] = vi;
     }
     __syncthreads();
@@ -435,15 +464,16 @@ __global__ void __launch_bounds__(256) k_lap_nr_a_fused(const double* __restrict
 #pragma unroll
   for (int q = 0; q < NCOL; ++q) {
     const int64_t j = tid + 256 * q;
-    if (j < mp) part[ch * mp + j] = acc[q];
+    if (j < mp) pa.part[ch * mp + j] = acc[q];
   }
-  // the count: threads 0..R-1 hold their rows' part
-  {
-    const double cw = wave_sum(cacc);
-    if (lane == 0) s_cnt[wv] = cw;
-    __syncthreads();
-    if (tid == 0) cnt[ch] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+  // the scalar sums: threads 0..R-1 hold their rows' parts
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    const double w = wave_sum(sacc[k]);
+    if (lane == 0) s_red[wv][k] = w;
   }
+  __syncthreads();
+  if (tid < NS) pa.sc[ch * NS + tid] = s_red[0][tid] + s_red[1][tid] + s_red[2][tid] + s_red[3][tid];
 }
 
 // part[ch][j] = sum_{i in chunk ch} K_ij^2
@@ -584,7 +614,7 @@ hipError_t launch_lap_nr_a(int64_t n, int64_t n_pad, const double* f, const doub
   return hipGetLastError();
 }
 
-int64_t lap_nr_a_fused_chunks(int64_t n_pad, int64_t mp) {
+int64_t lap_rowpass_chunks(int64_t n_pad, int64_t mp) {
   // ~8 row blocks per workgroup, at most LAP_NB x 4 workgroups
   const int64_t R = NRA_LDS / mp;
   int64_t nch = (n_pad + 8 * R - 1) / (8 * R);
@@ -592,10 +622,33 @@ int64_t lap_nr_a_fused_chunks(int64_t n_pad, int64_t mp) {
   return nch < 1 ? 1 : nch;
 }
 
-int64_t lap_nr_a_fused_slab(int64_t n_pad, int64_t mp) {
-  const int64_t nch = lap_nr_a_fused_chunks(n_pad, mp);
+int64_t lap_rowpass_slab(int64_t n_pad, int64_t mp) {
+  const int64_t nch = lap_rowpass_chunks(n_pad, mp);
   return nch * mp + nch;
 }
+
+namespace {
+template <int MODE>
+hipError_t launch_rowpass(const double* K, int64_t n, int64_t n_pad, int64_t mp, LapPassArgs pa,
+                          double* part, int64_t part_cap, double* out_t, double* out_sc,
+                          hipStream_t s) {
+  constexpr int NS = 1;
+  if (mp < 128 || mp > 2048 || mp % 128 != 0) return hipErrorInvalidValue;
+  const int64_t nch = lap_rowpass_chunks(n_pad, mp);
+  if (nch * mp + NS * nch > part_cap) return hipErrorInvalidValue;
+  const int64_t chunk = (n_pad + nch - 1) / nch;
+  const size_t shmem = sizeof(double) * (size_t)(NRA_LDS + mp);
+  pa.part = part;
+  pa.sc = part + nch * mp;
+  hipLaunchKernelGGL(k_lap_rowpass<MODE>, dim3((unsigned)nch), dim3(256), shmem, s, K, n, n_pad,
+                     mp, chunk, pa);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = launch_colsum(part, nch, mp, out_t, s);
+  if (e != hipSuccess) return e;
+  return launch_colsum(pa.sc, nch, NS, out_sc, s);
+}
+}  // namespace
 
 hipError_t launch_lap_nr_a_fused(const double* K, int64_t n, int64_t n_pad, int64_t mp,
                                  const double* x1, const double* f, const double* y,
@@ -603,19 +656,24 @@ hipError_t launch_lap_nr_a_fused(const double* K, int64_t n, int64_t n_pad, int6
                                  double expo, double tol, double* y1, double* g, double* omzw,
                                  double* v, double* gpsi, double* part, int64_t part_cap,
                                  double* out, double* out_cnt, hipStream_t s) {
-  if (mp < 128 || mp > 2048 || mp % 128 != 0) return hipErrorInvalidValue;
-  const int64_t nch = lap_nr_a_fused_chunks(n_pad, mp);
-  if (nch * mp + nch > part_cap) return hipErrorInvalidValue;
-  const int64_t chunk = (n_pad + nch - 1) / nch;
-  const size_t shmem = sizeof(double) * (size_t)(NRA_LDS + mp);
-  double* cnt = part + nch * mp;
-  hipLaunchKernelGGL(k_lap_nr_a_fused, dim3((unsigned)nch), dim3(256), shmem, s, K, n, n_pad, mp,
-                     chunk, x1, f, y, mu, Z, zinv, expo, tol, y1, g, omzw, v, gpsi, part, cnt);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  e = launch_colsum(part, nch, mp, out, s);
-  if (e != hipSuccess) return e;
-  return launch_colsum(cnt, nch, 1, out_cnt, s);
+  LapPassArgs pa{};
+  pa.x = x1; pa.f = const_cast<double*>(f); pa.y = y; pa.mu = mu; pa.Z = Z; pa.zinv = zinv;
+  pa.expo = expo; pa.tol = tol;
+  pa.y1 = y1; pa.g = g; pa.omzw = omzw; pa.v = v; pa.gpsi = gpsi;
+  return launch_rowpass<LAP_PASS_A>(K, n, n_pad, mp, pa, part, part_cap, out, out_cnt, s);
+}
+
+hipError_t launch_lap_nr_b_t_fused(const double* K, int64_t n, int64_t n_pad, int64_t mp,
+                                   const double* x2, double* f, const double* y,
+                                   const double* mu, const double* Z, const double* zinv,
+                                   const double* g, const double* omzw, const double* y1,
+                                   double* part, int64_t part_cap, double* out_t, double* out_rr,
+                                   hipStream_t s) {
+  LapPassArgs pa{};
+  pa.x = x2; pa.f = f; pa.y = y; pa.mu = mu; pa.Z = Z; pa.zinv = zinv;
+  pa.g_in = g; pa.omzw_in = omzw; pa.y1_in = y1;
+  double* out_sc = out_rr;
+  return launch_rowpass<LAP_PASS_B>(K, n, n_pad, mp, pa, part, part_cap, out_t, out_sc, s);
 }
 
 hipError_t launch_lap_nr_b(int64_t n, int64_t n_pad, double* f, const double* mu, const double* Z,

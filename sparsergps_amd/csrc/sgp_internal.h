@@ -279,14 +279,23 @@ hipError_t launch_lap_nr_a(int64_t n, int64_t n_pad, const double* f, const doub
                            const double* y1, double tol, double* g, double* omzw, double* v,
                            double* gpsi, double* slab, int* nblocks, hipStream_t s);
 // NR part a as one K pass (y1 = K x1, the row update above, out = K^T v, out_cnt = stop-rule
-// count); mp <= 2048; part: lap_nr_a_fused_slab(n_pad, mp) doubles.
+// count); mp <= 2048; part: lap_rowpass_slab(n_pad, mp) doubles.
 hipError_t launch_lap_nr_a_fused(const double* K, int64_t n, int64_t n_pad, int64_t mp,
                                  const double* x1, const double* f, const double* y,
                                  const double* mu, const double* Z, const double* zinv,
                                  double expo, double tol, double* y1, double* g, double* omzw,
                                  double* v, double* gpsi, double* part, int64_t part_cap,
                                  double* out, double* out_cnt, hipStream_t s);
-int64_t lap_nr_a_fused_slab(int64_t n_pad, int64_t mp);
+// NR part b + the next objective's t as one K pass: f updated in place (y2 = K x2), out_t =
+// K^T tv and out_rr = sum tv (f - mu) at the new f, tv = (f - mu)/Z.  mp <= 2048.
+hipError_t launch_lap_nr_b_t_fused(const double* K, int64_t n, int64_t n_pad, int64_t mp,
+                                   const double* x2, double* f, const double* y,
+                                   const double* mu, const double* Z, const double* zinv,
+                                   const double* g, const double* omzw, const double* y1,
+                                   double* part, int64_t part_cap, double* out_t, double* out_rr,
+                                   hipStream_t s);
+// work space of both fused passes (doubles)
+int64_t lap_rowpass_slab(int64_t n_pad, int64_t mp);
 hipError_t launch_lap_nr_b(int64_t n, int64_t n_pad, double* f, const double* mu, const double* Z,
                            const double* g, const double* omzw, const double* y1,
                            const double* y2, hipStream_t s);
