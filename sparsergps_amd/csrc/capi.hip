@@ -1065,10 +1065,10 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
 
 static int k22_factor_launches(sgp_ctx* c, hipStream_t s) {
   const int64_t mp = c->mp;
-  HIPCHK(hipMemcpyAsync(c->K22inv, c->K22, sizeof(double) * mp * mp, hipMemcpyDeviceToDevice, s));
+  // K22inv holds a copy of K22 already (k22_build writes both)
   HIPCHK(dense_spd_inverse(c->K22inv, mp, c->Xt22, c->T22, c->dinv22, c->logd22, c->status, s));
-  HIPCHK(launch_sum_small(c->logd22, mp / SGP_DB, c->sc + SC_LD22, s));
-  HIPCHK(launch_diag(c->K22inv, mp, mp, c->cdiag, s));
+  HIPCHK(launch_sum_and_diag(c->logd22, mp / SGP_DB, c->sc + SC_LD22, c->K22inv, mp, mp,
+                             c->cdiag, s));
   return SGP_OK;
 }
 
@@ -1089,7 +1089,8 @@ static int k22_sync(sgp_ctx* c) {
 // K22 = Kuu + (tau^2 + delta - diag_sub) I on aux (ev_k22m), and its factorisation/inverse
 // after it on aux (ev_k22).  VI runs the two halves in different phases.
 static int k22_build(sgp_ctx* c, double diag_sub) {
-  HIPCHK(launch_build_kmm(c->kp, c->U, c->mp, c->m, c->mp, diag_sub, c->K22, c->aux));
+  HIPCHK(launch_build_kmm(c->kp, c->U, c->mp, c->m, c->mp, diag_sub, c->K22, c->aux,
+                          c->K22inv));   // and the copy the in-place inverse starts from
   HIPCHK(hipEventRecord(c->ev_k22m, c->aux));
   return SGP_OK;
 }

@@ -343,7 +343,8 @@ __global__ void __launch_bounds__(256, WITH_T ? 3 : 4) k_build_knm_mfma(KernPara
 template <int DT>
 __global__ void __launch_bounds__(256) k_build_kmm(KernParams kp, const double* __restrict__ U,
                                                    int64_t ldu, int64_t m, int64_t mp,
-                                                   double diag_sub, double* __restrict__ K22) {
+                                                   double diag_sub, double* __restrict__ K22,
+                                                   double* __restrict__ K22b) {
   const int64_t k = (int64_t)blockIdx.x * 64 + threadIdx.x;
   const int64_t j = (int64_t)blockIdx.y * 4 + threadIdx.y;
   if (j >= mp || k >= mp) return;
@@ -375,6 +376,7 @@ __global__ void __launch_bounds__(256) k_build_kmm(KernParams kp, const double* 
     v = (j == k) ? 1.0 : 0.0;
   }
   K22[j * mp + k] = v;
+  if (K22b) K22b[j * mp + k] = v;   // the copy the in-place inverse starts from
 }
 
 // sum_{j,k<m} G22_jk dK22^p_jk with
@@ -645,13 +647,15 @@ hipError_t launch_build_knm_t(const KernParams& kp, const double* X, int64_t ldx
 }
 
 hipError_t launch_build_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,
-                            int64_t mp, double diag_sub, double* K22, hipStream_t s) {
+                            int64_t mp, double diag_sub, double* K22, hipStream_t s,
+                            double* K22_copy) {
   dim3 grid((unsigned)(mp / 64), (unsigned)((mp + 3) / 4));
   if (kp.d <= 8)
-    hipLaunchKernelGGL(k_build_kmm<8>, grid, dim3(64, 4), 0, s, kp, U, ldu, m, mp, diag_sub, K22);
+    hipLaunchKernelGGL(k_build_kmm<8>, grid, dim3(64, 4), 0, s, kp, U, ldu, m, mp, diag_sub, K22,
+                       K22_copy);
   else
     hipLaunchKernelGGL(k_build_kmm<SGP_MAXD>, grid, dim3(64, 4), 0, s, kp, U, ldu, m, mp,
-                       diag_sub, K22);
+                       diag_sub, K22, K22_copy);
   return hipGetLastError();
 }
 

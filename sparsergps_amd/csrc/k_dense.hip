@@ -439,6 +439,22 @@ __global__ void __launch_bounds__(256) k_colsum(const double* __restrict__ slab,
   if (threadIdx.x == 0) out[k] = s;
 }
 
+// k_sum_vec (block 0) and k_diag (every block) in one launch: the tail of the K22 chain
+__global__ void __launch_bounds__(256) k_sum_and_diag(const double* __restrict__ v, int64_t count,
+                                                      double* __restrict__ sum,
+                                                      const double* __restrict__ A, int64_t mp,
+                                                      int64_t lda, double* __restrict__ out) {
+  __shared__ double sh[4];
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j < mp) out[j] = A[j * lda + j];
+  if (blockIdx.x == 0) {
+    double s = 0.0;
+    for (int64_t e = threadIdx.x; e < count; e += 256) s += v[e];
+    s = block_sum(s, sh);
+    if (threadIdx.x == 0) sum[0] = s;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_diag(const double* __restrict__ A, int64_t mp,
                                               int64_t lda, double* __restrict__ out) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -632,6 +648,13 @@ hipError_t launch_colsum(const double* slab, int64_t nrows, int64_t ncol, double
 hipError_t launch_diag(const double* A, int64_t mp, int64_t lda, double* out, hipStream_t s) {
   hipLaunchKernelGGL(k_diag, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s, A, mp, lda,
                      out);
+  return hipGetLastError();
+}
+
+hipError_t launch_sum_and_diag(const double* v, int64_t count, double* sum, const double* A,
+                               int64_t mp, int64_t lda, double* diag, hipStream_t s) {
+  hipLaunchKernelGGL(k_sum_and_diag, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s, v,
+                     count, sum, A, mp, lda, diag);
   return hipGetLastError();
 }
 

@@ -138,7 +138,8 @@ hipError_t launch_build_knm(const KernParams& kp, const double* X, int64_t ldx, 
 // K22 = Kuu + diag_add on the diagonal, padded with identity (mp x mp, row-major).
 // diag value = ((sig2 + tau2 + delta) - diag_sub) exactly like R's make_cov(...) - tau^2 I.
 hipError_t launch_build_kmm(const KernParams& kp, const double* U, int64_t ldu, int64_t m,
-                            int64_t mp, double diag_sub, double* K22, hipStream_t s);
+                            int64_t mp, double diag_sub, double* K22, hipStream_t s,
+                            double* K22_copy = nullptr);   // also written when non-null
 // sum_{j,k<m} G22_jk * dK22^p_jk for every parameter p != tau, where
 // G22 = a*u u^T + b*(Ainv - Binv) + c*M3.  Writes P partial sums per block into slab.
 // records per block: P (sigma, length scales, tau-coincidence sum of G22)
@@ -246,6 +247,9 @@ hipError_t launch_colsum(const double* slab, int64_t nrows, int64_t ncol, double
 hipError_t launch_diag(const double* A, int64_t mp, int64_t lda, double* out, hipStream_t s);
 // sum of per-block logs -> out
 hipError_t launch_sum_small(const double* v, int64_t count, double* out, hipStream_t s);
+// launch_sum_small and launch_diag in one launch (sum over v[0..count), out diag of A)
+hipError_t launch_sum_and_diag(const double* v, int64_t count, double* sum, const double* A,
+                               int64_t mp, int64_t lda, double* diag, hipStream_t s);
 
 // FITC per-row helpers (k_dense.hip).
 // w_i = 1 / (c0 - q_i) for i < n (0 for padded rows); per-block sums of log(c0 - q_i) -> slab.
