@@ -37,6 +37,13 @@ def _stale():
     return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
 
 
+# Per-source compiler flags.  k_dense.hip: MFMA accumulators in VGPRs -- the Gauss-Jordan
+# pivot's scalar sweeps read and rewrite its accumulator tiles between MFMA blocks, and in AGPRs
+# every sweep paid v_accvgpr_read / write moves (pivot 10.8-11.3 -> 10.2-10.6 us, one m = 1024
+# chain 356-359 -> 342-345 us: profiles/r3/gj_vgpr_form_ab.txt)
+FILE_FLAGS = {"k_dense.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     """Compile every HIP source for gfx950 into lib/libsgp.so (incremental per object)."""
     if not force and not _stale():
@@ -52,7 +59,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         # for the product library
         extra = os.environ.get("SGP_HIPCC_DEFS", "").split()
         cmd = [cc, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wno-unused-result",
-               *extra, "-c", os.path.join(CSRC, src), "-o", obj]
+               *FILE_FLAGS.get(src, []), *extra, "-c", os.path.join(CSRC, src), "-o", obj]
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
     for cmd, p in procs:
         out, _ = p.communicate()
