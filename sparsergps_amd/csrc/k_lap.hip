@@ -311,7 +311,8 @@ enum { LAP_PASS_A = 0, LAP_PASS_B = 1 };
 
 struct LapPassArgs {
   const double* x;                            // x1 (A) / x2 (B), mp
-  double* f;                                  // A: read; B: updated
+  const double* f;                            // mode f at the step's start
+  double* f_out;                              // B: the updated f (may alias f)
   const double *y, *mu, *Z, *zinv;
   const double *g_in, *omzw_in, *y1_in;       // B
   double expo, tol;                           // A
@@ -432,7 +433,7 @@ __global__ void __launch_bounds__(256) k_lap_rowpass(const double* __restrict__ 
           const double a13 = y1i / om;
           const double a2 = sd / om;
           const double fn = fi + (a11 - a12 + a13 + a2);
-          pa.f[i] = fn;
+          pa.f_out[i] = fn;
           const double r = fn - mui;
           vi = iz * r;
           sacc[0] = fma(vi, r, sacc[0]);
@@ -657,7 +658,7 @@ hipError_t launch_lap_nr_a_fused(const double* K, int64_t n, int64_t n_pad, int6
                                  double* v, double* gpsi, double* part, int64_t part_cap,
                                  double* out, double* out_cnt, hipStream_t s) {
   LapPassArgs pa{};
-  pa.x = x1; pa.f = const_cast<double*>(f); pa.y = y; pa.mu = mu; pa.Z = Z; pa.zinv = zinv;
+  pa.x = x1; pa.f = f; pa.y = y; pa.mu = mu; pa.Z = Z; pa.zinv = zinv;
   pa.expo = expo; pa.tol = tol;
   pa.y1 = y1; pa.g = g; pa.omzw = omzw; pa.v = v; pa.gpsi = gpsi;
   return launch_rowpass<LAP_PASS_A>(K, n, n_pad, mp, pa, part, part_cap, out, out_cnt, s);
@@ -670,7 +671,7 @@ hipError_t launch_lap_nr_b_t_fused(const double* K, int64_t n, int64_t n_pad, in
                                    double* part, int64_t part_cap, double* out_t, double* out_rr,
                                    hipStream_t s) {
   LapPassArgs pa{};
-  pa.x = x2; pa.f = f; pa.y = y; pa.mu = mu; pa.Z = Z; pa.zinv = zinv;
+  pa.x = x2; pa.f = f; pa.f_out = f; pa.y = y; pa.mu = mu; pa.Z = Z; pa.zinv = zinv;
   pa.g_in = g; pa.omzw_in = omzw; pa.y1_in = y1;
   double* out_sc = out_rr;
   return launch_rowpass<LAP_PASS_B>(K, n, n_pad, mp, pa, part, part_cap, out_t, out_sc, s);
