@@ -1057,7 +1057,13 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   // K22's inverse (aux) is queued behind the SYRK here rather than in phase 2: it needs only
   // theta and U, so with several ranks it runs while the first all-reduce is in flight (the
   // caller issues it on the main stream between the phases); alone it starts where it did
-  st = k22_factor(c, true);
+  // Small SYRKs (C2: n m^2 = 6.6e9): the chain is queued right behind K22's build, not behind
+  // the SYRK; its workgroups still find no slots until the one-round SYRK ends, and the
+  // cross-stream event wait it saves was ~20 us of C2's critical path (1376 -> 1423 evals/s,
+  // profiles/r3/k22_nowait_ab.txt).  At C3 and the 8-GPU shard the same change was neutral
+  // overall but slowed the phase-2 chains by ~0.03 ms, so they keep the wait.
+  const bool k22_after_syrk = (double)c->n_pad * (double)mpv * (double)mpv > 3e10;
+  st = k22_factor(c, k22_after_syrk);
   if (st) return st;
   c->phase = 1;
   return SGP_OK;
