@@ -1047,6 +1047,9 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   HIPCHK(launch_knot_reduce(c->tslab, t_rows, mpv, 1, c->T1, c->mp_max * c->mp_max,
                             red1 + mmv, false, c->aux_lo));
   HIPCHK(launch_dot(c->r, c->r, c->n_pad, c->slab_aux, red1 + mmv + mpv, c->aux_lo));
+  // ev_lo also covers K22's build (aux): the main stream, which waits for ev_lo here, needs no
+  // second cross-stream wait before forming Bm = K22 + S/z in phase 2 (bm_stage)
+  HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_k22m, 0));
   HIPCHK(hipEventRecord(c->ev_lo, c->aux_lo));
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_lo, 0));
   {
@@ -1126,10 +1129,11 @@ static int bm_factor_launches(sgp_ctx* c, hipStream_t s) {
   return SGP_OK;
 }
 
-static int bm_stage(sgp_ctx* c, const double* S, double s_scale) {
+static int bm_stage(sgp_ctx* c, const double* S, double s_scale, bool k22_ordered = false) {
   const int64_t mp = c->mp, mm = mp * mp;
   Scope t(c, "dense_bm");
-  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22m, 0));   // Bm needs K22, not its inverse
+  if (!k22_ordered)   // Bm needs K22, not its inverse (VI: ordered through phase 1's ev_lo)
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22m, 0));
   HIPCHK(dense_axpby(1.0, c->K22, s_scale, S, c->Binv, mm, c->stream));
   return bm_factor_launches(c, c->stream);
 }
@@ -1168,7 +1172,7 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
       HIPCHK(hipEventRecord(c->ev_m3, c->aux_lo));
     }
   }
-  int st = bm_stage(c, S, 1.0 / z);
+  int st = bm_stage(c, S, 1.0 / z, true);   // K22's build ordered by phase 1's ev_lo
   if (st) return st;
   {
     Scope tm(c, "mm_vectors");
@@ -2271,7 +2275,7 @@ int sgp_vi_candidates(sgp_ctx* c, int kernel, const double* theta, const double*
   const double* S = c->red1;
   const double* t = c->red1 + mm;
   // K22's inverse was queued on aux by sgp_vi_phase1; it runs beside Bm's
-  st = bm_stage(c, S, 1.0 / z);
+  st = bm_stage(c, S, 1.0 / z, true);   // K22's build ordered by phase 1's ev_lo
   if (st) return st;
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
   {
