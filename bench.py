@@ -29,12 +29,12 @@ FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix peak (AMD spec; SURVEY
 HBM_PEAK_GBS = 8000.0
 
 
-def make_problem(config, n=None, m=None):
+def make_problem(config, n=None, m=None, d=None):
     """Synthetic inputs of SURVEY.md 8(d) (numpy PCG64 streams); no reference files read."""
     from sparsergps_amd.workloads import make_gaussian_problem, make_poisson_problem
     if config == "C5":
         return make_poisson_problem(n=n, m=m)
-    return make_gaussian_problem(config, n=n, m=m)
+    return make_gaussian_problem(config, n=n, m=m, d=d)
 
 
 def cpu_info():
@@ -218,6 +218,8 @@ def main():
     # abbreviation of its own options)
     ap.add_argument("--n", "--rows", dest="n", type=int, default=None)
     ap.add_argument("--m", type=int, default=None)
+    ap.add_argument("--d", type=int, default=None,
+                    help="C3's input dimension (default 8): times the d > 8 kernels")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-full", default=None, metavar="OUT_JSON",
                     help="run only SURVEY 8(d)'s full CPU plan (several minutes, no GPU) and "
@@ -235,6 +237,8 @@ def main():
         args.config = "C5" if args.mode == "laplace" else "C3"
     if (args.mode == "laplace") != (args.config == "C5"):
         ap.error("--mode laplace goes with --config C5 (Poisson data); vi/fitc with C2/C3")
+    if args.d is not None and args.config != "C3":
+        ap.error("--d applies to C3 only")
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -262,7 +266,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
     dev = torch.device("cuda", dev_index)
 
-    P = make_problem(args.config, n=args.n, m=args.m)
+    P = make_problem(args.config, n=args.n, m=args.m, d=args.d)
     n, m, d = P["X"].shape[0], P["U"].shape[0], P["X"].shape[1]
     cov_fun = P["cov_fun"]
     names = S.param_names(cov_fun, d)
@@ -361,6 +365,8 @@ def main():
         workload = {"vi": "Titsias VI ELBO + gradient", "fitc": "FITC log-likelihood + gradient",
                     "laplace": "Poisson Laplace: NR (warm start, tol_nr=%g) + obj_fun_pois + "
                                "dlogq_dcov_par" % args.tol_nr}[args.mode]
+        if args.mode == "vi" and (n, m, d) != (1_000_000, 1024, 8):
+            metric["vi"] = f"sparse-GP objective+gradient evals/sec at n={n}, m={m}, d={d}"
         out = {
             "metric": metric[args.mode],
             "value": args.steps / elapsed,
@@ -382,7 +388,7 @@ def main():
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
                          "traffic": traffic if args.mode == "vi" else None,
-                         "kernel": con_key + " (k_contract<8>)",
+                         "kernel": con_key + (" (k_contract<8>)" if d <= 8 else " (k_contract<32>)"),
                          "flops_per_launch": flops},
             "kernel_rooflines": kernel_rooflines(args.mode, phase_avg, n_loc, m),
             "phases_ms": {k: round(v, 4) for k, v in phase_avg.items()},

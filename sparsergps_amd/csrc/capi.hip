@@ -193,7 +193,7 @@ struct sgp_ctx {
   double *slab_syrk = nullptr, *slab_con = nullptr, *slab_small = nullptr, *sc = nullptr;
   double* tslab = nullptr;                // builder t = K^T r partials (VI), n_pad/64 x mp
   // stored products of the FITC / Laplace row-quadratic passes (n_pad x mp each, allocated on
-  // first use; d <= 8): tq = K K22^-1, tp = K Bm^-1 (FITC) or K C (Laplace).  The gradient
+  // first use): tq = K K22^-1, tp = K Bm^-1 (FITC) or K C (Laplace).  The gradient
   // contraction passes read them instead of recomputing the same 2 n m^2 GEMMs.
   double *tq = nullptr, *tp = nullptr;
   int tstore_state = 0;                   // 0 untried, 1 allocated, -1 unavailable
@@ -368,10 +368,9 @@ int dalloc(T** p, int64_t count) {
   return SGP_OK;
 }
 
-// Stored-product buffers for the FITC / Laplace passes; false (GEMM path) when d > 8 or HBM is
-// short -- the evaluation is the same either way.
+// Stored-product buffers for the FITC / Laplace passes; false (GEMM path) when HBM is short --
+// the evaluation is the same either way.
 bool tstore_ready(sgp_ctx* c) {
-  if (c->kp.d > 8) return false;
   if (c->tstore_state == 0) {
     const int64_t cnt = c->n_pad * c->mp_max;
     if (hipMalloc(reinterpret_cast<void**>(&c->tq), sizeof(double) * cnt) == hipSuccess &&

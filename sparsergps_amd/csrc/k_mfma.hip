@@ -1494,6 +1494,28 @@ static void launch_con_grad(bool v2, const KernParams& kp, const double* K, cons
                        (double*)nullptr);
 }
 
+// the gradient pass over a stored product T = K M (FROM_T: no k-loop)
+template <int DT>
+static void launch_con_from_t(bool v2, bool kn, const KernParams& kp, const double* K,
+                              const double* M, const double* X, int64_t ldx, int64_t n,
+                              int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
+                              const ConArgs& ca, double* slab, int nrec, int64_t nwg,
+                              hipStream_t s) {
+  const dim3 g((unsigned)nwg), b(256);
+  if (v2 && kn)
+    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, true, true, true>), g, b, 0, s, kp, K, M, X, ldx,
+                       n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
+  else if (v2)
+    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, true, false, true>), g, b, 0, s, kp, K, M, X, ldx,
+                       n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
+  else if (kn)
+    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, false, true, true>), g, b, 0, s, kp, K, M, X, ldx,
+                       n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
+  else
+    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, false, false, true>), g, b, 0, s, kp, K, M, X,
+                       ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
+}
+
 hipError_t launch_contract_args(const KernParams& kp, const double* K, const double* M,
                                 const double* X, int64_t ldx, int64_t n, int64_t n_pad,
                                 const double* U, int64_t ldu, int64_t m, int64_t mp,
@@ -1503,25 +1525,13 @@ hipError_t launch_contract_args(const KernParams& kp, const double* K, const dou
   const int nrec = kp.L + 5;
   *nrec_out = nrec;
   *nwg_out = nwg;
-  if (ca.tin != nullptr) {   // stored product: no k-loop (d <= 8, alpha from alpha_in)
-    if (kp.d > 8 || (ca.uvec != nullptr && ca.alpha_in == nullptr)) return hipErrorInvalidValue;
+  if (ca.tin != nullptr) {   // stored product: no k-loop (alpha from alpha_in)
+    if (ca.uvec != nullptr && ca.alpha_in == nullptr) return hipErrorInvalidValue;
     const bool v2 = ca.beta_in != nullptr, kn = ca.knot_slab != nullptr;
-    if (v2 && kn)
-      hipLaunchKernelGGL((k_contract<8, EPI_GRAD, true, true, true>), dim3((unsigned)nwg),
-                         dim3(256), 0, s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab,
-                         nrec, (double*)nullptr);
-    else if (v2)
-      hipLaunchKernelGGL((k_contract<8, EPI_GRAD, true, false, true>), dim3((unsigned)nwg),
-                         dim3(256), 0, s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab,
-                         nrec, (double*)nullptr);
-    else if (kn)
-      hipLaunchKernelGGL((k_contract<8, EPI_GRAD, false, true, true>), dim3((unsigned)nwg),
-                         dim3(256), 0, s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab,
-                         nrec, (double*)nullptr);
-    else
-      hipLaunchKernelGGL((k_contract<8, EPI_GRAD, false, false, true>), dim3((unsigned)nwg),
-                         dim3(256), 0, s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab,
-                         nrec, (double*)nullptr);
+    if (kp.d <= 8) launch_con_from_t<8>(v2, kn, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab,
+                                        nrec, nwg, s);
+    else launch_con_from_t<SGP_MAXD>(v2, kn, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab,
+                                     nrec, nwg, s);
     return hipGetLastError();
   }
   if (ca.knot_slab != nullptr) {

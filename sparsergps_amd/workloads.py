@@ -14,11 +14,12 @@ def _rng(seed):
     return np.random.Generator(np.random.PCG64(seed))
 
 
-def make_gaussian_problem(config, n=None, m=None):
+def make_gaussian_problem(config, n=None, m=None, d=None):
     """C2 / C3 (and C4 = C3 row-sharded) synthetic Gaussian regression inputs.
 
     C2: d=3, sqexp, theta=(sigma=1, l=1, tau=0.5); seeds X=2, U=3, y=4.
     C3: d=8, ARD,   theta=(sigma=1, l1..l8=3, tau=0.5); seeds X=5, U=6, y=7.
+    `d` overrides C3's input dimension (timing of the d > 8 kernels only; not a BASELINE config).
     y = sum_c sin(x_c) [/sqrt(d) for C3] + N(0, 0.5^2); mu = mean(y) (quirk Q14).
     """
     if config == "C2":
@@ -33,7 +34,7 @@ def make_gaussian_problem(config, n=None, m=None):
     elif config in ("C3", "C4"):
         n = n or 1_000_000
         m = m or 1024
-        d, sx, su, sy = 8, 5, 6, 7
+        d, sx, su, sy = d or 8, 5, 6, 7
         X = _rng(sx).uniform(0.0, 10.0, size=(n, d))
         U = _rng(su).uniform(0.0, 10.0, size=(m, d))
         y = np.sin(X).sum(axis=1) / math.sqrt(d) + _rng(sy).normal(0.0, 0.5, size=n)

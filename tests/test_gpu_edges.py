@@ -196,7 +196,7 @@ def test_vi_high_dim(sgp, n, m, d, cov_fun):
     _close(obj, grad, o, g, cp)
 
 
-@pytest.mark.parametrize("n,m,d,cov_fun", HD_SHAPES[:3])
+@pytest.mark.parametrize("n,m,d,cov_fun", HD_SHAPES)
 def test_fitc_high_dim(sgp, n, m, d, cov_fun):
     P = _gauss_hd(n, m, d, cov_fun, seed=500 + d)
     cp = P["cov_par"]
