@@ -205,29 +205,27 @@ __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* 
   }
 }
 
-// K12 row-major (n_pad x mp) on the matrix cores, d <= 8, sqexp / ARD.
+// K12 row-major (n_pad x mp) on the matrix cores, d <= 4 NC (NC = 2, 4, 8), sqexp / ARD.
 // The exponent log(sig2) - 1/2 |x~ - u~|^2 (x~ = (x - ctr) / l per coordinate, ctr = the
-// knots' mean) is one GEMM with inner dimension 12 over augmented coordinates
-//   A_i = [x~_i (8), -|x~_i|^2 / 2, 1, 1, 0]    B_j = [u~_j (8), 1, -|u~_j|^2 / 2, log sig2, 0]
-// i.e. three v_mfma_f64_16x16x4_f64 per 16 x 16 tile, so the VALU only evaluates exp (the
-// per-pair coordinate differences of k_build_knm cost ~40 % of its VALU work, which then
-// matched the store time); padding rows / knots carry -1e300 in the |.|^2 slot, so the clamped
-// exponent gives exactly 0 there without a select.  The expansion's rounding is ~1e-16 (|x~|^2 + |u~|^2) absolute in the
+// knots' mean) is one GEMM with inner dimension 4 NC + 4 over augmented coordinates
+//   A_i = [x~_i (4 NC), -|x~_i|^2 / 2, 1, 1, 0]    B_j = [u~_j (4 NC), 1, -|u~_j|^2 / 2, log sig2, 0]
+// i.e. NC + 1 v_mfma_f64_16x16x4_f64 per 16 x 16 tile (lane l >> 4 feeds coordinates
+// 4 k + (l >> 4) of chunk k), so the VALU only evaluates exp (the per-pair coordinate
+// differences of k_build_knm cost ~40 % of its VALU work, which then matched the store time);
+// padding rows / knots carry -1e300 in the |.|^2 slot, so the clamped exponent gives exactly 0
+// there without a select.  The expansion's rounding is ~1e-16 (|x~|^2 + |u~|^2) absolute in the
 // exponent -- ~1e-14 relative in K at the configs' scales, centring keeps it there for data far
 // from the origin.  Block: 4 waves x 16 rows of a 64-row block, 128 knots; tile 2p (2p+1) holds
 // knots j0 + 32p + 2 l' (+1) in MFMA column l' = lane & 15, so each lane stores its two adjacent
 // knots as one 16-byte store (lanes 0-15: 256 contiguous bytes of one row).  Persistent over
 // row blocks rb0 + blockIdx.y + k gridDim.y; with t, the workgroup's t = K^T r partial over all
 // its row blocks goes to slot slot0 + blockIdx.y of tslab (fixed order: deterministic).
-template <bool WITH_T>
-__global__ void __launch_bounds__(256, WITH_T ? 3 : 4) k_build_knm_mfma(KernParams kp, const double* __restrict__ X,
-                                                        int64_t ldx, int64_t n,
-                                                        const double* __restrict__ U, int64_t ldu,
-                                                        int64_t m, int64_t mp,
-                                                        double* __restrict__ K,
-                                                        const double* __restrict__ rvec,
-                                                        double* __restrict__ tslab, int64_t slot0,
-                                                        int64_t rb0, int64_t rb1) {
+template <bool WITH_T, int NC>
+__global__ void __launch_bounds__(256, NC > 4 ? (WITH_T ? 2 : 3) : (WITH_T ? 3 : 4))
+k_build_knm_mfma(KernParams kp, const double* __restrict__ X, int64_t ldx, int64_t n,
+                 const double* __restrict__ U, int64_t ldu, int64_t m, int64_t mp,
+                 double* __restrict__ K, const double* __restrict__ rvec,
+                 double* __restrict__ tslab, int64_t slot0, int64_t rb0, int64_t rb1) {
   __shared__ double tsh[WITH_T ? 4 : 1][128];
   __shared__ double etab[32];
   if (threadIdx.x < 32) etab[threadIdx.x] = kp.et[threadIdx.x];
@@ -235,28 +233,47 @@ __global__ void __launch_bounds__(256, WITH_T ? 3 : 4) k_build_knm_mfma(KernPara
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ln = lane & 15, lq = lane >> 4;
   const int d = kp.d;
-  const int c0 = lq, c1 = 4 + lq;               // the two coordinates this lane feeds
-  const bool f0 = c0 < d, f1 = c1 < d;
-  const double ct0 = f0 ? kp.ctr[c0] : 0.0, ct1 = f1 ? kp.ctr[c1] : 0.0;
-  const double rl0 = f0 ? kp.rl[c0] : 0.0, rl1 = f1 ? kp.rl[c1] : 0.0;
+  bool fc[NC];                  // this lane's coordinate of chunk k: 4 k + lq
+  double ct[NC], rl[NC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    fc[k] = 4 * k + lq < d;
+    ct[k] = fc[k] ? kp.ctr[4 * k + lq] : 0.0;
+    rl[k] = fc[k] ? kp.rl[4 * k + lq] : 0.0;
+  }
   const int64_t j0 = (int64_t)blockIdx.x * 128;
-  double b0[8], b1[8], b2[8];
-  bool jv[8];
+  // knot fragments: in registers for d <= 8; for wider d (4 NC + 4 per lane and tile) they
+  // would not fit beside the row state, so they sit in LDS as [chunk][tile][lane] (each read
+  // one conflict-free ds_read_b64), written by wave w for tiles 2w, 2w + 1
+  constexpr bool BL = NC > 2;
+  __shared__ double sbf[BL ? (NC + 1) * 8 * 64 : 1];
+  double bc[BL ? 1 : NC][8], b2[BL ? 1 : 8];
 #pragma unroll
   for (int tt = 0; tt < 8; ++tt) {
+    if (BL && (tt >> 1) != w) continue;
     const int64_t j = j0 + 32 * (tt >> 1) + 2 * ln + (tt & 1);
-    jv[tt] = j < m;
-    const double u0 = (jv[tt] && f0) ? (U[j + c0 * ldu] - ct0) * rl0 : 0.0;
-    const double u1 = (jv[tt] && f1) ? (U[j + c1 * ldu] - ct1) * rl1 : 0.0;
-    double u2 = fma(u0, u0, u1 * u1);
+    const bool jv = j < m;
+    double u2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const double u = (jv && fc[k]) ? (U[j + (4 * k + lq) * ldu] - ct[k]) * rl[k] : 0.0;
+      if constexpr (BL) sbf[(k * 8 + tt) * 64 + lane] = u;
+      else bc[k][tt] = u;
+      u2 = fma(u, u, u2);
+    }
     u2 += __shfl_xor(u2, 16, 64);
     u2 += __shfl_xor(u2, 32, 64);
-    b0[tt] = u0;
-    b1[tt] = u1;
     // padding knots: an exponent of -1e300 (clamped to -746 below) gives K = 0 with no
     // per-pair select
-    b2[tt] = lq == 0 ? 1.0 : (lq == 1 ? (jv[tt] ? -0.5 * u2 : -1e300) : (lq == 2 ? kp.lsig2 : 0.0));
+    const double bv = lq == 0 ? 1.0 : (lq == 1 ? (jv ? -0.5 * u2 : -1e300) : (lq == 2 ? kp.lsig2 : 0.0));
+    if constexpr (BL) sbf[(NC * 8 + tt) * 64 + lane] = bv;
+    else b2[tt] = bv;
   }
+  if constexpr (BL) __syncthreads();
+  auto bfr = [&](int k, int tt) -> double {
+    if constexpr (BL) return sbf[(k * 8 + tt) * 64 + lane];
+    else return k < NC ? bc[k][tt] : b2[tt];
+  };
   const double ehi = kp.lsig2;
   double tacc[8];
 #pragma unroll
@@ -265,27 +282,32 @@ __global__ void __launch_bounds__(256, WITH_T ? 3 : 4) k_build_knm_mfma(KernPara
   // The next row block's coordinates and r are loaded before this block's stores: vmcnt
   // counts loads and stores in issue order, so loads issued after the stores would make every
   // block wait for the previous block's 16 stores to drain.
-  double xn0 = 0.0, xn1 = 0.0, rn[4] = {0.0, 0.0, 0.0, 0.0};
+  double xn[NC], rn[4] = {0.0, 0.0, 0.0, 0.0};
   auto load_rows = [&](int64_t rb) {
     const int64_t ib = rb * 64 + 16 * w, ia = ib + ln;   // X is zero-padded to n_pad rows
-    xn0 = f0 ? X[ia + c0 * ldx] : 0.0;
-    xn1 = f1 ? X[ia + c1 * ldx] : 0.0;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) xn[k] = fc[k] ? X[ia + (4 * k + lq) * ldx] : 0.0;
     if (WITH_T) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) rn[r] = rvec[ib + lq + 4 * r];
     }
   };
+#pragma unroll
+  for (int k = 0; k < NC; ++k) xn[k] = 0.0;
   if (rb0 + (int64_t)blockIdx.y < rb1) load_rows(rb0 + blockIdx.y);
   for (int64_t rb = rb0 + blockIdx.y; rb < rb1; rb += gridDim.y) {
     const int64_t ib = rb * 64 + 16 * w;
     const int64_t ia = ib + ln;                 // this lane's A row
-    const double a0 = f0 ? (xn0 - ct0) * rl0 : 0.0;
-    const double a1 = f1 ? (xn1 - ct1) * rl1 : 0.0;
+    double ac[NC], x2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      ac[k] = fc[k] ? (xn[k] - ct[k]) * rl[k] : 0.0;
+      x2 = fma(ac[k], ac[k], x2);
+    }
     double rr[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) rr[r] = rn[r];
     if (rb + gridDim.y < rb1) load_rows(rb + gridDim.y);
-    double x2 = fma(a0, a0, a1 * a1);
     x2 += __shfl_xor(x2, 16, 64);
     x2 += __shfl_xor(x2, 32, 64);
     // exponent = x~.u~ - |x~|^2 / 2 - |u~|^2 / 2 + log(sig2); padding rows as padding knots
@@ -293,12 +315,15 @@ __global__ void __launch_bounds__(256, WITH_T ? 3 : 4) k_build_knm_mfma(KernPara
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const d4 z = {0.0, 0.0, 0.0, 0.0};
-      d4 e0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0[2 * p], z, 0, 0, 0);
-      d4 e1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0[2 * p + 1], z, 0, 0, 0);
-      e0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1[2 * p], e0, 0, 0, 0);
-      e1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1[2 * p + 1], e1, 0, 0, 0);
-      e0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2[2 * p], e0, 0, 0, 0);
-      e1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2[2 * p + 1], e1, 0, 0, 0);
+      d4 e0 = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[0], bfr(0, 2 * p), z, 0, 0, 0);
+      d4 e1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[0], bfr(0, 2 * p + 1), z, 0, 0, 0);
+#pragma unroll
+      for (int k = 1; k < NC; ++k) {
+        e0 = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[k], bfr(k, 2 * p), e0, 0, 0, 0);
+        e1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[k], bfr(k, 2 * p + 1), e1, 0, 0, 0);
+      }
+      e0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, bfr(NC, 2 * p), e0, 0, 0, 0);
+      e1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, bfr(NC, 2 * p + 1), e1, 0, 0, 0);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         // K = exp(exponent) <= sig2: clamp the rounding above log(sig2), and below at -746
@@ -545,23 +570,27 @@ hipError_t launch_fill_dcov(const KernParams& kp, const double* x, int64_t n, in
 
 // One builder launch over row blocks [rb0, rb1) with at most wpc workgroups per CU.  t
 // partials (rvec != nullptr) go to tslab rows [slot0, slot0 + *slots): one per workgroup row
-// for the matrix-core builder, one per row block for the VALU builder (d > 8).
+// for the matrix-core builder, one per row block for the VALU builder (exp kernel, wide spans).
 static hipError_t build_knm_range(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
                                   const double* U, int64_t ldu, int64_t m, int64_t mp, double* K,
                                   const double* r, double* tslab, int64_t slot0, int64_t* slots,
                                   int64_t rb0, int64_t rb1, int wpc, hipStream_t s) {
-  static int cus = 0, occ_t = 0, occ_n = 0;
+  static int cus = 0, occ[2][3];   // [with t][NC = 2, 4, 8]
   if (cus == 0) {
     int dev = 0;
     hipDeviceProp_t prop;
     cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
               ? prop.multiProcessorCount : 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_t, k_build_knm_mfma<true>, 256, 0) !=
-            hipSuccess || occ_t < 1)
-      occ_t = 2;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_n, k_build_knm_mfma<false>, 256, 0) !=
-            hipSuccess || occ_n < 1)
-      occ_n = 2;
+    const void* fns[2][3] = {
+        {(const void*)k_build_knm_mfma<false, 2>, (const void*)k_build_knm_mfma<false, 4>,
+         (const void*)k_build_knm_mfma<false, 8>},
+        {(const void*)k_build_knm_mfma<true, 2>, (const void*)k_build_knm_mfma<true, 4>,
+         (const void*)k_build_knm_mfma<true, 8>}};
+    for (int t = 0; t < 2; ++t)
+      for (int q = 0; q < 3; ++q)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[t][q], fns[t][q], 256, 0) !=
+                hipSuccess || occ[t][q] < 1)
+          occ[t][q] = 2;
   }
   if (slots) *slots = 0;
   if (rb1 <= rb0) return hipSuccess;
@@ -570,17 +599,25 @@ static hipError_t build_knm_range(const KernParams& kp, const double* X, int64_t
   const bool ard = kp.kernel == 1;
   if (knm_mfma_ok(kp)) {
     // persistent: one residency round of workgroups, each walking its share of row blocks
-    const int occ = r ? occ_t : occ_n;
-    const int per_cu = wpc < occ ? wpc : occ;
+    const int q = kp.d <= 8 ? 0 : (kp.d <= 16 ? 1 : 2);
+    const int oc = occ[r ? 1 : 0][q];
+    const int per_cu = wpc < oc ? wpc : oc;
     int64_t gy = ((int64_t)cus * per_cu) / (ncb > 0 ? ncb : 1);
     gy = gy < 1 ? 1 : (gy > rb1 - rb0 ? rb1 - rb0 : gy);
     dim3 grid((unsigned)ncb, (unsigned)gy);
-    if (r)
-      hipLaunchKernelGGL(k_build_knm_mfma<true>, grid, dim3(256), 0, s, kp, X, ldx, n, U, ldu, m,
-                         mp, K, r, tslab, slot0, rb0, rb1);
-    else
-      hipLaunchKernelGGL(k_build_knm_mfma<false>, grid, dim3(256), 0, s, kp, X, ldx, n, U, ldu, m,
-                         mp, K, r, tslab, slot0, rb0, rb1);
+#define SGP_BUILD_MFMA(T, NCV)                                                                 \
+  hipLaunchKernelGGL((k_build_knm_mfma<T, NCV>), grid, dim3(256), 0, s, kp, X, ldx, n, U, ldu, m, \
+                     mp, K, r, tslab, slot0, rb0, rb1)
+    if (r) {
+      if (q == 0) SGP_BUILD_MFMA(true, 2);
+      else if (q == 1) SGP_BUILD_MFMA(true, 4);
+      else SGP_BUILD_MFMA(true, 8);
+    } else {
+      if (q == 0) SGP_BUILD_MFMA(false, 2);
+      else if (q == 1) SGP_BUILD_MFMA(false, 4);
+      else SGP_BUILD_MFMA(false, 8);
+    }
+#undef SGP_BUILD_MFMA
     if (slots) *slots = gy;
     return hipGetLastError();
   }

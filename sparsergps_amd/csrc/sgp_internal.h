@@ -75,7 +75,7 @@ void set_exp_consts(KernParams* kp);
 // direct-difference form (1e4 * 2^-52 * a few); the C2 / C3 / C5 workloads sit below 100.
 constexpr double SGP_MFMA_SPAN2_MAX = 1.0e4;
 inline bool knm_mfma_ok(const KernParams& kp) {
-  return kp.d <= 8 && kp.kernel != 2 && kp.span2 <= SGP_MFMA_SPAN2_MAX;
+  return kp.d <= 32 && kp.kernel != 2 && kp.span2 <= SGP_MFMA_SPAN2_MAX;
 }
 
 // exp(x) for x already clamped to [-746, log(DBL_MAX)] by a 32-entry table: x = (32 e + j) ln2/32
