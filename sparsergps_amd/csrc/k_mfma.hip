@@ -765,7 +765,11 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
       // Eight half-height stages (16 rows: the 8 rows a lane's q pair needs, of each 64-row
       // half), double-buffered in the LDS one 32-row stage took, each issued one half-stage
       // ahead of its use (round 3; four single-buffered 32-row stages before: the same time at
-      // C3, 31.3-31.4 ms, and 1-3 % more at C2, profiles/r3/kdb_ab.txt)
+      // C3, 31.3-31.4 ms, and 1-3 % more at C2, profiles/r3/kdb_ab.txt).  The compiler waits
+      // vmcnt(0) after each issue (it tracks the DMA as an LDS write it cannot tell apart from
+      // the stage being read); a real two-ahead prefetch (inline-asm DMA, three buffers) was no
+      // faster -- the stage phase is bound by the issue slots the co-resident workgroup's k-loop
+      // leaves, not by the load latency (profiles/r3/con_epi_dma_ab.txt)
 #define CON_KHALF(s_)                                                                    \
       _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_) {                                 \
         const int rho_ = wv * 4 + q_;                                                    \
