@@ -1021,7 +1021,7 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   }
   // ev_knots after the builder: aux may build K22 from here on (first needed by phase 2), and
   // aux_lo may reduce the builder's t partials.  The SYRK goes right behind the builder (it
-  // needs only K12); the resets and the small t / rr reductions run on aux_lo beside it
+  // needs only K12); red1's reset and the small t / rr reductions run on aux_lo beside it
   // instead of between the two on the main stream, where at small n (C2) the GPU idled while
   // the host issued them one by one
   st = k22_sync(c);
@@ -1034,14 +1034,16 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   // K22 itself only (aux); its inverse runs in phase 2 beside the Bm inverse -- nothing in
   // phase 1 needs it, and the latency-bound chain no longer gates the one-round SYRK or shares
   // the CUs with the builder
+  // status / scalar resets on aux ahead of K22's build: the K22 chain (aux; at small n queued
+  // right behind the build) is their first writer, phase 2 (main, behind ev_lo, which covers
+  // ev_k22m) the next.  (On aux_lo they raced the small-n chain.)
+  HIPCHK(hipMemsetAsync(c->status, 0, sizeof(int) * 4, c->aux));
+  HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->aux));
   st = k22_build(c, kp.tau2);
   if (st) return st;
-  // aux_lo, after the builder: status / scalar resets (first written by the K22 chain -- queued
-  // after the SYRK reduction, aux waiting on the main stream -- and by phase 2), red1's zeroing
-  // (before the SYRK reduction below writes S into it: the main stream waits for ev_lo), t and rr
+  // aux_lo, after the builder: red1's zeroing (before the SYRK reduction below writes S into
+  // it: the main stream waits for ev_lo), t and rr
   HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_knots, 0));
-  HIPCHK(hipMemsetAsync(c->status, 0, sizeof(int) * 4, c->aux_lo));
-  HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->aux_lo));
   HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_vi_red1_count(m), c->aux_lo));
   HIPCHK(launch_knot_reduce(c->tslab, t_rows, mpv, 1, c->T1, c->mp_max * c->mp_max,
                             red1 + mmv, false, c->aux_lo));
