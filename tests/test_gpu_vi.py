@@ -164,6 +164,26 @@ def test_not_positive_definite(sgp):
         sgp.vi_eval(P["cov_par"], "sqexp", U, P["X"], P["y"], P["mu"], delta=-1e-3)
 
 
+def test_status_reset_after_not_positive_definite(sgp):
+    """A non-PD evaluation, then valid ones on the same context.  At small n the K22 chain is
+    queued right behind K22's build on the aux stream; the status / scalar resets of each
+    evaluation go on that stream ahead of the build (sgp_vi_phase1), so a failed evaluation's
+    status and K22 log-determinant never reach the next one."""
+    from oracle import adjoint_ref as A
+    P = _problem("C2", 300, 12)
+    th = np.array(list(P["cov_par"].values()))
+    U_bad = np.vstack([P["U"], P["U"][:1]])       # duplicated knot, negative nugget -> not PD
+    o, g = A.eval_vi("sqexp", th, P["X"], P["y"], P["mu"], P["U"], P["delta"])
+    with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=16) as ctx:
+        for _ in range(2):
+            with pytest.raises(sgp.NotPositiveDefinite):
+                ctx.eval_vi(th, "sqexp", U_bad, -1e-3)
+            for _ in range(3):
+                obj, grad = ctx.eval_vi(th, "sqexp", P["U"], P["delta"])
+                assert abs(obj - o) / abs(o) < 1e-9
+                assert _rel(grad, g) < 1e-7
+
+
 def test_r_det_quirk(sgp):
     """With SGP_FLAG_R_DET the log(det(K22)) term follows R's det() (finite here -> equal)."""
     P = _problem("C2", 300, 20)
