@@ -158,8 +158,9 @@ int sgp_lap_set_f(sgp_ctx* ctx, const double* f /* n host values, or NULL */, do
 int sgp_lap_get_f(sgp_ctx* ctx, double* f /* n host values */);
 /* grad psi of the last Newton-Raphson step (n host values): the `gradient` element
  * newtrap_sparseGP returns (R/newtrap_sparseGP.R:183-184) -- evaluated at the mode estimate
- * that step started from, as the reference's loop leaves it.  SGP_EINVAL when no NR step has
- * run since sgp_lap_set_f (or since OAT candidate scoring). */
+ * that step started from, as the reference's loop leaves it.  SGP_EINVAL unless an NR step
+ * has run since the last NR run began (sgp_lap_begin; a maxit = 0 evaluation takes no step),
+ * and after sgp_lap_set_f or OAT candidate scoring. */
 int sgp_lap_get_grad_psi(sgp_ctx* ctx, double* grad_psi);
 /* objective_function_values of the last NR run (first min(count, max_n) copied; *count = all) */
 int sgp_lap_objective_values(sgp_ctx* ctx, double* out, int max_n, int* count);

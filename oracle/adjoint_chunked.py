@@ -154,3 +154,200 @@ def eval_vi(kernel, theta, X, y, mu, U, delta=1e-6, chunk=8192, n_global=None):
     grad[1:L + 1] = e_l + np.asarray(g22[1:])
     grad[L + 1] = 2 * tau2 * (c_sum - (c_cnt - delta * c_dg) / tau2) + 2 * tau2 * trW - 2 * T
     return obj, grad
+
+
+# ------------------------------------------------------------------------------ Laplace model
+def eval_laplace(kernel, theta, X, y, mu, U, f0, expo=1.0, delta=1e-6, tol=1e-5, maxit=1000,
+                 chunk=8192):
+    """Poisson sparse Laplace (newtrap_sparseGP to the mode from f0, then dlogq_dcov_par there)
+    with O(chunk * m) memory: the algebra and the NR state machine of
+    ``adjoint_ref.NumpyLaplaceRank`` (which mirrors sgp_lap_begin / sgp_lap_step, DESIGN.md
+    sec. 3.3), K12 rebuilt per row chunk in every pass.  References: R/newtrap_sparseGP.R:6-186
+    (+ newtrap_sparseGP_update 234-325: the NR step and its stop rule), obj_fun_pois
+    R/laplace_approx_obj_funs.R:108-174, dlogq_dcov_par R/laplace_approx_gradient.R:25-553
+    (comp3's 2 dS12 GG form).
+
+    Passes over the rows: one at the start (Z = diag FITC, S_Z, and the first objective's
+    partials), two per NR iteration (part a: K x1, K^T(gpsi / (1 - ZW)) and the stop-rule
+    count; part b: the f update fused with the next objective's S_B, t_Z), two for the
+    gradient.  Returns (last objective, d/d log theta in [sigma, l.., tau] order, the mode f,
+    the objective values of the NR run)."""
+    X = np.asarray(X, dtype=np.float64)
+    U = np.asarray(U, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    mu = np.broadcast_to(np.asarray(mu, dtype=np.float64), y.shape)
+    f = np.array(f0, dtype=np.float64).reshape(-1)
+    n, d = X.shape
+    m = U.shape[0]
+    a_ = float(expo)
+    L, sigma, tau, ls = _params(kernel, theta, d)
+    sig2, tau2 = sigma * sigma, tau * tau
+    center = U.mean(axis=0)
+    Us = _scaled(kernel, U, center, ls)
+    u2 = np.einsum("ij,ij->i", Us, Us)
+    buf = np.empty((min(chunk, n), m))
+    Kuu, dU = _kmat(kernel, U, U, sigma, ls)
+    K22 = Kuu.copy()
+    K22[np.diag_indices(m)] = np.diag(Kuu) + tau2 + delta              # quirk Q1 (Laplace)
+    K22inv = np.linalg.inv(K22)
+    ld22 = np.linalg.slogdet(K22)[1]
+    from scipy.special import gammaln
+    lgy = gammaln(y + 1.0)
+    log_a = math.log(a_)
+
+    def chunks():
+        for s0 in range(0, n, chunk):
+            s1 = min(n, s0 + chunk)
+            Xs = _scaled(kernel, X[s0:s1], center, ls)
+            x2 = np.einsum("ij,ij->i", Xs, Xs)
+            yield s0, s1, Xs, x2, _kblock(Xs, x2, Us, u2, sig2, out=buf[:s1 - s0])
+
+    Z = np.empty(n)
+
+    def obj_partials(K, sl):
+        """S_B, t_Z and the scalar sums of obj_fun_pois at the current f (rows sl)."""
+        fz, Zc = f[sl], Z[sl]
+        W = -a_ * np.exp(fz)
+        B = W / (Zc * W - 1.0)
+        r = fz - mu[sl]
+        rz = r / Zc
+        return (K.T @ (B[:, None] * K), K.T @ rz,
+                np.array([r @ rz, float(np.sum(y[sl] * log_a - lgy[sl] - a_ * np.exp(fz) + y[sl] * fz)),
+                          float(np.sum(np.log(1.0 - W * Zc)))]))
+
+    # ---- begin: Z, S_Z and the first objective's partials
+    SZ = np.zeros((m, m))
+    SB = np.zeros((m, m))
+    tZ = np.zeros(m)
+    sc = np.zeros(3)
+    for s0, s1, _, _, K in chunks():
+        sl = slice(s0, s1)
+        q = np.einsum("ij,ij->i", K, K @ K22inv)
+        Z[sl] = sig2 + tau2 + delta - q
+        SZ += K.T @ ((1.0 / Z[sl])[:, None] * K)
+        pb, pt, ps = obj_partials(K, sl)
+        SB += pb
+        tZ += pt
+        sc += ps
+    BmZinv = np.linalg.inv(K22 + SZ)
+    objs = []
+    y1 = np.empty(n)
+    g = np.empty(n)
+    omzw = np.empty(n)
+    rv = np.empty(n)
+
+    def consume(SB, tZ, sc):
+        BmB = K22 + SB
+        C = np.linalg.inv(BmB)
+        x1 = BmZinv @ tZ
+        objs.append(-0.5 * sc[0] + 0.5 * tZ @ x1 + sc[1]
+                    - 0.5 * (-ld22 + np.linalg.slogdet(BmB)[1]) - 0.5 * sc[2])
+        return C, x1
+
+    C, x1 = consume(SB, tZ, sc)
+    cnt = 0.0
+    while len(objs) == 1 or (len(objs) < maxit and (abs(objs[-1] - objs[-2]) > tol or cnt > 0)):
+        # NR part a: y1 = K x1, grad psi, v = K^T (gpsi / (1 - ZW)), the stop-rule count
+        v = np.zeros(m)
+        cnt = 0.0
+        for s0, s1, _, _, K in chunks():
+            sl = slice(s0, s1)
+            fz, Zc = f[sl], Z[sl]
+            W = -a_ * np.exp(fz)
+            omzw[sl] = 1.0 - Zc * W
+            g[sl] = y[sl] - a_ * np.exp(fz)
+            rv[sl] = fz - mu[sl]
+            y1[sl] = K @ x1
+            gpsi = g[sl] - (rv[sl] - y1[sl]) / Zc
+            v += K.T @ (gpsi / omzw[sl])
+            cnt += float(np.sum(np.abs(gpsi) > tol))
+        # NR part b: f update, then the next objective's partials from the same chunk
+        x2 = C @ v
+        SB = np.zeros((m, m))
+        tZ = np.zeros(m)
+        sc = np.zeros(3)
+        for s0, s1, _, _, K in chunks():
+            sl = slice(s0, s1)
+            f[sl] = f[sl] + (Z[sl] * g[sl] - rv[sl] + y1[sl] + K @ x2) / omzw[sl]
+            pb, pt, ps = obj_partials(K, sl)
+            SB += pb
+            tZ += pt
+            sc += ps
+        C, x1 = consume(SB, tZ, sc)
+
+    # ---- gradient part a: c2, p = diag(K C K^T), sv; K^T c2, K^T g, K^T (B sv)
+    c2 = np.empty(n)
+    Bv = np.empty(n)
+    sv = np.empty(n)
+    dMt = np.empty(n)
+    red = np.zeros(3 * m)
+    for s0, s1, _, _, K in chunks():
+        sl = slice(s0, s1)
+        fz, Zc = f[sl], Z[sl]
+        W = -a_ * np.exp(fz)
+        B = W / (Zc * W - 1.0)
+        Bv[sl] = B
+        g[sl] = y[sl] - a_ * np.exp(fz)
+        c2[sl] = (fz - mu[sl] - K @ x1) / Zc
+        p = np.einsum("ij,ij->i", K, K @ C)
+        dMt[sl] = B - B * B * p
+        D = W - 1.0 / Zc
+        coef = 1.0 / (Zc * D)
+        sv[sl] = -1.0 / D + coef * coef * p                          # comp4 (W3 / W = 1)
+        red[:m] += K.T @ c2[sl]
+        red[m:2 * m] += K.T @ g[sl]
+        red[2 * m:] += K.T @ (B * sv[sl])
+    s = K22inv @ red[:m]
+    GG = K22inv @ red[m:2 * m]
+    Cw = C @ red[2 * m:]
+
+    # ---- gradient part b: G = c2 s^T - h GG^T - diag(B) K C - diag(2a) K K22^-1 contracted
+    # with dK12 / dlog theta; S_a = K^T diag(a) K, sum a
+    Sa = np.zeros((m, m))
+    suma = 0.0
+    e_sig = 0.0
+    e_l = np.zeros(L)
+    c_sum = 0.0
+    ukeys = _row_keys(U)
+    korder = np.argsort(ukeys)
+    usorted = ukeys[korder]
+    for s0, s1, Xs, x2, K in chunks():
+        sl = slice(s0, s1)
+        B = Bv[sl]
+        h = B * sv[sl] - B * (K @ Cw)
+        a = -0.5 * dMt[sl] + 0.5 * c2[sl] ** 2 - 0.5 * h * g[sl]
+        G = np.outer(c2[sl], s)
+        G -= np.outer(h, GG)
+        G -= B[:, None] * (K @ C)
+        G -= (2.0 * a)[:, None] * (K @ K22inv)
+        keys = _row_keys(X[s0:s1])
+        pos = np.searchsorted(usorted, keys)
+        pos[pos >= m] = m - 1
+        for i in np.nonzero(usorted[pos] == keys)[0]:
+            for j in np.nonzero(ukeys == keys[i])[0]:
+                c_sum += G[i, j]
+        Sa += K.T @ (a[:, None] * K)
+        suma += float(a.sum())
+        G *= K                                                       # W = G o K
+        rs = G.sum(axis=1)
+        cs = G.sum(axis=0)
+        e_sig += float(rs.sum())
+        XW = Xs.T @ G
+        if kernel == "sqexp":
+            e_l[0] += float(x2 @ rs - 2.0 * np.sum(XW * Us.T) + cs @ u2)
+        else:
+            e_l += (Xs * Xs).T @ rs - 2.0 * np.sum(XW * Us.T, axis=1) + (Us * Us).T @ cs
+
+    # ---- finish (adjoint_ref.NumpyLaplaceRank._finish)
+    Xo = np.outer(Cw, GG)
+    G22 = 0.5 * (K22inv - C) - 0.5 * np.outer(s, s) + 0.25 * (Xo + Xo.T) + K22inv @ Sa @ K22inv
+    grad = np.zeros(L + 2)
+    grad[0] = 2 * e_sig + np.sum(G22 * 2 * Kuu) + 2 * sig2 * suma
+    if kernel == "sqexp":
+        grad[1] = e_l[0] + np.sum(G22 * Kuu * np.sum(dU ** 2, axis=2)) / ls[0] ** 2
+    else:
+        for c in range(L):
+            grad[1 + c] = e_l[c] + np.sum(G22 * Kuu * (dU[:, :, c] / ls[c]) ** 2)
+    coinc22 = np.all(dU == 0.0, axis=2)
+    grad[L + 1] = 2 * tau2 * c_sum + 2 * tau2 * np.sum(G22[coinc22]) + 2 * tau2 * suma
+    return objs[-1], grad, f, np.array(objs)

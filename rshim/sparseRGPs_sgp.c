@@ -18,10 +18,12 @@
  * Part 2 is the fused hot path for the R drivers (rshim/R/sgp_hotpath.R): a device-resident
  * context per fit (external pointer with a finalizer) and one call per optimizer iteration.
  *
- * Build: see rshim/Makevars (links -lsgp).  Not compiled in this repository's CI (R's headers
- * are absent); tests/test_rshim.py checks the registry against the reference's, checks that
- * every sgp_* symbol used is declared in sgp.h and exported by libsgp.so, and syntax-checks
- * this file against the R API prototypes it uses.
+ * Build: see rshim/Makevars (links -lsgp).  R itself is absent from this repository's
+ * environments, so the file is compiled (gcc -Werror) against tests/r_api/'s declarations of
+ * the R API it uses and linked with a mock R runtime (tests/r_api/mock_rt.c):
+ * tests/test_rshim_exec.py calls every registered routine by name and arity, checks PROTECT
+ * balance after each call and compares the results with fixtures and the oracle;
+ * tests/test_rshim.py checks the registry against the reference's RcppExports.cpp.
  */
 #include <R.h>
 #include <Rinternals.h>

@@ -2,6 +2,13 @@
 
 The shared library lands in sparsergps_amd/lib/libsgp.so so it travels with the repository
 snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
+
+The product build takes no flags from the environment: experiment variants (-D knobs of
+sgp_probe.h) are built by `build_variant()` into their own directory under tools/ab/, never
+into lib/.  Every object records the compile flags it was built with in a stamp file beside
+it (`<obj>.cmd`); an object is rebuilt when a source or header is newer than it or when its
+flags differ from the stamp, so a library built with other flags can never be kept as the
+product by an mtime check.
 """
 from __future__ import annotations
 
@@ -10,12 +17,14 @@ import shutil
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libsgp.so")
+VARIANT_ROOT = os.path.join(ROOT, "tools", "ab")
 SOURCES = ["capi.hip", "k_cov.hip", "k_mfma.hip", "k_dense.hip", "k_lap.hip"]
-HEADERS = ["sgp_internal.h", os.path.join("..", "..", "include", "sgp.h")]
-ARCH = os.environ.get("SGP_OFFLOAD_ARCH", "gfx950")
+HEADERS = ["sgp_internal.h", "sgp_probe.h", os.path.join("..", "..", "include", "sgp.h")]
+ARCH = "gfx950"
 
 
 class HipccMissing(RuntimeError):
@@ -23,18 +32,10 @@ class HipccMissing(RuntimeError):
 
 
 def hipcc():
-    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
         if cand and os.path.exists(cand):
             return cand
     raise HipccMissing("hipcc not found: cannot build libsgp.so")
-
-
-def _stale():
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS]
-    return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
 
 
 # Per-source compiler flags.  k_dense.hip: MFMA accumulators in VGPRs -- the Gauss-Jordan
@@ -44,37 +45,138 @@ def _stale():
 FILE_FLAGS = {"k_dense.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile every HIP source for gfx950 into lib/libsgp.so (incremental per object)."""
-    if not force and not _stale():
-        return LIB
-    os.makedirs(LIBDIR, exist_ok=True)
-    cc = hipcc()
-    objs = []
-    procs = []
+def _compile_flags(src, defs=()):
+    return ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wno-unused-result",
+            *FILE_FLAGS.get(src, []), *defs]
+
+
+def _compile_cmd(cc, src, obj, defs=()):
+    return [cc, *_compile_flags(src, defs), "-c", os.path.join(CSRC, src), "-o", obj]
+
+
+LINK_FLAGS = [f"--offload-arch={ARCH}", "-shared", "-fPIC"]
+
+
+def _link_cmd(cc, objs, out):
+    return [cc, *LINK_FLAGS, "-o", out] + list(objs)
+
+
+# The stamps hold the flags and inputs by name only (no compiler or repository path), so a
+# snapshot of the tree that lands at another path (the GPU box) sees its objects as current.
+def _stamp(path):
+    return path + ".cmd"
+
+
+def _read_stamp(path):
+    try:
+        with open(_stamp(path)) as f:
+            return f.read()
+    except OSError:
+        return None
+
+
+def _write_stamp(path, key):
+    with open(_stamp(path), "w") as f:
+        f.write(key)
+
+
+def _obj_key(src, defs):
+    return "\0".join([src, *_compile_flags(src, defs)])
+
+
+def _lib_key(objs):
+    return "\0".join([*LINK_FLAGS, *(os.path.basename(o) for o in objs)])
+
+
+def _obj_stale(obj, key, src):
+    if not os.path.exists(obj) or _read_stamp(obj) != key:
+        return True
+    # a source depends on its own text and on every header (all sources include sgp_internal.h)
+    t = os.path.getmtime(obj)
+    deps = [os.path.join(CSRC, src)] + [os.path.join(CSRC, h) for h in HEADERS]
+    return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
+
+
+def _plan(outdir, defs):
+    objs, todo = [], []
     for src in SOURCES:
-        obj = os.path.join(LIBDIR, src.replace(".hip", ".o"))
+        obj = os.path.join(outdir, src.replace(".hip", ".o"))
         objs.append(obj)
-        # SGP_HIPCC_DEFS: extra -D flags for A/B experiment builds (tools/ab_*.sh), never set
-        # for the product library
-        extra = os.environ.get("SGP_HIPCC_DEFS", "").split()
-        cmd = [cc, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wno-unused-result",
-               *FILE_FLAGS.get(src, []), *extra, "-c", os.path.join(CSRC, src), "-o", obj]
-        procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
-    for cmd, p in procs:
+        if _obj_stale(obj, _obj_key(src, defs), src):
+            todo.append((src, obj))
+    return objs, todo
+
+
+def _lib_stale(lib, objs):
+    if not os.path.exists(lib) or _read_stamp(lib) != _lib_key(objs):
+        return True
+    t = os.path.getmtime(lib)
+    return any(os.path.getmtime(o) > t for o in objs)
+
+
+def _build_into(outdir, lib, defs, force, verbose):
+    cc = hipcc()
+    os.makedirs(outdir, exist_ok=True)
+    objs, todo = _plan(outdir, defs)
+    if force:
+        todo = list(zip(SOURCES, objs))
+    procs = []
+    for src, obj in todo:
+        cmd = _compile_cmd(cc, src, obj, defs)
+        procs.append((src, cmd, obj,
+                      subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+    failed = None
+    for src, cmd, obj, p in procs:
         out, _ = p.communicate()
         if p.returncode != 0:
-            raise RuntimeError(f"hipcc failed ({' '.join(cmd)}):\n{out.decode(errors='replace')}")
+            failed = failed or f"hipcc failed ({' '.join(cmd)}):\n{out.decode(errors='replace')}"
+            continue
+        _write_stamp(obj, _obj_key(src, defs))
         if verbose and out:
             print(out.decode(errors="replace"))
-    tmp = LIB + ".tmp"
-    cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
-    res = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    if failed:
+        raise RuntimeError(failed)
+    if not force and not todo and not _lib_stale(lib, objs):
+        return lib
+    tmp = lib + ".tmp"
+    res = subprocess.run(_link_cmd(cc, objs, tmp), stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     if res.returncode != 0:
         raise RuntimeError(f"link failed:\n{res.stdout.decode(errors='replace')}")
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    _write_stamp(lib, _lib_key(objs))
+    return lib
+
+
+def stale() -> bool:
+    """True when build() would compile or link anything."""
+    objs, todo = _plan(LIBDIR, ())
+    return bool(todo) or _lib_stale(LIB, objs)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile the HIP sources for gfx950 into lib/libsgp.so, recompiling only the objects
+    whose source, headers or compile command changed."""
+    if os.environ.get("SGP_HIPCC_DEFS"):
+        raise RuntimeError("SGP_HIPCC_DEFS is not honoured by the product build; "
+                           "use sparsergps_amd._build.build_variant() for A/B libraries")
+    return _build_into(LIBDIR, LIB, (), force, verbose)
+
+
+def build_variant(name: str, defs, force: bool = False, verbose: bool = False) -> str:
+    """An experiment library (extra -D flags, SGP_PROBE_BUILD implied) in tools/ab/<name>/.
+
+    Load it with SGP_AB_LIB=<returned path> (sparsergps_amd._lib accepts only paths under
+    tools/ab/).  The product lib/libsgp.so is never touched."""
+    if not name or "/" in name or name.startswith("."):
+        raise ValueError(f"bad variant name {name!r}")
+    defs = ["-DSGP_PROBE_BUILD", *defs]
+    outdir = os.path.join(VARIANT_ROOT, name)
+    return _build_into(outdir, os.path.join(outdir, "libsgp.so"), defs, force, verbose)
 
 
 if __name__ == "__main__":
-    print(build(force=True, verbose=True))
+    import sys
+    if len(sys.argv) > 2 and sys.argv[1] == "variant":
+        print(build_variant(sys.argv[2], sys.argv[3:], force=True, verbose=True))
+    else:
+        print(build(force=True, verbose=True))

@@ -9,7 +9,7 @@ import ctypes as C
 import os
 import threading
 
-from ._build import LIB, HipccMissing, build
+from ._build import LIB, VARIANT_ROOT, HipccMissing, build
 
 _lock = threading.Lock()
 _lib = None
@@ -112,24 +112,40 @@ class NotPositiveDefinite(SGPError):
     """R's chol() failure (caught by try() in the reference's knot proposals)."""
 
 
+def _ab_lib():
+    """SGP_AB_LIB: an experiment library built by _build.build_variant() (tools/ab/<name>/),
+    for A/B timing runs only.  Any other path is refused, so the variable cannot point the
+    product at an arbitrary binary."""
+    p = os.environ.get("SGP_AB_LIB")
+    if not p:
+        return None
+    p = os.path.realpath(p)
+    root = os.path.realpath(VARIANT_ROOT) + os.sep
+    if not p.startswith(root):
+        raise RuntimeError(f"SGP_AB_LIB must name a library under {root} (got {p})")
+    return p
+
+
 def lib(auto_build: bool = True):
     """Load (building if needed) libsgp.so.  Raises if it cannot be loaded."""
     global _lib
     with _lock:
         if _lib is not None:
             return _lib
-        if auto_build:
-            # rebuilds only when a source is newer than the library (a stale .so would
-            # otherwise be loaded silently).  Only a missing hipcc lets the existing library
-            # be used; a compile or link error always propagates.
+        path = _ab_lib()
+        if path is None and auto_build:
+            # rebuilds when a source or header is newer than an object or its compile command
+            # changed (a stale .so would otherwise be loaded silently).  Only a missing hipcc
+            # lets the existing library be used; a compile or link error always propagates.
             try:
                 build()
             except HipccMissing:
                 if not os.path.exists(LIB):
                     raise
-        if not os.path.exists(LIB):
-            raise RuntimeError(f"libsgp.so not found at {LIB}; run sparsergps_amd._build.build()")
-        h = C.CDLL(LIB, mode=C.RTLD_GLOBAL)
+        path = path or LIB
+        if not os.path.exists(path):
+            raise RuntimeError(f"libsgp.so not found at {path}; run sparsergps_amd._build.build()")
+        h = C.CDLL(path, mode=C.RTLD_GLOBAL)
         for name, (res, args) in PROTOTYPES.items():
             fn = getattr(h, name)
             fn.restype = res

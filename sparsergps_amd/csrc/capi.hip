@@ -119,8 +119,12 @@ namespace {
 // kp->ctr = column means of the m x d knot matrix U (column-major, ld ldu; host memory), and
 // kp->span2 = a bound on |x~|^2 over the knots and the data box [xlo, xhi] (per coordinate;
 // NULL = knots only) that the matrix-core builder's accuracy guard reads (knm_mfma_ok).
+// extra (T points, column-major, ld ldx; NULL = none): further points the same parameters will
+// be built against (OAT candidate knots, which may lie outside the data box): they widen
+// span2 but do not move the centre.
 void set_center(KernParams* kp, const double* U, int64_t m, int64_t ldu, const double* xlo,
-                const double* xhi) {
+                const double* xhi, const double* extra = nullptr, int64_t T = 0,
+                int64_t ldx = 0) {
   double span2 = 0.0;
   for (int c = 0; c < kp->d; ++c) {
     double s = 0.0, lo = U[c * ldu], hi = U[c * ldu];
@@ -134,6 +138,11 @@ void set_center(KernParams* kp, const double* U, int64_t m, int64_t ldu, const d
     if (xlo && xhi) {
       lo = xlo[c] < lo ? xlo[c] : lo;
       hi = xhi[c] > hi ? xhi[c] : hi;
+    }
+    for (int64_t j = 0; extra && j < T; ++j) {
+      const double v = extra[j + c * ldx];
+      lo = v < lo ? v : lo;
+      hi = v > hi ? v : hi;
     }
     const double e = fmax(fabs(lo - kp->ctr[c]), fabs(hi - kp->ctr[c])) * kp->rl[c];
     span2 += e * e;
@@ -438,16 +447,22 @@ uint64_t coord_hash_host(const double* x, int64_t stride, int d) {
   return h;
 }
 
-int upload_knots(sgp_ctx* c, const double* U, int64_t m, int64_t ldu) {
-  // An evaluation that was begun but never finished (an error between the phases) can leave
-  // the K22 chain (aux: writes status[0], sc[SC_LD22], reads U) and aux_lo work queued.  The
-  // new evaluation's knot upload and status / scalar resets on the main stream must not
-  // overtake it.
+// An evaluation that was begun but never finished (an error or an abandoned caller between
+// the phases) can leave the K22 chain (aux: writes status[0], sc[SC_LD22], reads U) and aux_lo
+// work queued.  Every entry that begins an evaluation (VI / FITC phase 1, Laplace begin, the
+// full GP) calls this before it touches phase, U, status or sc, so the new evaluation's knot
+// upload and resets on the main stream cannot overtake that work.  Only an abandoned
+// evaluation (phase != 0) pays the two cross-stream waits.
+int drain_abandoned(sgp_ctx* c) {
   if (c->phase != 0) {
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_m3, 0));
     c->phase = 0;
   }
+  return SGP_OK;
+}
+
+int upload_knots(sgp_ctx* c, const double* U, int64_t m, int64_t ldu) {
   // optimizer iterations with fixed knots (xu_opt = "fixed") pass the same U every time: keep
   // the resident copy and its hash table
   if (c->knots_valid && c->knots_mp == c->mp && (int64_t)c->hU.size() == m * c->d) {
@@ -1002,6 +1017,8 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   if (st) return st;
   if (!red1) { set_err("red1 is NULL"); return SGP_EINVAL; }
   HIPCHK(hipSetDevice(c->device));
+  st = drain_abandoned(c);
+  if (st) return st;
   timers_reset(c);
   c->kp = kp;
   c->m = m;
@@ -1319,6 +1336,8 @@ int sgp_fitc_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U
   if (st) return st;
   if (!red1) { set_err("red1 is NULL"); return SGP_EINVAL; }
   HIPCHK(hipSetDevice(c->device));
+  st = drain_abandoned(c);
+  if (st) return st;
   timers_reset(c);
   c->kp = kp;
   c->m = m;
@@ -1615,6 +1634,8 @@ int sgp_lap_begin(sgp_ctx* c, int kernel, const double* theta, const double* U, 
     return SGP_EINVAL;
   }
   HIPCHK(hipSetDevice(c->device));
+  st = drain_abandoned(c);
+  if (st) return st;
   st = lap_ensure(c);
   if (st) return st;
   timers_reset(c);
@@ -1622,13 +1643,13 @@ int sgp_lap_begin(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   c->m = m;
   c->mp = round_up(m, SGP_TILE);
   c->delta = delta;
-  c->phase = 0;
   c->lap_expo = expo;
   c->lap_tol = tol;
   c->lap_maxit = maxit;
   c->flags = flags;
   c->lap_it = 0;
   c->lap_cnt = 0.0;
+  c->lap_gpsi_valid = false;   // grad psi belongs to the NR run that starts here
   c->lap_objs.clear();
   const int64_t mp = c->mp;
   st = upload_knots(c, U, m, ldu);
@@ -2004,6 +2025,8 @@ int sgp_eval_full(sgp_ctx* c, int kernel, const double* theta, double delta, uns
   int st = make_params(kernel, c->d, theta, delta, &kp);
   if (st) return st;
   HIPCHK(hipSetDevice(c->device));
+  st = drain_abandoned(c);   // before U is overwritten below
+  if (st) return st;
   timers_reset(c);
   c->kp = kp;
   c->m = c->n;
@@ -2287,6 +2310,10 @@ int sgp_vi_candidates(sgp_ctx* c, int kernel, const double* theta, const double*
     HIPCHK(hipMemcpyAsync(c->sc + SC_RR, c->red1 + mm + mp, sizeof(double),
                           hipMemcpyDeviceToDevice, c->stream));
   }
+  // the candidate builds' parameters: phase 1's (same centre), with the accuracy guard's span
+  // widened to the candidates, which may lie outside the data box (knot bounds, Q9)
+  KernParams kpc = kp;
+  set_center(&kpc, U, m, ldu, c->xmin.data(), c->xmax.data(), cand, T, ldc);
   constexpr int64_t TP = 128;
   DevBuf Kc, slab, P, part, rk, cc, Uc, K22c, W, SW, Bt, BB, base, out;
   const int64_t slab_cap = gemm_tn_slab_doubles(n_pad, mp, TP);
@@ -2335,11 +2362,11 @@ int sgp_vi_candidates(sgp_ctx* c, int kernel, const double* theta, const double*
     HIPCHK(hipMemcpyAsync(Uc.p, hU.data(), sizeof(double) * hU.size(), hipMemcpyHostToDevice,
                           c->stream));
     Scope tm(c, "candidates");
-    HIPCHK(launch_build_knm(kp, c->X, n_pad, c->n, n_pad, Uc.p, TP, tc, TP, Kc.p, c->stream));
+    HIPCHK(launch_build_knm(kpc, c->X, n_pad, c->n, n_pad, Uc.p, TP, tc, TP, Kc.p, c->stream));
     HIPCHK(launch_gemm_tn(c->K, mp, mp, Kc.p, TP, TP, n_pad, slab.p, slab_cap, P.p, c->stream));
     HIPCHK(launch_gemv_cols(Kc.p, n_pad, TP, c->r, n_pad, 1, part.p, part_cap, rk.p, c->stream));
     HIPCHK(launch_colnorm2(Kc.p, n_pad, TP, part.p, part_cap, cc.p, c->stream));
-    HIPCHK(launch_build_knm(kp, c->U, mp, m, mp, Uc.p, TP, tc, TP, K22c.p, c->stream));
+    HIPCHK(launch_build_knm(kpc, c->U, mp, m, mp, Uc.p, TP, tc, TP, K22c.p, c->stream));
     HIPCHK(launch_gemm64(false, false, false, mp, TP, mp, 1.0, c->K22inv, mp, K22c.p, TP, 0.0,
                          W.p, TP, c->stream));
     HIPCHK(launch_gemm64(false, false, false, mp, TP, mp, 1.0, S, mp, W.p, TP, 0.0, SW.p, TP,

@@ -10,6 +10,7 @@
 // R/laplace_approx_gradient.R:133-336) with a = exposure (`m` in the reference's Poisson
 // helpers): W = d2 = d3 = -a e^f, d1 = y - a e^f.
 #include "sgp_internal.h"
+#include "sgp_probe.h"
 
 namespace {
 
@@ -302,9 +303,6 @@ __global__ void __launch_bounds__(128) k_gemv_cols(const double* __restrict__ K,
 //   pass and S_B comes from the weighted SYRK without t.
 // One workgroup per row chunk; part[ch][0..mp) and the scalars sc[ch][..] are reduced by
 // launch_colsum (fixed order).  mp <= 2048 (x staged beside the rows).
-#ifndef SGP_NRA_LDS
-#define SGP_NRA_LDS 8192
-#endif
 constexpr int NRA_LDS = SGP_NRA_LDS;          // doubles of the row-block image
 constexpr int NRA_LD2 = NRA_LDS / 512;        // double2 loads per thread and block
 enum { LAP_PASS_A = 0, LAP_PASS_B = 1 };

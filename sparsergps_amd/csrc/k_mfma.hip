@@ -124,9 +124,6 @@ __device__ __forceinline__ void mfma_interleave() {
 #pragma unroll
   for (int i = 0; i < 64; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                      // MFMA
-#ifndef SGP_IL_VMEM0
-#define SGP_IL_VMEM0 0
-#endif
     if (i >= SGP_IL_VMEM0 && i < SGP_IL_VMEM0 + NVMEM)
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                    // VMEM read
     if (SPREAD ? (i & 1) == 0 : i < 32)
@@ -136,12 +133,6 @@ __device__ __forceinline__ void mfma_interleave() {
       __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);                    // DS write
   }
 }
-#ifndef SGP_CON_IL_PAT
-#define SGP_CON_IL_PAT 2   // contraction: stores in the last MFMA slots (65.5 vs 64.5 TF/s)
-#endif
-#ifndef SGP_SYRK_IL_PAT
-#define SGP_SYRK_IL_PAT 0
-#endif
 // With-t SYRK: the next k-step's operand loads pinned to the top of the step (a scheduling
 // barrier after them, no VMEM groups in the interleave).  The group-barrier request alone
 // leaves the loads at MFMA slots 16-54 of 64 with their vmcnt wait 4-30 slots later
@@ -630,9 +621,6 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
           acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
     }
     CON_SSTORE(cur ^ 1);   // on the last step into the idle buffer
-#ifndef SGP_CON_IL_SPREAD
-#define SGP_CON_IL_SPREAD false   // reads up front: 66.5-66.9 vs 65.3 TF/s spread
-#endif
     mfma_interleave<SGP_CON_IL_SPREAD, SGP_CON_IL_PAT>();
     __syncthreads();
   }
@@ -1477,11 +1465,8 @@ hipError_t launch_knot_reduce(const double* knot_slab, int64_t ntiles, int64_t m
   return hipGetLastError();
 }
 
-// dynamic LDS of the gradient-contraction launches: 0 in the product; tools/micro/con_trace.hip
-// builds with a pad that leaves one workgroup per CU (the k-loop without a co-resident partner)
-#ifndef SGP_CON_SHMEM
-#define SGP_CON_SHMEM 0
-#endif
+// dynamic LDS of the gradient-contraction launches: SGP_CON_SHMEM (sgp_probe.h) is 0 in the
+// product; tools/micro/con_trace.hip builds with a pad that leaves one workgroup per CU
 template <int DT, bool KNOT = false>
 static void launch_con_grad(bool v2, const KernParams& kp, const double* K, const double* M,
                             const double* X, int64_t ldx, int64_t n, int64_t n_pad,

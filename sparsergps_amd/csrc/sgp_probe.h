@@ -8,11 +8,42 @@
 //   SGP_CON_TRACE(k)       s_memtime stamp k of a k_contract workgroup   (tools/micro/con_trace.hip)
 //   SGP_CON_NO_EPILOGUE    k_contract<.., EPI_GRAD> returns after the k-loop (timing only)
 //   SGP_GJ_TRACE(k, p)     stamp p of the GJ look-ahead workgroup at pivot k (tools/micro/gj_trace.hip)
+//
+// Experiment knobs (schedule / staging alternatives measured in A/B runs).  The product values
+// are fixed here; overriding one needs SGP_PROBE_BUILD, i.e. a variant library built by
+// sparsergps_amd._build.build_variant() into tools/ab/ (the product build takes no -D flags):
+//   SGP_IL_VMEM0        first MFMA slot of the k-step's global loads (mfma_interleave)
+//   SGP_CON_IL_PAT      LDS-store placement of the contraction's k-step (mfma_interleave PAT)
+//   SGP_SYRK_IL_PAT     the same for the SYRKs
+//   SGP_CON_IL_SPREAD   contraction: LDS fragment reads spread over the step instead of up front
+//   SGP_CON_SHMEM       dynamic LDS pad of the gradient-contraction launches
+//   SGP_NRA_LDS         doubles of k_lap_rowpass's row-block image
 #pragma once
 
-#if (defined(SGP_CON_TRACE) || defined(SGP_CON_NO_EPILOGUE) || defined(SGP_GJ_TRACE)) && \
+#if (defined(SGP_CON_TRACE) || defined(SGP_CON_NO_EPILOGUE) || defined(SGP_GJ_TRACE) ||      \
+     defined(SGP_IL_VMEM0) || defined(SGP_CON_IL_PAT) || defined(SGP_SYRK_IL_PAT) ||          \
+     defined(SGP_CON_IL_SPREAD) || defined(SGP_CON_SHMEM) || defined(SGP_NRA_LDS)) &&         \
     !defined(SGP_PROBE_BUILD)
-#error "timing probes are for tools/micro builds only (define SGP_PROBE_BUILD there)"
+#error "timing probes and experiment knobs are for variant builds only (SGP_PROBE_BUILD)"
+#endif
+
+#ifndef SGP_IL_VMEM0
+#define SGP_IL_VMEM0 0
+#endif
+#ifndef SGP_CON_IL_PAT
+#define SGP_CON_IL_PAT 2   // contraction: stores in the last MFMA slots (65.5 vs 64.5 TF/s)
+#endif
+#ifndef SGP_SYRK_IL_PAT
+#define SGP_SYRK_IL_PAT 0
+#endif
+#ifndef SGP_CON_IL_SPREAD
+#define SGP_CON_IL_SPREAD false   // reads up front: 66.5-66.9 vs 65.3 TF/s spread
+#endif
+#ifndef SGP_CON_SHMEM
+#define SGP_CON_SHMEM 0
+#endif
+#ifndef SGP_NRA_LDS
+#define SGP_NRA_LDS 8192
 #endif
 
 // k_contract: stamp k from thread 0 of the workgroup

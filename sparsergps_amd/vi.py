@@ -39,6 +39,9 @@ class SparseGPContext:
     """Device-resident rows (X, y - mu) plus work space for up to ``m_max`` knots."""
 
     def __init__(self, xy, y, mu, m_max, device=None, stream=None):
+        if mu is None:
+            raise ValueError("SparseGPContext: mu is required (mean(y) for VI / FITC, "
+                             "log mean(y) for Poisson Laplace)")
         self._lib = _lib.lib()
         _lib.require_gpu()
         X = np.asfortranarray(np.asarray(xy, dtype=np.float64).reshape(len(y), -1))
@@ -67,6 +70,8 @@ class SparseGPContext:
         _lib.check(self._lib.sgp_ctx_set_stream(self.handle, C.c_void_p(int(stream) if stream else 0)))
 
     def set_data(self, y, mu):
+        if mu is None:
+            raise ValueError("set_data: mu is required")
         y = np.ascontiguousarray(np.asarray(y, dtype=np.float64).reshape(-1))
         mu = np.ascontiguousarray(np.broadcast_to(np.asarray(mu, dtype=np.float64), y.shape))
         _lib.check(self._lib.sgp_ctx_set_data(self.handle, _lib.dptr(y), _lib.dptr(mu)))
@@ -378,10 +383,14 @@ def _fingerprint(a):
 def _context_for(xy, y, mu, m, mu_vec=None):
     """Reuse one device context per (xy, y, mu), like the reference driver reuses xy across
     iterations.  Arrays are keyed by identity plus a sampled fingerprint; a scalar mu (the
-    mean(y) default, quirk Q14) is keyed by value, mu=None by the path's default.  mu_vec: the
-    mean actually uploaded."""
-    if mu is None:                       # the path's own default (mean(y) / log mean(y))
-        mu_key = ("default",)
+    mean(y) default, quirk Q14) is keyed by value.  mu_vec: the mean actually uploaded; with
+    mu=None it is the path's own default (a broadcast scalar: mean(y) for VI / FITC, log mean(y)
+    for Laplace) and the key is that value, so paths with different defaults never share a
+    context."""
+    if mu is None:
+        if mu_vec is None:
+            raise ValueError("mu=None: the caller must resolve the path's default mean")
+        mu_key = ("scalar", float(np.asarray(mu_vec, dtype=np.float64).reshape(-1)[0]))
     elif np.ndim(mu) == 0:
         mu_key = ("scalar", float(mu))
     else:
@@ -445,6 +454,8 @@ def vi_eval(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6, ctx=None, r_det=False, 
     theta = theta_vector(cov_par, cov_fun, d, lnames)
     names = param_names(cov_fun, d, lnames)
     xu_m = np.asarray(xu, dtype=np.float64).reshape(-1, d)
+    if mu is None:
+        mu = np.mean(np.asarray(y, dtype=np.float64))                   # quirk Q14
     if ctx is None:
         ctx = _context_for(xy, y, mu, xu_m.shape[0])
     obj, g = ctx.eval_vi(theta, cov_fun, xu_m, delta, r_det=r_det, obj_only=obj_only)
@@ -466,6 +477,8 @@ def fitc_eval(cov_par, cov_fun, xu, xy, y, mu, delta=1e-6, ctx=None, r_det=False
     theta = theta_vector(cov_par, cov_fun, d, lnames)
     names = param_names(cov_fun, d, lnames)
     xu_m = np.asarray(xu, dtype=np.float64).reshape(-1, d)
+    if mu is None:
+        mu = np.mean(np.asarray(y, dtype=np.float64))
     if ctx is None:
         ctx = _context_for(xy, y, mu, xu_m.shape[0])
     obj, g = ctx.eval_fitc(theta, cov_fun, xu_m, delta, r_det=r_det, obj_only=obj_only)

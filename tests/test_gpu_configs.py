@@ -129,6 +129,32 @@ def test_c5_own_knot_count_against_adjoint_model(sgp):
     assert _rel(grad, g) < 1e-7
 
 
+def test_c5_full_size_against_chunked_laplace_model(sgp):
+    """configs[4] exactly (the Laplace bench workload): n = 5e5, m = 512, d = 5, sqexp Poisson,
+    NR from f0 = log mean(y) to the stop rule, then dlogq_dcov_par at the mode -- against the
+    row-chunked CPU model of the same algebra (oracle/adjoint_chunked.eval_laplace, pinned to
+    the literal newtrap_sparseGP + dlogq_dcov_par in tests/test_oracle.py; ~15-30 s of host
+    BLAS).  NR count exact, every NR objective to 1e-9, the mode to 1e-8, the gradient to 1e-7.
+    Reference: R/newtrap_sparseGP.R:6-186, R/laplace_approx_gradient.R:25-553."""
+    from oracle import adjoint_chunked as AC
+    from sparsergps_amd.workloads import make_poisson_problem
+    P = make_poisson_problem()
+    assert P["X"].shape == (500_000, 5) and P["U"].shape == (512, 5)
+    th = np.array(list(P["cov_par"].values()))
+    o, g, f, objs = AC.eval_laplace("sqexp", th, P["X"], P["y"], P["mu"], P["U"], P["f0"], P["a"],
+                                    P["delta"], tol=1e-5)
+    with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=512) as ctx:
+        ctx.lap_set_f(P["f0"])
+        obj, grad, nit = ctx.eval_laplace(th, "sqexp", P["U"], P["delta"], P["a"], 1e-5, 1000)
+        fg = ctx.lap_get_f()
+        ov = ctx.lap_objective_values()
+    assert nit == len(objs) == len(ov)
+    np.testing.assert_allclose(ov, objs, rtol=1e-9, atol=0)
+    assert abs(obj - o) / abs(o) < 1e-9
+    assert np.max(np.abs(fg - f)) < 1e-8
+    assert _rel(grad, g) < 1e-7
+
+
 def test_c3_headline_shape_against_chunked_adjoint_model(sgp):
     """configs[2] exactly (the bench workload): n = 1e6, m = 1024, d = 8, ARD -- the product
     path against the row-chunked CPU model of the same adjoint algebra (~15-40 s of host

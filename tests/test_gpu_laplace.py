@@ -146,3 +146,65 @@ def test_dlogq_mu_omitted_defaults_to_log_mean(sgp):
     s12, s22, Z = O.laplace_mats(P["cov_par"], "sqexp", P["U"], P["X"], P["delta"])
     o_ref = O.obj_fun_pois(ff, np.full(310, np.log(P["y"].mean())), Z, s12, s22, P["y"], P["a"])
     assert abs(o - o_ref) / abs(o_ref) < 1e-10
+
+
+def test_mu_none_defaults_do_not_share_a_context(sgp):
+    """A Laplace call with mu=None (log mean(y)) followed by VI / FITC calls with mu=None
+    (mean(y), quirk Q14) on the same arrays: each path uses its own default mean."""
+    P = _problem(300, 20)
+    X, y = P["X"], P["y"].astype(np.float64)
+    sgp.obj_fun_pois(P["f0"], P["cov_par"], "sqexp", P["U"], X, y, None, P["a"], P["delta"])
+    mu_vi = np.full(len(y), y.mean())
+    o_vi, g_vi = sgp.vi_eval(P["cov_par"], "sqexp", P["U"], X, y, None, P["delta"])
+    o_ref = O.elbo_eval(P["cov_par"], "sqexp", P["U"], X, y, mu_vi, P["delta"])
+    assert abs(o_vi - o_ref) / abs(o_ref) < EVAL_RTOL
+    o_fitc, _ = sgp.fitc_eval(P["cov_par"], "sqexp", P["U"], X, y, None, P["delta"])
+    o_fitc_ref, _ = sgp.fitc_eval(P["cov_par"], "sqexp", P["U"], X, y, y.mean(), P["delta"])
+    assert abs(o_fitc - o_fitc_ref) / abs(o_fitc_ref) < 1e-12
+    # and back: the Laplace default is still log mean(y)
+    o = sgp.obj_fun_pois(P["f0"], P["cov_par"], "sqexp", P["U"], X, y, None, P["a"], P["delta"])
+    s12, s22, Z = O.laplace_mats(P["cov_par"], "sqexp", P["U"], X, P["delta"])
+    o_ref = O.obj_fun_pois(P["f0"], np.full(len(y), np.log(y.mean())), Z, s12, s22, y, P["a"])
+    assert abs(o - o_ref) / abs(o_ref) < 1e-10
+
+
+def test_grad_psi_invalid_after_maxit0_eval(sgp):
+    """sgp_lap_get_grad_psi refers to the last NR run: after an NR run followed by a maxit = 0
+    evaluation (no NR step) it reports SGP_EINVAL instead of the earlier run's values."""
+    from sparsergps_amd import _lib
+    P = _problem(300, 20)
+    th = np.array(list(P["cov_par"].values()))
+    with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=20) as ctx:
+        ctx.lap_set_f(P["f0"])
+        ctx.lap_nr(th, "sqexp", P["U"], P["delta"], P["a"], 1e-5, 1000)
+        ctx.lap_get_grad_psi()
+        ctx.eval_laplace(th * 1.1, "sqexp", P["U"], P["delta"], P["a"], 1e-5, 0)
+        with pytest.raises(_lib.SGPError):
+            ctx.lap_get_grad_psi()
+
+
+@pytest.mark.parametrize("first", ["vi", "fitc"])
+def test_abandoned_phase1_then_laplace(sgp, first):
+    """A VI / FITC evaluation begun (phase 1, other knots) and never finished, then a Laplace
+    evaluation on the same context: the abandoned evaluation's queued K22 chain must not race
+    the new one's knot upload and resets (sgp_lap_begin drains it first)."""
+    import torch
+    P = _problem(400, 30)
+    th = np.array(list(P["cov_par"].values()))
+    with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=64) as ctx:
+        if first == "vi":
+            red1 = torch.zeros(ctx.vi_red1_count(30), dtype=torch.float64, device="cuda")
+            torch.cuda.synchronize()
+            ctx.vi_phase1(th, "sqexp", P["U"] + 0.3, P["delta"], red1.data_ptr())
+        else:
+            red1 = torch.zeros(ctx.fitc_red1_count(30), dtype=torch.float64, device="cuda")
+            torch.cuda.synchronize()
+            ctx.fitc_phase1(th, "sqexp", P["U"] + 0.3, P["delta"], red1.data_ptr())
+        ctx.lap_set_f(P["f0"])
+        obj, grad, it = ctx.eval_laplace(th, "sqexp", P["U"], P["delta"], P["a"], 1e-5, 1000)
+        torch.cuda.synchronize()
+    nr, g = _oracle(P, P["f0"], 1e-5)
+    assert it == len(nr["objective_function_values"])
+    assert abs(obj - nr["objective_function_values"][-1]) / abs(obj) < EVAL_RTOL
+    gv = np.array(list(g.values()))
+    assert np.max(np.abs(grad - gv) / np.maximum(1, np.abs(gv))) < EVAL_RTOL
