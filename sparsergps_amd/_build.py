@@ -50,8 +50,8 @@ def _compile_flags(src, defs=()):
             *FILE_FLAGS.get(src, []), *defs]
 
 
-def _compile_cmd(cc, src, obj, defs=()):
-    return [cc, *_compile_flags(src, defs), "-c", os.path.join(CSRC, src), "-o", obj]
+def _compile_cmd(cc, src, obj, defs=(), csrc=CSRC):
+    return [cc, *_compile_flags(src, defs), "-c", os.path.join(csrc, src), "-o", obj]
 
 
 LINK_FLAGS = [f"--offload-arch={ARCH}", "-shared", "-fPIC"]
@@ -88,21 +88,21 @@ def _lib_key(objs):
     return "\0".join([*LINK_FLAGS, *(os.path.basename(o) for o in objs)])
 
 
-def _obj_stale(obj, key, src):
+def _obj_stale(obj, key, src, csrc=CSRC):
     if not os.path.exists(obj) or _read_stamp(obj) != key:
         return True
     # a source depends on its own text and on every header (all sources include sgp_internal.h)
     t = os.path.getmtime(obj)
-    deps = [os.path.join(CSRC, src)] + [os.path.join(CSRC, h) for h in HEADERS]
+    deps = [os.path.join(csrc, src)] + [os.path.join(csrc, h) for h in HEADERS]
     return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
 
 
-def _plan(outdir, defs):
+def _plan(outdir, defs, csrc=CSRC):
     objs, todo = [], []
     for src in SOURCES:
         obj = os.path.join(outdir, src.replace(".hip", ".o"))
         objs.append(obj)
-        if _obj_stale(obj, _obj_key(src, defs), src):
+        if _obj_stale(obj, _obj_key(src, defs), src, csrc):
             todo.append((src, obj))
     return objs, todo
 
@@ -114,15 +114,15 @@ def _lib_stale(lib, objs):
     return any(os.path.getmtime(o) > t for o in objs)
 
 
-def _build_into(outdir, lib, defs, force, verbose):
+def _build_into(outdir, lib, defs, force, verbose, csrc=CSRC):
     cc = hipcc()
     os.makedirs(outdir, exist_ok=True)
-    objs, todo = _plan(outdir, defs)
+    objs, todo = _plan(outdir, defs, csrc)
     if force:
         todo = list(zip(SOURCES, objs))
     procs = []
     for src, obj in todo:
-        cmd = _compile_cmd(cc, src, obj, defs)
+        cmd = _compile_cmd(cc, src, obj, defs, csrc)
         procs.append((src, cmd, obj,
                       subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
     failed = None
@@ -162,8 +162,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return _build_into(LIBDIR, LIB, (), force, verbose)
 
 
-def build_variant(name: str, defs, force: bool = False, verbose: bool = False) -> str:
-    """An experiment library (extra -D flags, SGP_PROBE_BUILD implied) in tools/ab/<name>/.
+def build_variant(name: str, defs=(), force: bool = False, verbose: bool = False,
+                  rev: str | None = None) -> str:
+    """An experiment library in tools/ab/<name>/: extra -D flags (SGP_PROBE_BUILD implied)
+    and/or the HIP sources of git revision `rev` (A/B against an earlier kernel).
 
     Load it with SGP_AB_LIB=<returned path> (sparsergps_amd._lib accepts only paths under
     tools/ab/).  The product lib/libsgp.so is never touched."""
@@ -171,12 +173,30 @@ def build_variant(name: str, defs, force: bool = False, verbose: bool = False) -
         raise ValueError(f"bad variant name {name!r}")
     defs = ["-DSGP_PROBE_BUILD", *defs]
     outdir = os.path.join(VARIANT_ROOT, name)
-    return _build_into(outdir, os.path.join(outdir, "libsgp.so"), defs, force, verbose)
+    csrc = CSRC
+    if rev is not None:
+        # the revision's sources (csrc + include/sgp.h) exported under tools/ab/<name>/src
+        src_root = os.path.join(outdir, "src")
+        os.makedirs(src_root, exist_ok=True)
+        for path in ["sparsergps_amd/csrc/" + f for f in SOURCES + HEADERS[:2]] + ["include/sgp.h"]:
+            out = subprocess.run(["git", "-C", ROOT, "show", f"{rev}:{path}"],
+                                 stdout=subprocess.PIPE, stderr=subprocess.PIPE, check=True).stdout
+            dst = os.path.join(src_root, path)
+            os.makedirs(os.path.dirname(dst), exist_ok=True)
+            old = open(dst, "rb").read() if os.path.exists(dst) else None
+            if old != out:
+                with open(dst, "wb") as f:
+                    f.write(out)
+        csrc = os.path.join(src_root, "sparsergps_amd", "csrc")
+    return _build_into(outdir, os.path.join(outdir, "libsgp.so"), defs, force, verbose, csrc)
 
 
 if __name__ == "__main__":
     import sys
     if len(sys.argv) > 2 and sys.argv[1] == "variant":
-        print(build_variant(sys.argv[2], sys.argv[3:], force=True, verbose=True))
+        # variant NAME [REV] [-DFLAG ...]
+        rest = sys.argv[3:]
+        rev = rest.pop(0) if rest and not rest[0].startswith("-") else None
+        print(build_variant(sys.argv[2], rest, verbose=True, rev=rev))
     else:
         print(build(force=True, verbose=True))
