@@ -237,8 +237,10 @@ struct sgp_ctx {
   // concurrently with the latency-bound Bm inversion on the main stream
   hipEvent_t ev_s = nullptr, ev_m3 = nullptr, ev_bm = nullptr;
   hipEvent_t ev_lo = nullptr;             // VI phase 1: builder done (main) / side work done (aux_lo)
+  bool vi_k22_ordered = true;             // VI phase 1 ordered main behind K22's build (ev_lo)
   hipStream_t aux_lo = nullptr;           // ... at normal priority (the Bm chain keeps its CUs)
   double* slab_aux = nullptr;             // partials of the aux stream's small reductions
+  double* rr_dev = nullptr;               // r^T r of the resident r (set with r)
   // launch-bound Bm factorisation captured once per (mp, S pointer) and replayed
   // Poisson-Laplace state (row/knot vectors allocated on first use)
   double *y = nullptr, *mu = nullptr;     // per-row data (n_pad), kept for the Laplace path
@@ -403,7 +405,8 @@ void ctx_free(sgp_ctx* c) {
                   c->red2,   c->slab_syrk, c->slab_con, c->slab_small, c->slab_aux, c->sc,
                   c->Xt22,   c->T22,    c->dinv22, c->omega, c->pvec, c->rowq, c->red2f,
                   c->y,      c->mu,     c->lv,     c->lm,    c->lslab, c->lred[0], c->lred[1],
-                  c->Cprev,  c->knot_slab, c->knot_part, c->knot_kmm, c->tslab, c->tq, c->tp};
+                  c->Cprev,  c->knot_slab, c->knot_part, c->knot_kmm, c->tslab, c->tq, c->tp,
+                  c->rr_dev};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->khash) hipFree(c->khash);
@@ -738,6 +741,7 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   c->slab_small_cap = std::max<int64_t>(SLAB_SMALL, mp * (SGP_MAXD + 2));
   st = st ? st : dalloc(&c->slab_small, c->slab_small_cap);
   st = st ? st : dalloc(&c->slab_aux, c->slab_small_cap);
+  st = st ? st : dalloc(&c->rr_dev, 1);
   st = st ? st : dalloc(&c->sc, SC_N);
   st = st ? st : dalloc(&c->y, np_);
   st = st ? st : dalloc(&c->mu, np_);
@@ -780,6 +784,8 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   if (e == hipSuccess) e = hipMemset(c->K, 0, sizeof(double) * np_ * mp);
   if (e == hipSuccess) e = upload_rows(c->y, y, n, np_);
   if (e == hipSuccess) e = upload_rows(c->mu, mu, n, np_);
+  if (e == hipSuccess) e = launch_dot(c->r, c->r, np_, c->slab_aux, c->rr_dev, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
     set_err("HIP error '%s' uploading data", hipGetErrorString(e));
     ctx_free(c);
@@ -814,6 +820,7 @@ int sgp_ctx_set_data(sgp_ctx* c, const double* y, const double* mu) {
   for (int64_t i = 0; i < c->n; ++i) hr[(size_t)i] = y[i] - mu[i];
   HIPCHK(hipMemcpyAsync(c->r, hr.data(), sizeof(double) * hr.size(), hipMemcpyHostToDevice,
                         c->stream));
+  HIPCHK(launch_dot(c->r, c->r, c->n_pad, c->slab_aux, c->rr_dev, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(upload_rows(c->y, y, c->n, c->n_pad));
   HIPCHK(upload_rows(c->mu, mu, c->n, c->n_pad));
@@ -1028,6 +1035,14 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   if (st) return st;
   const int64_t mpv = c->mp, mmv = mpv * mpv;
   int64_t t_rows = 0;
+  // mp = 256 (C2): the fragment-balanced SYRK finishes ~35 us sooner, and the side work that
+  // the main stream waited for on aux_lo (t's partial sums, r^T r, red1's zeroing), starved of
+  // CUs beside the SYRK, would then sit on the critical path; instead t is summed on the main
+  // stream right after the SYRK (a free GPU: two short launches), r^T r is the context's
+  // precomputed constant, red1 needs no zeroing (S, t, rr are all written), and phase 2 waits
+  // for K22's build itself
+  const bool small_syrk = syrk_use_s256(mpv, false);
+  c->vi_k22_ordered = !small_syrk;
   {
     // K12, and t = K^T r riding along in the memory-bound builder (keeps the SYRK's
     // diagonal tiles as cheap as the others); the first HIP call of the evaluation, so the
@@ -1058,22 +1073,28 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->aux));
   st = k22_build(c, kp.tau2);
   if (st) return st;
-  // aux_lo, after the builder: red1's zeroing (before the SYRK reduction below writes S into
-  // it: the main stream waits for ev_lo), t and rr
-  HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_knots, 0));
-  HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_vi_red1_count(m), c->aux_lo));
-  HIPCHK(launch_knot_reduce(c->tslab, t_rows, mpv, 1, c->T1, c->mp_max * c->mp_max,
-                            red1 + mmv, false, c->aux_lo));
-  HIPCHK(launch_dot(c->r, c->r, c->n_pad, c->slab_aux, red1 + mmv + mpv, c->aux_lo));
-  // ev_lo also covers K22's build (aux): the main stream, which waits for ev_lo here, needs no
-  // second cross-stream wait before forming Bm = K22 + S/z in phase 2 (bm_stage)
-  HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_k22m, 0));
-  HIPCHK(hipEventRecord(c->ev_lo, c->aux_lo));
-  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_lo, 0));
+  if (small_syrk) {
+    HIPCHK(launch_knot_reduce(c->tslab, t_rows, mpv, 1, c->T1, c->mp_max * c->mp_max,
+                              red1 + mmv, false, c->stream));
+  } else {
+    // aux_lo, after the builder: red1's zeroing (before the SYRK reduction below writes S into
+    // it: the main stream waits for ev_lo), t and rr
+    HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_knots, 0));
+    HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_vi_red1_count(m), c->aux_lo));
+    HIPCHK(launch_knot_reduce(c->tslab, t_rows, mpv, 1, c->T1, c->mp_max * c->mp_max,
+                              red1 + mmv, false, c->aux_lo));
+    HIPCHK(launch_dot(c->r, c->r, c->n_pad, c->slab_aux, red1 + mmv + mpv, c->aux_lo));
+    // ev_lo also covers K22's build (aux): the main stream, which waits for ev_lo here, needs
+    // no second cross-stream wait before forming Bm = K22 + S/z in phase 2 (bm_stage)
+    HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_k22m, 0));
+    HIPCHK(hipEventRecord(c->ev_lo, c->aux_lo));
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_lo, 0));
+  }
   {
+    // S into red1 (and with small_syrk the constant r^T r; the words past it are not read)
     Scope t(c, "syrk_reduce");
     HIPCHK(launch_syrk_aug(c->K, c->n_pad, mpv, c->r, nullptr, c->slab_syrk, c->slab_syrk_cap,
-                           red1, c->stream, 2, nullptr, 0));
+                           red1, c->stream, 2, nullptr, 0, small_syrk ? c->rr_dev : nullptr));
   }
   // K22's inverse (aux) is queued behind the SYRK here rather than in phase 2: it needs only
   // theta and U, so with several ranks it runs while the first all-reduce is in flight (the
@@ -1190,7 +1211,8 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
       HIPCHK(hipEventRecord(c->ev_m3, c->aux_lo));
     }
   }
-  int st = bm_stage(c, S, 1.0 / z, true);   // K22's build ordered by phase 1's ev_lo
+  // K22's build ordered by phase 1's ev_lo (or waited for here when phase 1 had no side work)
+  int st = bm_stage(c, S, 1.0 / z, c->vi_k22_ordered);
   if (st) return st;
   {
     Scope tm(c, "mm_vectors");
@@ -2299,7 +2321,7 @@ int sgp_vi_candidates(sgp_ctx* c, int kernel, const double* theta, const double*
   const double* S = c->red1;
   const double* t = c->red1 + mm;
   // K22's inverse was queued on aux by sgp_vi_phase1; it runs beside Bm's
-  st = bm_stage(c, S, 1.0 / z, true);   // K22's build ordered by phase 1's ev_lo
+  st = bm_stage(c, S, 1.0 / z, c->vi_k22_ordered);   // as sgp_vi_phase2
   if (st) return st;
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
   {

@@ -119,16 +119,18 @@ struct SyrkTMap {
 // PAT (experiments, tools/micro/con_trace.hip): where the LDS stores go (0: MFMA slots 48-55,
 // 2: 56-63, 3: 32-39, 4: not grouped)
 // NVMEM: global loads of the step placed one per MFMA slot (the 8 operand loads).
-template <bool SPREAD = false, int PAT = 0, int NVMEM = 8>
+// NMFMA: MFMAs in the step (64; 32 for the contraction's 128 x 64 tail tiles), the store slots
+// keeping their distance from the end of the step.
+template <bool SPREAD = false, int PAT = 0, int NVMEM = 8, int NMFMA = 64>
 __device__ __forceinline__ void mfma_interleave() {
 #pragma unroll
-  for (int i = 0; i < 64; ++i) {
+  for (int i = 0; i < NMFMA; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                      // MFMA
     if (i >= SGP_IL_VMEM0 && i < SGP_IL_VMEM0 + NVMEM)
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                    // VMEM read
     if (SPREAD ? (i & 1) == 0 : i < 32)
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                    // DS read
-    constexpr int w0 = PAT == 2 ? 56 : PAT == 3 ? 32 : 48;
+    constexpr int w0 = PAT == 2 ? NMFMA - 8 : PAT == 3 ? NMFMA / 2 : NMFMA - 16;
     if (PAT != 4 && i >= w0 && i < w0 + 8)
       __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);                    // DS write
   }
@@ -362,18 +364,142 @@ k_syrk_reduce_grp(double* __restrict__ slab, int splits, int64_t nblk) {
 
 __global__ void __launch_bounds__(256)
 k_syrk_reduce_blk(const double* __restrict__ slab, int splits, int64_t nblk, int64_t mp,
-                  double* __restrict__ red, int stride) {
+                  double* __restrict__ red, int stride, const double* __restrict__ rr_src) {
   const int64_t bid = blockIdx.y;
   const int e = blockIdx.x * 256 + threadIdx.x;   // element of the 64 x 64 block
+  if (rr_src && bid == 0 && e == 0) red[mp * mp + mp] = *rr_src;   // a precomputed r^T r
   int rp = (int)((sqrtf(8.0f * (float)bid + 1.0f) - 1.0f) * 0.5f);
   while ((int64_t)(rp + 1) * (rp + 2) / 2 <= bid) ++rp;
   while ((int64_t)rp * (rp + 1) / 2 > bid) --rp;
   const int cp = (int)(bid - (int64_t)rp * (rp + 1) / 2);
+  // a diagonal 64-block's upper fragments are not written by k_syrk_s256: the lower element of
+  // each symmetric pair writes both (a, b) and (b, a), for both SYRK kernels
+  if (rp == cp && (e / 64) / 16 < (e % 64) / 16) return;
   double v = 0.0;
   for (int sp = 0; sp < splits; sp += stride) v += slab[((int64_t)sp * nblk + bid) * 4096 + e];
   const int64_t a = (int64_t)rp * 64 + e / 64, b = (int64_t)cp * 64 + e % 64;
   red[a * mp + b] = v;
   red[b * mp + a] = v;
+}
+
+// ============================================================================ SYRK, mp = 256
+// S = K^T diag(w) K for mp = 256 (C2's knot count), without t.  The packed 64-block kernel
+// above runs 12 wave-blocks per row chunk there for 8 of algorithmic work (its diagonal
+// 64-blocks whole and two idle packing slots: 1.5 n m^2 executed), and every packed workgroup
+// keeps one full-cost wave, so skipping work inside it does not shorten the barrier-bound step
+// (profiles/r4/syrk_kind_skip_ab.txt).  Here the 136 lower 16x16 fragments of S are split evenly
+// over the 8 waves of a row chunk's two workgroups: wave v owns fragment rows v and 15 - v
+// (v + 1 and 16 - v fragments: 17 each), so the chunk executes 136 / 128 = 1.06 n m^2 and every
+// wave has the same MFMA count.  Each workgroup stages the chunk's whole 16 x 256 row slab (two
+// workgroups per CU: one waits at its step barrier while the other computes -- one 512-thread
+// workgroup sharing a single staged slab ran 20 % slower); the weights scale the two A
+// fragments of a k-substep (2 multiplies, not 4).  The lower fragments land in the 64-block
+// slabs of k_syrk_blk (k_syrk_reduce_blk mirrors a diagonal block's lower fragments and skips
+// its upper ones, which are never written).
+constexpr int SB2 = 272;   // [k][256] image row stride: 2 * 272 % 64 == 32, as SB
+
+template <int V, bool WEIGHTED>
+__device__ __forceinline__ void syrk256_body(const double* __restrict__ K,
+                                             const double* __restrict__ w, int64_t rbeg,
+                                             int nsteps, double (*Ks)[BK * SB2],
+                                             double (*ws)[BK], double* __restrict__ out) {
+  constexpr int R0 = V, R1 = 15 - V, N0 = R0 + 1, N1 = R1 + 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  d4 acc0[N0], acc1[N1];
+#pragma unroll
+  for (int c = 0; c < N0; ++c) acc0[c] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int c = 0; c < N1; ++c) acc1[c] = d4{0.0, 0.0, 0.0, 0.0};
+  // loader: row tid >> 4 of the step, double2 columns (tid & 15) + 16 q, q < 8
+  const int lrow = tid >> 4, lc = tid & 15;
+  const double2* gK = reinterpret_cast<const double2*>(K + (rbeg + lrow) * 256) + lc;
+  constexpr int64_t gstep = BK * 256 / 2;
+  double2 v[8];
+  double vw = 1.0;
+#define S256_GLOAD(step)                                                        \
+  {                                                                             \
+    const int64_t o_ = (int64_t)(step) * gstep;                                 \
+    _Pragma("unroll") for (int q = 0; q < 8; ++q) v[q] = gK[o_ + 16 * q];       \
+    if constexpr (WEIGHTED) vw = w[rbeg + (int64_t)(step) * BK + (tid & (BK - 1))]; \
+  }
+#define S256_SSTORE(buf)                                                        \
+  {                                                                             \
+    double2* p_ = reinterpret_cast<double2*>(&Ks[buf][lrow * SB2]) + lc;        \
+    _Pragma("unroll") for (int q = 0; q < 8; ++q) p_[16 * q] = v[q];            \
+    if constexpr (WEIGHTED) ws[buf][tid & (BK - 1)] = vw;                       \
+  }
+  if (nsteps > 0) {
+    S256_GLOAD(0);
+    S256_SSTORE(0);
+  }
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
+    S256_GLOAD(step + 1 < nsteps ? step + 1 : step);   // one basic block per step
+    const double* Kc = Ks[cur];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int krow = kk * 4 + (lane >> 4);
+      const double* row = Kc + krow * SB2 + (lane & 15);
+      double a0 = row[R0 * 16], a1 = row[R1 * 16];
+      if constexpr (WEIGHTED) {
+        const double wk = ws[cur][krow];
+        a0 *= wk;
+        a1 *= wk;
+      }
+#pragma unroll
+      for (int c = 0; c < N1; ++c) {
+        const double b = row[c * 16];
+        if (c < N0) acc0[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b, acc0[c], 0, 0, 0);
+        acc1[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b, acc1[c], 0, 0, 0);
+      }
+    }
+    S256_SSTORE(cur ^ 1);   // on the last step into the idle buffer
+    __syncthreads();
+  }
+#undef S256_GLOAD
+#undef S256_SSTORE
+  // fragment (R, c) -> 64-block (R / 4, c / 4) of the slab, element ((R % 4) * 16 + row) * 64 +
+  // (c % 4) * 16 + col
+#pragma unroll
+  for (int c = 0; c < N1; ++c)
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      if (hh == 0 && c >= N0) continue;
+      const int R = hh == 0 ? R0 : R1;
+      const d4& a = hh == 0 ? acc0[c] : acc1[c];
+      const int rp = R / 4, cp = c / 4;
+      double* blk = out + (int64_t)(rp * (rp + 1) / 2 + cp) * 4096;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        blk[((R % 4) * 16 + (lane >> 4) + 4 * q) * 64 + (c % 4) * 16 + (lane & 15)] = a[q];
+    }
+}
+
+template <bool WEIGHTED>
+__global__ void __launch_bounds__(256, 2)
+k_syrk_s256(const double* __restrict__ K, int64_t n_pad, const double* __restrict__ w,
+            int64_t chunk, double* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) double Ks[2][BK * SB2];
+  __shared__ double ws[2][BK];
+  const int64_t nwg = (int64_t)gridDim.x;
+  const int64_t wgid = xcd_remap(blockIdx.x, nwg);   // a chunk's two workgroups on one XCD
+  const int64_t split = wgid >> 1;
+  const int v = (int)(wgid & 1) * 4 + (threadIdx.x >> 6);
+  const int64_t rbeg = split * chunk;
+  int64_t rend = rbeg + chunk;
+  if (rend > n_pad) rend = n_pad;
+  const int nsteps = rend > rbeg ? (int)((rend - rbeg) / BK) : 0;
+  double* out = slab + split * 10 * 4096;   // nblk = 10 lower 64-blocks at mp = 256
+#define S256_CASE(v_)                                                          \
+  case v_:                                                                     \
+    syrk256_body<v_, WEIGHTED>(K, w, rbeg, nsteps, Ks, ws, out);               \
+    break;
+  switch (v) {   // wave-uniform: each wave runs its own fragment rows' k-loop
+    S256_CASE(0) S256_CASE(1) S256_CASE(2) S256_CASE(3)
+    S256_CASE(4) S256_CASE(5) S256_CASE(6) S256_CASE(7)
+  }
+#undef S256_CASE
 }
 
 // ============================================================================ TN GEMM
@@ -1318,19 +1444,58 @@ SyrkPlan syrk_plan_blk(int64_t n_pad, int64_t mp) {
   return p;
 }
 
+// k_syrk_s256 (mp = 256): two workgroups per row chunk, as many chunks as fill one residency
+// round
+static SyrkPlan syrk_plan_s256(int64_t n_pad) {
+  SyrkPlan p;
+  p.nb = 2;
+  p.T = 2;
+  constexpr int64_t kSlots = 512;
+  const int64_t max_splits = n_pad / BK > 0 ? n_pad / BK : 1;
+  int64_t sp = kSlots / p.T;
+  if (sp > max_splits) sp = max_splits;
+  int64_t chunk = (n_pad + sp - 1) / sp;
+  chunk = (chunk + BK - 1) / BK * BK;
+  p.chunk = chunk;
+  p.splits = (int)((n_pad + chunk - 1) / chunk);
+  return p;
+}
+
 }  // namespace
 
-int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp) {
+// the fragment-balanced k_syrk_s256 serves the SYRKs without t at mp = 256
+bool syrk_use_s256(int64_t mp, bool with_t) { return mp == 256 && !with_t; }
+
+namespace {
+
+int64_t syrk_slab_doubles_mp(int64_t n_pad, int64_t mp) {
   SyrkPlan q = syrk_plan_blk(n_pad, mp);
   const int64_t nblk = (int64_t)(2 * q.nb) * (2 * q.nb + 1) / 2;
-  return (int64_t)q.splits * nblk * 4096 + (int64_t)q.splits * q.nb * T128 + q.splits;
+  int64_t need = (int64_t)q.splits * nblk * 4096 + (int64_t)q.splits * q.nb * T128 + q.splits;
+  if (mp == 256) {
+    SyrkPlan r = syrk_plan_s256(n_pad);
+    need = std::max(need, (int64_t)r.splits * (10 * 4096 + 2 * T128 + 1));   // as the launcher lays out
+  }
+  return need;
+}
+}  // namespace
+
+// slab capacity for every knot count up to mp (an evaluation may use fewer knots than the
+// context was created for, and the small-m plans have more splits)
+int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp) {
+  int64_t need = 0;
+  for (int64_t q = T128; q <= mp; q += T128) need = std::max(need, syrk_slab_doubles_mp(n_pad, q));
+  return need;
 }
 
 hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const double* r,
                            const double* w, double* slab, int64_t slab_cap, double* red,
-                           hipStream_t s, int part, const double* tv, int with_t) {
-  {   // the packed 64-block kernel (no redundant diagonal-tile halves)
-    SyrkPlan q = syrk_plan_blk(n_pad, mp);
+                           hipStream_t s, int part, const double* tv, int with_t,
+                           const double* rr_src) {
+  {   // the packed 64-block kernel (no redundant diagonal-tile halves), or at mp = 256 the
+      // fragment-balanced k_syrk_s256 (same slab layout and reduction)
+    const bool s256 = syrk_use_s256(mp, with_t != 0);
+    SyrkPlan q = s256 ? syrk_plan_s256(n_pad) : syrk_plan_blk(n_pad, mp);
     const int64_t nblk = (int64_t)(2 * q.nb) * (2 * q.nb + 1) / 2;
     double* sl_s = slab;
     double* sl_t = sl_s + (int64_t)q.splits * nblk * 4096;
@@ -1349,7 +1514,12 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
         for (int gi = 0; gi < q.T; ++gi) tm.e[gi] = (signed char)(tm.S > 0 ? tmap[gi] : -1);
       }
     }
-    if (part & 1) {
+    if ((part & 1) && s256) {
+      if (w)
+        hipLaunchKernelGGL((k_syrk_s256<true>), grid, dim3(256), 0, s, K, n_pad, w, q.chunk, sl_s);
+      else
+        hipLaunchKernelGGL((k_syrk_s256<false>), grid, dim3(256), 0, s, K, n_pad, w, q.chunk, sl_s);
+    } else if (part & 1) {
       // with t: the weighted forms only (FITC phase 1: w = 1/Z; Laplace: w = B with tv)
       if (with_t && !w) return hipErrorInvalidValue;
       // rows of the t slice per thread: 8 / S (tm.S == 0: one slice per panel)
@@ -1385,7 +1555,7 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
         stride = SYRK_RGRP;
       }
       hipLaunchKernelGGL(k_syrk_reduce_blk, dim3(4096 / 256, (unsigned)nblk), dim3(256), 0, s,
-                         sl_s, q.splits, nblk, mp, red, stride);
+                         sl_s, q.splits, nblk, mp, red, stride, rr_src);
       if (with_t)
         hipLaunchKernelGGL(k_syrk_reduce_t, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s,
                            sl_t, sl_rr, q.splits, q.nb, mp, red);

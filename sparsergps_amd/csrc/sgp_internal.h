@@ -158,8 +158,11 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
                            const double* w, double* slab, int64_t slab_cap, double* red,
                            hipStream_t s, int part = 3,  // part: 1 = main kernel, 2 = reduce
                            const double* tv = nullptr,
-                           int with_t = 1);              // 0: S only (red[mm..] untouched)
+                           int with_t = 1,               // 0: S only (red[mm..] untouched)
+                           const double* rr_src = nullptr);   // part 2: copy *rr_src to red[mm+mp]
 int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp);
+// true when launch_syrk_aug uses the fragment-balanced mp = 256 kernel (S only)
+bool syrk_use_s256(int64_t mp, bool with_t);
 // Gradient contraction on T = K M (K: n_pad x mp, M: mp x mp):
 //   G_ij = alpha_i u_j + rs_i T_ij,  alpha_i = (r_i - K_i u) * iz_i computed in the same pass
 //   (iz_i = invz_vec ? invz_vec[i] : invz; uvec == nullptr -> alpha = u = 0;
