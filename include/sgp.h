@@ -130,6 +130,14 @@ int sgp_vi_phase1(sgp_ctx* ctx, int kernel, const double* theta, const double* U
                   int64_t ldu, double delta, double* red1);
 int sgp_vi_phase2(sgp_ctx* ctx, const double* red1, int64_t n_global, unsigned flags, double* red2);
 int sgp_vi_finish(sgp_ctx* ctx, const double* red2, double* obj, double* grad);
+/* Packed first reduction (multi-GPU VI): with packing on, phase1 writes S as its lower 64 x 64
+ * blocks only -- the (mp/64)(mp/64 + 1)/2 blocks of 4096 doubles, block (r, c) with r >= c
+ * at index r (r + 1) / 2 + c, row-major inside -- followed by t (mp) and r'r, i.e.
+ * sgp_vi_red1_packed_count(m) doubles instead of sgp_vi_red1_count(m) (53 % of it at
+ * m = 1024), and phase2 unpacks the summed buffer on the device.  Only the all-reduce between
+ * the phases sees the layout; the result is the same. */
+int64_t sgp_vi_red1_packed_count(int64_t m);
+int sgp_ctx_set_packed_reduction(sgp_ctx* ctx, int enable);
 
 /* Multi-GPU FITC (three steps, two all-reduces): red1 = [S_D, t, r'D^-1 r, sum log Z],
  * red2 = [S_omega, ..., sum omega, contraction records]; sgp_fitc_finish runs the replicated

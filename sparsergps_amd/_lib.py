@@ -49,6 +49,8 @@ PROTOTYPES = {
     "sgp_eval_fitc": (C.c_int, [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_int64, C.c_int64,
                                 C.c_double, C.c_uint, c_double_p, c_double_p]),
     "sgp_vi_red1_count": (C.c_int64, [C.c_int64]),
+    "sgp_vi_red1_packed_count": (C.c_int64, [C.c_int64]),
+    "sgp_ctx_set_packed_reduction": (C.c_int, [C.c_void_p, C.c_int]),
     "sgp_vi_red2_count": (C.c_int64, [C.c_int, C.c_int]),
     "sgp_vi_phase1": (C.c_int, [C.c_void_p, C.c_int, c_double_p, c_double_p, C.c_int64, C.c_int64,
                                 C.c_double, C.c_void_p]),

@@ -238,6 +238,8 @@ struct sgp_ctx {
   hipEvent_t ev_s = nullptr, ev_m3 = nullptr, ev_bm = nullptr;
   hipEvent_t ev_lo = nullptr;             // VI phase 1: builder done (main) / side work done (aux_lo)
   bool vi_k22_ordered = true;             // VI phase 1 ordered main behind K22's build (ev_lo)
+  bool pack_red1 = false;                 // VI red1 carries S as packed lower 64-blocks
+  double* Sfull = nullptr;                // S unpacked from a packed red1 (mp_max^2)
   hipStream_t aux_lo = nullptr;           // ... at normal priority (the Bm chain keeps its CUs)
   double* slab_aux = nullptr;             // partials of the aux stream's small reductions
   double* rr_dev = nullptr;               // r^T r of the resident r (set with r)
@@ -406,7 +408,7 @@ void ctx_free(sgp_ctx* c) {
                   c->Xt22,   c->T22,    c->dinv22, c->omega, c->pvec, c->rowq, c->red2f,
                   c->y,      c->mu,     c->lv,     c->lm,    c->lslab, c->lred[0], c->lred[1],
                   c->Cprev,  c->knot_slab, c->knot_part, c->knot_kmm, c->tslab, c->tq, c->tp,
-                  c->rr_dev};
+                  c->rr_dev, c->Sfull};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->khash) hipFree(c->khash);
@@ -892,6 +894,28 @@ int64_t sgp_vi_red1_count(int64_t m) {
 
 int64_t sgp_vi_red2_count(int kernel, int d) { return num_ls(kernel, d) + 5; }
 
+int64_t sgp_vi_red1_packed_count(int64_t m) {
+  const int64_t mp = round_up(m, SGP_TILE);
+  return syrk_packed_doubles(mp) + mp + 8;
+}
+
+int sgp_ctx_set_packed_reduction(sgp_ctx* c, int enable) {
+  if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
+  if (c->phase != 0) { set_err("cannot change the reduction layout inside an evaluation"); return SGP_EINVAL; }
+  if (enable && !c->Sfull) {
+    HIPCHK(hipSetDevice(c->device));
+    int st = dalloc(&c->Sfull, c->mp_max * c->mp_max);
+    if (st) return st;
+  }
+  c->pack_red1 = enable != 0;
+  return SGP_OK;
+}
+
+// offset of t in VI's red1 (after S, full or packed); r'r follows t
+static int64_t vi_red1_toff(const sgp_ctx* c, int64_t mp) {
+  return c->pack_red1 ? syrk_packed_doubles(mp) : mp * mp;
+}
+
 int64_t sgp_knot_red_extra(int d, int64_t m) { return round_up(m, SGP_TILE) * d; }
 
 // One K12 contraction pass: per-tile records summed into rec_out (L + 5 doubles) and, with
@@ -1073,17 +1097,19 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   HIPCHK(hipMemsetAsync(c->sc, 0, sizeof(double) * SC_N, c->aux));
   st = k22_build(c, kp.tau2);
   if (st) return st;
+  // red1 = [S (full, or its packed lower 64-blocks), t, r'r]
+  const int64_t toff = vi_red1_toff(c, mpv);
   if (small_syrk) {
     HIPCHK(launch_knot_reduce(c->tslab, t_rows, mpv, 1, c->T1, c->mp_max * c->mp_max,
-                              red1 + mmv, false, c->stream));
+                              red1 + toff, false, c->stream));
   } else {
     // aux_lo, after the builder: red1's zeroing (before the SYRK reduction below writes S into
     // it: the main stream waits for ev_lo), t and rr
     HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_knots, 0));
-    HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * sgp_vi_red1_count(m), c->aux_lo));
+    HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * (toff + mpv + 8), c->aux_lo));
     HIPCHK(launch_knot_reduce(c->tslab, t_rows, mpv, 1, c->T1, c->mp_max * c->mp_max,
-                              red1 + mmv, false, c->aux_lo));
-    HIPCHK(launch_dot(c->r, c->r, c->n_pad, c->slab_aux, red1 + mmv + mpv, c->aux_lo));
+                              red1 + toff, false, c->aux_lo));
+    HIPCHK(launch_dot(c->r, c->r, c->n_pad, c->slab_aux, red1 + toff + mpv, c->aux_lo));
     // ev_lo also covers K22's build (aux): the main stream, which waits for ev_lo here, needs
     // no second cross-stream wait before forming Bm = K22 + S/z in phase 2 (bm_stage)
     HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_k22m, 0));
@@ -1094,7 +1120,8 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
     // S into red1 (and with small_syrk the constant r^T r; the words past it are not read)
     Scope t(c, "syrk_reduce");
     HIPCHK(launch_syrk_aug(c->K, c->n_pad, mpv, c->r, nullptr, c->slab_syrk, c->slab_syrk_cap,
-                           red1, c->stream, 2, nullptr, 0, small_syrk ? c->rr_dev : nullptr));
+                           red1, c->stream, 2, nullptr, 0, small_syrk ? c->rr_dev : nullptr,
+                           c->pack_red1));
   }
   // K22's inverse (aux) is queued behind the SYRK here rather than in phase 2: it needs only
   // theta and U, so with several ranks it runs while the first all-reduce is in flight (the
@@ -1187,10 +1214,14 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
   const int64_t mp = c->mp, mm = mp * mp;
   const double z = kp.tau2 + c->delta;
   const double* S = red1;
-  (void)mm;
-  const double* t = red1 + mm;
+  const int64_t toff = vi_red1_toff(c, mp);
+  const double* t = red1 + toff;
   c->n_global = n_global;
   c->flags = flags;
+  if (c->pack_red1) {   // the summed packed blocks -> full S (m x m consumers below)
+    HIPCHK(launch_unpack_lower64(red1, mp, c->Sfull, c->stream));
+    S = c->Sfull;
+  }
   // K22's inverse (queued on aux at the end of phase 1) runs concurrently with Bm's on the
   // main stream: two latency-bound chains of 256-workgroup steps fit one residency round
   {
@@ -1219,7 +1250,7 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
     if (flags & SGP_FLAG_OBJ_ONLY) {   // elbo_fun alone: no adjoint work
       HIPCHK(dense_gemv(c->Binv, mp, t, 1.0 / z, c->uvec, c->stream));       // u = Binv t / z
       HIPCHK(launch_dot(t, c->uvec, mp, c->slab_small, c->sc + SC_TU, c->stream));
-      HIPCHK(hipMemcpyAsync(c->sc + SC_RR, red1 + mm + mp, sizeof(double),
+      HIPCHK(hipMemcpyAsync(c->sc + SC_RR, red1 + toff + mp, sizeof(double),
                             hipMemcpyDeviceToDevice, c->stream));
       HIPCHK(hipStreamWaitEvent(c->stream, c->ev_m3, 0));
       c->phase = 2;
@@ -1228,7 +1259,7 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
     // u = Binv t / z, P = tau^-2 K22inv - z^-1 Binv, t.u, tr(Binv S) and r^T r in two
     // launches (they sit between the Bm chain and the contraction, on the critical path)
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
-    HIPCHK(launch_vi_mm_vectors(c->Binv, c->K22inv, S, t, red1 + mm + mp, mp, 1.0 / z,
+    HIPCHK(launch_vi_mm_vectors(c->Binv, c->K22inv, S, t, red1 + toff + mp, mp, 1.0 / z,
                                 1.0 / kp.tau2, -1.0 / z, c->uvec, c->Pm, c->slab_small,
                                 c->sc + SC_TU, c->sc + SC_TRBS, c->sc + SC_RR, c->stream));
     HIPCHK(hipEventRecord(c->ev_bm, c->stream));
@@ -2319,7 +2350,12 @@ int sgp_vi_candidates(sgp_ctx* c, int kernel, const double* theta, const double*
   const int64_t mp = c->mp, mm = mp * mp, n_pad = c->n_pad, d = kp.d;
   const double z = kp.tau2 + delta;
   const double* S = c->red1;
-  const double* t = c->red1 + mm;
+  const int64_t toff = vi_red1_toff(c, mp);
+  const double* t = c->red1 + toff;
+  if (c->pack_red1) {
+    HIPCHK(launch_unpack_lower64(c->red1, mp, c->Sfull, c->stream));
+    S = c->Sfull;
+  }
   // K22's inverse was queued on aux by sgp_vi_phase1; it runs beside Bm's
   st = bm_stage(c, S, 1.0 / z, c->vi_k22_ordered);   // as sgp_vi_phase2
   if (st) return st;
@@ -2329,7 +2365,7 @@ int sgp_vi_candidates(sgp_ctx* c, int kernel, const double* theta, const double*
     HIPCHK(dense_gemv(c->Binv, mp, t, 1.0 / z, c->uvec, c->stream));
     HIPCHK(launch_dot(t, c->uvec, mp, c->slab_small, c->sc + SC_TU, c->stream));
     HIPCHK(launch_dot(c->K22inv, S, mm, c->slab_small, c->sc + SC_TRKS, c->stream));
-    HIPCHK(hipMemcpyAsync(c->sc + SC_RR, c->red1 + mm + mp, sizeof(double),
+    HIPCHK(hipMemcpyAsync(c->sc + SC_RR, c->red1 + toff + mp, sizeof(double),
                           hipMemcpyDeviceToDevice, c->stream));
   }
   // the candidate builds' parameters: phase 1's (same centre), with the accuracy guard's span

@@ -364,22 +364,46 @@ k_syrk_reduce_grp(double* __restrict__ slab, int splits, int64_t nblk) {
 
 __global__ void __launch_bounds__(256)
 k_syrk_reduce_blk(const double* __restrict__ slab, int splits, int64_t nblk, int64_t mp,
-                  double* __restrict__ red, int stride, const double* __restrict__ rr_src) {
+                  double* __restrict__ red, int stride, const double* __restrict__ rr_src,
+                  double* __restrict__ rr_dst, int packed) {
   const int64_t bid = blockIdx.y;
   const int e = blockIdx.x * 256 + threadIdx.x;   // element of the 64 x 64 block
-  if (rr_src && bid == 0 && e == 0) red[mp * mp + mp] = *rr_src;   // a precomputed r^T r
+  if (rr_src && bid == 0 && e == 0) *rr_dst = *rr_src;   // a precomputed r^T r
   int rp = (int)((sqrtf(8.0f * (float)bid + 1.0f) - 1.0f) * 0.5f);
   while ((int64_t)(rp + 1) * (rp + 2) / 2 <= bid) ++rp;
   while ((int64_t)rp * (rp + 1) / 2 > bid) --rp;
   const int cp = (int)(bid - (int64_t)rp * (rp + 1) / 2);
   // a diagonal 64-block's upper fragments are not written by k_syrk_s256: the lower element of
-  // each symmetric pair writes both (a, b) and (b, a), for both SYRK kernels
-  if (rp == cp && (e / 64) / 16 < (e % 64) / 16) return;
+  // each symmetric pair writes both (a, b) and (b, a), for both SYRK kernels (packed: the
+  // block as it is, its upper fragments zero; k_unpack_lower64 mirrors)
+  const bool upper = rp == cp && (e / 64) / 16 < (e % 64) / 16;
+  if (upper && !packed) return;
   double v = 0.0;
-  for (int sp = 0; sp < splits; sp += stride) v += slab[((int64_t)sp * nblk + bid) * 4096 + e];
+  if (!upper)
+    for (int sp = 0; sp < splits; sp += stride) v += slab[((int64_t)sp * nblk + bid) * 4096 + e];
+  if (packed) {
+    red[bid * 4096 + e] = v;
+    return;
+  }
   const int64_t a = (int64_t)rp * 64 + e / 64, b = (int64_t)cp * 64 + e % 64;
   red[a * mp + b] = v;
   red[b * mp + a] = v;
+}
+
+// Full symmetric S (mp x mp) from its packed lower 64-blocks (k_syrk_reduce_blk, packed): an
+// element below the block diagonal, or in a diagonal block's lower 16x16 fragments, is read
+// as stored, the rest from its mirror.
+__global__ void __launch_bounds__(256)
+k_unpack_lower64(const double* __restrict__ packed, int64_t mp, double* __restrict__ S) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= mp * mp) return;
+  const int64_t a = idx / mp, b = idx % mp;
+  const int64_t ra = a / 64, rb = b / 64;
+  const int ia = (int)(a % 64), ib = (int)(b % 64);
+  const bool lower = ra > rb || (ra == rb && ia / 16 >= ib / 16);
+  const int64_t r = lower ? ra : rb, c = lower ? rb : ra;
+  const int i = lower ? ia : ib, j = lower ? ib : ia;
+  S[idx] = packed[(r * (r + 1) / 2 + c) * 4096 + i * 64 + j];
 }
 
 // ============================================================================ SYRK, mp = 256
@@ -1491,7 +1515,8 @@ int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp) {
 hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const double* r,
                            const double* w, double* slab, int64_t slab_cap, double* red,
                            hipStream_t s, int part, const double* tv, int with_t,
-                           const double* rr_src) {
+                           const double* rr_src, bool packed) {
+  if (packed && with_t) return hipErrorInvalidValue;   // the packed layout is VI's (no t)
   {   // the packed 64-block kernel (no redundant diagonal-tile halves), or at mp = 256 the
       // fragment-balanced k_syrk_s256 (same slab layout and reduction)
     const bool s256 = syrk_use_s256(mp, with_t != 0);
@@ -1555,13 +1580,25 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
         stride = SYRK_RGRP;
       }
       hipLaunchKernelGGL(k_syrk_reduce_blk, dim3(4096 / 256, (unsigned)nblk), dim3(256), 0, s,
-                         sl_s, q.splits, nblk, mp, red, stride, rr_src);
+                         sl_s, q.splits, nblk, mp, red, stride, rr_src,
+                         red + (packed ? nblk * 4096 : mp * mp) + mp, packed ? 1 : 0);
       if (with_t)
         hipLaunchKernelGGL(k_syrk_reduce_t, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s,
                            sl_t, sl_rr, q.splits, q.nb, mp, red);
     }
     return hipGetLastError();
   }
+}
+
+int64_t syrk_packed_doubles(int64_t mp) {
+  const int64_t nb64 = mp / 64;
+  return nb64 * (nb64 + 1) / 2 * 4096;
+}
+
+hipError_t launch_unpack_lower64(const double* packed, int64_t mp, double* S, hipStream_t s) {
+  hipLaunchKernelGGL(k_unpack_lower64, dim3((unsigned)((mp * mp + 255) / 256)), dim3(256), 0, s,
+                     packed, mp, S);
+  return hipGetLastError();
 }
 
 int64_t gemm_tn_splits(int64_t n_pad, int ntile) {

@@ -96,6 +96,10 @@ class HipRowBackend:
     def stream_context(self):
         return self.torch.cuda.stream(self.stream)
 
+    def set_packed_reduction(self, on=True):
+        if self.mode == "vi":
+            self.ctx.set_packed_reduction(on)
+
     def phase1(self, theta, U, delta):
         m = np.asarray(U).shape[0]
         if self.mode == "vi":
@@ -162,6 +166,10 @@ class RowShardedVI:
         if force and not dist.is_initialized():
             raise RuntimeError("force_collectives needs an initialised torch.distributed group")
         self.collective = self.world > 1 or force
+        # all-reduce #1 carries S as its lower 64 x 64 blocks (8.4 -> 4.5 MB at m = 1024);
+        # phase 2 unpacks on the device
+        if self.collective and hasattr(backend, "set_packed_reduction"):
+            backend.set_packed_reduction(True)
 
     def eval(self, theta, U, delta=1e-6):
         b = self.backend

@@ -233,3 +233,35 @@ def test_high_dimension_ard_matches_oracle(sgp, d):
         assert abs(obj - ro) / abs(ro) < EVAL_RTOL
         for k in cp:
             assert abs(grad[k] - rg[k]) / max(1.0, abs(rg[k])) < EVAL_RTOL, (fun.__name__, k)
+
+
+@pytest.mark.parametrize("cfg,n,m,coinc", [("C2", 3000, 200, False), ("C2", 3000, 256, True),
+                                            ("C3", 2500, 1024, False), ("C3", 1200, 320, True)])
+def test_packed_first_reduction_matches_full(sgp, cfg, n, m, coinc):
+    """sgp_ctx_set_packed_reduction (multi-GPU all-reduce #1 with S as its packed lower 64-blocks,
+    unpacked in phase 2): the phase-split evaluation equals the fused one exactly, for both SYRK
+    kernels (mp = 256: fragment-balanced, its diagonal blocks' upper fragments never written;
+    larger mp: the packed 64-block kernel), with and without coincident knots."""
+    import torch
+    P = O.make_gaussian_problem(cfg, n=n, m=m)
+    U = P["U"].copy()
+    if coinc:
+        U[:2] = P["X"][[5, n - 2]]
+    th = np.array(list(P["cov_par"].values()))
+    with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=m) as ctx:
+        o_ref, g_ref = ctx.eval_vi(th, P["cov_fun"], U, P["delta"])
+        full = ctx.vi_red1_count(m)
+        ctx.set_packed_reduction(True)
+        packed = ctx.vi_red1_count(m)
+        assert packed < full
+        red1 = torch.full((packed,), float("nan"), dtype=torch.float64, device="cuda")
+        red2 = torch.zeros(ctx.vi_red2_count(P["cov_fun"]), dtype=torch.float64, device="cuda")
+        torch.cuda.synchronize()
+        ctx.vi_phase1(th, P["cov_fun"], U, P["delta"], red1.data_ptr())
+        ctx.vi_phase2(red1.data_ptr(), n, red2.data_ptr())
+        o, g = ctx.vi_finish(red2.data_ptr(), th.size)
+        # the fused entry point on the same (packed) context, and the candidates path
+        o2, g2 = ctx.eval_vi(th, P["cov_fun"], U, P["delta"])
+    assert o == o_ref and o2 == o_ref
+    np.testing.assert_array_equal(g, g_ref)
+    np.testing.assert_array_equal(g2, g_ref)
