@@ -1730,7 +1730,8 @@ int sgp_lap_begin(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   {
     Scope t(c, "syrk_z");
     HIPCHK(launch_syrk_aug(c->K, c->n_pad, mp, c->r, lvec(c, LV_ZI), c->slab_syrk,
-                           c->slab_syrk_cap, red_out, c->stream, 3, nullptr, 0));
+                           c->slab_syrk_cap, red_out, c->stream, 3, nullptr, 0, nullptr, false,
+                           true));   // 1/Z > 0
   }
   st = lap_obj_partials(c, red_out, lap_obj_off(mp));
   if (st) return st;
@@ -1893,8 +1894,10 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
       HIPCHK(launch_lap_obj(n, n_pad, lvec(c, LV_F), c->y, c->mu, lvec(c, LV_Z), lvec(c, LV_ZI),
                             c->lap_expo, lvec(c, LV_B), lvec(c, LV_RF), lvec(c, LV_TV),
                             c->slab_small, &nb, c->stream));
+      // B = W / (Z W - 1) >= 0 (W = -a e^f <= 0, Z > 0)
       HIPCHK(launch_syrk_aug(c->K, n_pad, mp, lvec(c, LV_RF), lvec(c, LV_B), c->slab_syrk,
-                             c->slab_syrk_cap, red_out, c->stream, 3, nullptr, 0));
+                             c->slab_syrk_cap, red_out, c->stream, 3, nullptr, 0, nullptr, false,
+                             true));
       HIPCHK(launch_colsum(c->slab_small, nb, 2, red_out + mm + mp + 1, c->stream));
       *count = mm + mp + 3;
       c->lap_state = LS_OBJ;

@@ -142,11 +142,15 @@ __device__ __forceinline__ void mfma_interleave() {
 // ms), but the same pin made the VI SYRK 10 % and the contraction 1.5 % slower and the omega
 // SYRK 5 % slower (profiles/r3/gload_pin_ab.txt), so only the t variants use it.
 
-// WEIGHTED: rows scaled by w (FITC / Laplace); compiled out for the unweighted VI SYRK, whose
-// k-loop otherwise multiplies every A fragment by 1.0 (16 fp64 VALU ops per 64 MFMAs).
+// WMODE: how rows are weighted.  0: not (VI; compiled out, the k-loop would otherwise multiply
+// every A fragment by 1.0); 1: by w on the A fragments, between their LDS reads and the MFMAs
+// (16 fp64 VALU per step on the MFMA operand path; any sign: FITC, Laplace's a and the
+// t-carrying forms); 2 (S only): w >= 0 given as sqrt(w) (k_sqrt_rows), scaling both staged
+// images as they are stored -- the same VALU count, but on the staging path of the next step
+// instead of in front of this step's MFMAs (Laplace's NR objectives S_B and S_Z: 2.7-4 %).
 // TMODE: 0 no t; 1 t = K^T (w o r) with rr = sum w r^2; 2 t = K^T tv with rr = sum tv r.
 // TR: rows of the t slice per thread and step, 8 / S for S slices per panel (syrk_t_table)
-template <int TMODE, bool WEIGHTED, int TR = 2>
+template <int TMODE, int WMODE, int TR = 2>
 __global__ void __launch_bounds__(256, 2)
 k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __restrict__ w,
            const double* __restrict__ r, const double* __restrict__ tv,
@@ -171,6 +175,7 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
   const int dg = (gi >= noff) ? (int)(gi - noff) : -1;
   constexpr bool WITH_T = TMODE != 0;
   constexpr bool with_t = WITH_T;
+  static_assert(!(WMODE == 2 && TMODE != 0), "sqrt(w)-scaled images: S only");
   // tm.S == 0 (more groups than the table holds, m > 1920): one whole-panel slice per panel,
   // panel a >= 1 on the strictly-lower group (a, 0) and panel 0 on diagonal group 0 -- distinct
   // groups, each holding its panel as image A
@@ -211,7 +216,7 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
   const double2* gB = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + tb * (int64_t)T128) + lc;
   const int64_t gstep = BK * mp / 2;
   double2 va0, va1, va2, va3, vb0, vb1, vb2, vb3;
-  double vw = 1.0;
+  double vw = 1.0, vsa = 1.0;   // vw: row tid % BK's weight (WMODE 1); vsa: row lrow's sqrt(w)
   // operand images and column offsets of this wave's row / column panels
   const int ra = (rs >> 1) & 1, ro = (rs & 1) * 64;
   const int ca_ = (cs >> 1) & 1, co = (cs & 1) * 64;
@@ -223,7 +228,8 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
     vb0 = gB[o_]; vb1 = gB[o_ + 16]; vb2 = gB[o_ + 32]; vb3 = gB[o_ + 48];      \
     /* one block: every lane stages row tid % BK (16 lanes per row) */          \
     const int64_t rr_ = rbeg + (int64_t)(step) * BK + (tid & (BK - 1));        \
-    if constexpr (WEIGHTED) vw = w[rr_];                                        \
+    if constexpr (WMODE == 1) vw = w[rr_];                                      \
+    if constexpr (WMODE == 2) vsa = w[rbeg + (int64_t)(step) * BK + lrow];      \
     if constexpr (WITH_T) {                                                     \
       vrr = r[rr_];                                                             \
       if constexpr (has_tv) vr = tv[rr_];                                       \
@@ -235,9 +241,15 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
   {                                                                             \
     double2* pa_ = reinterpret_cast<double2*>(&Ka[buf][lrow * SB]) + lc;        \
     double2* pb_ = reinterpret_cast<double2*>(&Kb[buf][lrow * SB]) + lc;        \
+    if constexpr (WMODE == 2) {                    /* sqrt(w) K in both images */ \
+      va0.x *= vsa; va0.y *= vsa; va1.x *= vsa; va1.y *= vsa;                   \
+      va2.x *= vsa; va2.y *= vsa; va3.x *= vsa; va3.y *= vsa;                   \
+      vb0.x *= vsa; vb0.y *= vsa; vb1.x *= vsa; vb1.y *= vsa;                   \
+      vb2.x *= vsa; vb2.y *= vsa; vb3.x *= vsa; vb3.y *= vsa;                   \
+    }                                                                           \
     pa_[0] = va0; pa_[16] = va1; pa_[32] = va2; pa_[48] = va3;                  \
     pb_[0] = vb0; pb_[16] = vb1; pb_[32] = vb2; pb_[48] = vb3;                  \
-    ws[buf][tid & (BK - 1)] = vw;                                               \
+    if constexpr (WMODE == 1) ws[buf][tid & (BK - 1)] = vw;                     \
     if constexpr (WITH_T) {                                                     \
       double rw_;                                  /* tv_i or (w r)_i */        \
       if constexpr (has_tv) rw_ = vr;                                           \
@@ -273,7 +285,7 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
           af[f] = As[krow * SB + f * 16 + (lane & 15)];
           bf[f] = Bs[krow * SB + f * 16 + (lane & 15)];
         }
-        if constexpr (WEIGHTED) {
+        if constexpr (WMODE == 1) {
           const double wk = ws[cur][krow];
 #pragma unroll
           for (int f = 0; f < 4; ++f) af[f] *= wk;
@@ -346,6 +358,14 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
         const int col = fn * 16 + (lane & 15);
         out[row * 64 + col] = acc[fm][fn][q];
       }
+}
+
+// sqrt of non-negative row weights for k_syrk_blk<.., WMODE 2, ..> (NaN for a negative one, which
+// then surfaces as a failed factorisation instead of a silently wrong S)
+__global__ void __launch_bounds__(256)
+k_sqrt_rows(const double* __restrict__ w, int64_t n, double* __restrict__ sw) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) sw[i] = sqrt(w[i]);
 }
 
 // S (mp x mp full symmetric) from the per-split lower 64-blocks, fixed split order
@@ -1495,10 +1515,11 @@ namespace {
 int64_t syrk_slab_doubles_mp(int64_t n_pad, int64_t mp) {
   SyrkPlan q = syrk_plan_blk(n_pad, mp);
   const int64_t nblk = (int64_t)(2 * q.nb) * (2 * q.nb + 1) / 2;
-  int64_t need = (int64_t)q.splits * nblk * 4096 + (int64_t)q.splits * q.nb * T128 + q.splits;
+  int64_t need = (int64_t)q.splits * nblk * 4096 + (int64_t)q.splits * q.nb * T128 + q.splits +
+                 n_pad;   // + the sqrt(w) rows of WMODE 2
   if (mp == 256) {
     SyrkPlan r = syrk_plan_s256(n_pad);
-    need = std::max(need, (int64_t)r.splits * (10 * 4096 + 2 * T128 + 1));   // as the launcher lays out
+    need = std::max(need, (int64_t)r.splits * (10 * 4096 + 2 * T128 + 1) + n_pad);   // as laid out
   }
   return need;
 }
@@ -1515,7 +1536,7 @@ int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp) {
 hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const double* r,
                            const double* w, double* slab, int64_t slab_cap, double* red,
                            hipStream_t s, int part, const double* tv, int with_t,
-                           const double* rr_src, bool packed) {
+                           const double* rr_src, bool packed, bool w_nonneg) {
   if (packed && with_t) return hipErrorInvalidValue;   // the packed layout is VI's (no t)
   {   // the packed 64-block kernel (no redundant diagonal-tile halves), or at mp = 256 the
       // fragment-balanced k_syrk_s256 (same slab layout and reduction)
@@ -1525,7 +1546,7 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
     double* sl_s = slab;
     double* sl_t = sl_s + (int64_t)q.splits * nblk * 4096;
     double* sl_rr = sl_t + (int64_t)q.splits * q.nb * T128;
-    if (sl_rr + q.splits > slab + slab_cap) return hipErrorInvalidValue;
+    if (sl_rr + q.splits + n_pad > slab + slab_cap) return hipErrorInvalidValue;   // + sqrt(w)
     const dim3 grid((unsigned)(q.splits * q.T));
     SyrkTMap tm{};
     tm.S = 1;
@@ -1549,25 +1570,36 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
       if (with_t && !w) return hipErrorInvalidValue;
       // rows of the t slice per thread: 8 / S (tm.S == 0: one slice per panel)
       const int tr = tm.S >= 4 ? 2 : tm.S == 2 ? 4 : 8;
-#define SYRK_T_LAUNCH(tmode_, tr_)                                                             \
-  hipLaunchKernelGGL((k_syrk_blk<tmode_, true, tr_>), grid, dim3(256), 0, s, K, n_pad, mp, w, r, \
-                     tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm)
+      // non-negative weights without t: their square roots scale the staged images (with t
+      // the extra staging work made FITC's phase-1 SYRK 4.6 % slower, 17.66 -> 18.47 ms at
+      // C3, against 2.7 % faster NR objectives at C5: profiles/r4/syrk_sqrt_rows_ab.txt)
+      const bool wsq = w && w_nonneg && !with_t;
+      const double* wk = w;
+      if (wsq) {
+        double* sw = sl_rr + q.splits;   // n_pad doubles past the partial sums
+        hipLaunchKernelGGL(k_sqrt_rows, dim3((unsigned)((n_pad + 255) / 256)), dim3(256), 0, s,
+                           w, n_pad, sw);
+        wk = sw;
+      }
+#define SYRK_T_LAUNCH(tmode_, wmode_, tr_)                                                     \
+  hipLaunchKernelGGL((k_syrk_blk<tmode_, wmode_, tr_>), grid, dim3(256), 0, s, K, n_pad, mp, wk, \
+                     r, tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm)
       if (with_t && tv) {
-        if (tr == 2) SYRK_T_LAUNCH(2, 2);
-        else if (tr == 4) SYRK_T_LAUNCH(2, 4);
-        else SYRK_T_LAUNCH(2, 8);
+        if (tr == 2) SYRK_T_LAUNCH(2, 1, 2);
+        else if (tr == 4) SYRK_T_LAUNCH(2, 1, 4);
+        else SYRK_T_LAUNCH(2, 1, 8);
       } else if (with_t) {
-        if (tr == 2) SYRK_T_LAUNCH(1, 2);
-        else if (tr == 4) SYRK_T_LAUNCH(1, 4);
-        else SYRK_T_LAUNCH(1, 8);
+        if (tr == 2) SYRK_T_LAUNCH(1, 1, 2);
+        else if (tr == 4) SYRK_T_LAUNCH(1, 1, 4);
+        else SYRK_T_LAUNCH(1, 1, 8);
+      } else if (wsq) {
+        SYRK_T_LAUNCH(0, 2, 2);
+      } else if (w) {
+        SYRK_T_LAUNCH(0, 1, 2);
+      } else {
+        SYRK_T_LAUNCH(0, 0, 2);
       }
 #undef SYRK_T_LAUNCH
-      else if (w)
-        hipLaunchKernelGGL((k_syrk_blk<0, true>), grid, dim3(256), 0, s, K, n_pad, mp, w, r,
-                           tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm);
-      else
-        hipLaunchKernelGGL((k_syrk_blk<0, false>), grid, dim3(256), 0, s, K, n_pad, mp, w, r,
-                           tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm);
     }
     if (part & 2) {
       // many splits (small m): a first pass sums groups of SYRK_RGRP slabs in parallel, the
