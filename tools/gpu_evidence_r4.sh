@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-2 evidence pass on the GPU box: GPU tests, the default bench line (with the CPU
+# Round-4 evidence pass on the GPU box: GPU tests, the default bench line (with the CPU
 # baseline), its rocprofv3 kernel-trace summary, separate PMC passes (FETCH_SIZE, WRITE_SIZE,
-# two SQ sets, L2 hit/miss), the store-bandwidth micro, the secondary modes, shard-size lines
+# two SQ sets, L2 hit/miss), the secondary modes, the 8-GPU shard-size line
 # and the torchrun N=1 (RCCL) rehearsal.
-#   usage (inside gpurun): bash tools/gpu_evidence_r2.sh TAG
+#   usage (inside gpurun): bash tools/gpu_evidence_r4.sh TAG
 set -o pipefail
 T=$1
 D=gpurun_out/$T
@@ -18,12 +18,8 @@ case $rc in 0|1) ;; *) echo "pytest rc=$rc: stopping"; exit $rc;; esac
 step bench
 timeout -k 10 400 python3 bench.py > $D/bench.json 2> $D/bench.err || { tail -20 $D/bench.err; exit 1; }
 cut -c1-300 $D/bench.json
-step store_bw
-timeout -k 10 120 ./tools/micro/store_bw > $D/store_bw.txt 2>&1 || { tail -5 $D/store_bw.txt; exit 1; }
 step kernel-trace
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/k -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $D/k.json 2> $D/k.err || { tail -20 $D/k.err; exit 1; }
-step counters-list
-timeout -k 10 60 rocprofv3 -L > $D/counters_list.txt 2>&1 || true
 step pmc-fetch
 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $D/pf -o run -- $B > $D/pf.json 2> $D/pf.err || { tail -20 $D/pf.err; exit 1; }
 step pmc-write
@@ -39,12 +35,14 @@ timeout -k 10 300 python3 bench.py --mode fitc --no-cpu-baseline > $D/fitc.json 
 timeout -k 10 300 python3 bench.py --mode laplace --steps 10 --warmup 2 --no-cpu-baseline > $D/laplace.json 2> $D/laplace.err || exit 1
 timeout -k 10 300 python3 bench.py --config C2 --steps 20 --warmup 3 --no-cpu-baseline > $D/c2.json 2> $D/c2.err || exit 1
 timeout -k 10 300 python3 bench.py --knots --no-cpu-baseline > $D/knots.json 2> $D/knots.err || exit 1
+step c2-trace
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $D/c2k -o run -- python3 bench.py --config C2 --steps 20 --warmup 3 --no-cpu-baseline > $D/c2k.json 2> $D/c2k.err || { tail -20 $D/c2k.err; exit 1; }
 step shards
-for nn in 125000 250000 500000; do
-  timeout -k 10 200 python3 bench.py --n $nn --steps 10 --warmup 3 --no-cpu-baseline > $D/rows$nn.json 2> $D/rows$nn.err || exit 1
+for nn in 125000; do
+  timeout -k 10 200 python3 bench.py --rows $nn --steps 10 --warmup 3 --no-cpu-baseline > $D/rows$nn.json 2> $D/rows$nn.err || exit 1
 done
 step torchrun
-timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --no-cpu-baseline > $D/trun.json 2> $D/trun.err || { tail -20 $D/trun.err; exit 1; }
+timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --rows 125000 --steps 10 --warmup 3 --no-cpu-baseline > $D/trun.json 2> $D/trun.err || { tail -20 $D/trun.err; exit 1; }
 python3 - "$D" <<'PY'
 import glob, json, sys
 for f in sorted(glob.glob(sys.argv[1] + "/*.json")):
