@@ -1103,13 +1103,12 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
     HIPCHK(launch_knot_reduce(c->tslab, t_rows, mpv, 1, c->T1, c->mp_max * c->mp_max,
                               red1 + toff, false, c->stream));
   } else {
-    // aux_lo, after the builder: red1's zeroing (before the SYRK reduction below writes S into
-    // it: the main stream waits for ev_lo), t and rr
+    // aux_lo, after the builder: red1's zeroing (before the SYRK reduction below writes S and
+    // r^T r into it: the main stream waits for ev_lo) and t
     HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_knots, 0));
     HIPCHK(hipMemsetAsync(red1, 0, sizeof(double) * (toff + mpv + 8), c->aux_lo));
     HIPCHK(launch_knot_reduce(c->tslab, t_rows, mpv, 1, c->T1, c->mp_max * c->mp_max,
                               red1 + toff, false, c->aux_lo));
-    HIPCHK(launch_dot(c->r, c->r, c->n_pad, c->slab_aux, red1 + toff + mpv, c->aux_lo));
     // ev_lo also covers K22's build (aux): the main stream, which waits for ev_lo here, needs
     // no second cross-stream wait before forming Bm = K22 + S/z in phase 2 (bm_stage)
     HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_k22m, 0));
@@ -1117,11 +1116,10 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_lo, 0));
   }
   {
-    // S into red1 (and with small_syrk the constant r^T r; the words past it are not read)
+    // S into red1, and r^T r (the context's constant; the words past it are not read)
     Scope t(c, "syrk_reduce");
     HIPCHK(launch_syrk_aug(c->K, c->n_pad, mpv, c->r, nullptr, c->slab_syrk, c->slab_syrk_cap,
-                           red1, c->stream, 2, nullptr, 0, small_syrk ? c->rr_dev : nullptr,
-                           c->pack_red1));
+                           red1, c->stream, 2, nullptr, 0, c->rr_dev, c->pack_red1));
   }
   // K22's inverse (aux) is queued behind the SYRK here rather than in phase 2: it needs only
   // theta and U, so with several ranks it runs while the first all-reduce is in flight (the

@@ -100,6 +100,19 @@ int main(int argc, char** argv) {
   }
   std::sort(kl.begin(), kl.end());
   std::sort(ep.begin(), ep.end());
+  // epilogue phases: 1 -> 4 setup (alpha, u / cdiag, first K stages, coordinate staging, wait),
+  // 4 -> 5 the eight K half-stages (W and its MFMA products), 5 -> 6 column sums / E /
+  // records into LDS, 6 -> 2 the record reduction and store
+  const int idx[5] = {1, 4, 5, 6, 2};
+  for (int p = 0; p < 4; ++p) {
+    std::vector<double> ph;
+    for (int64_t w = 0; w < nwg; ++w) {
+      const unsigned long long* t = &ht[w * 8];
+      ph.push_back((double)(t[idx[p + 1]] - t[idx[p]]));
+    }
+    std::sort(ph.begin(), ph.end());
+    printf("  epilogue phase t%d->t%d: median %.0f ticks\n", idx[p], idx[p + 1], ph[ph.size() / 2]);
+  }
   printf("n=%lld m=%lld nwg=%lld  median k-loop %.0f ticks, epilogue %.0f ticks, span %llu ticks\n",
          (long long)n, (long long)m, (long long)nwg, kl[kl.size() / 2], ep[ep.size() / 2], tmax - tmin);
   return 0;
