@@ -142,6 +142,111 @@ __device__ __forceinline__ void mfma_interleave() {
 // ms), but the same pin made the VI SYRK 10 % and the contraction 1.5 % slower and the omega
 // SYRK 5 % slower (profiles/r3/gload_pin_ab.txt), so only the t variants use it.
 
+// Balanced S-only plan (syrk_plan_bal): a diagonal 128-tile t of S -- 36 lower 16x16 fragments
+// -- split over the 4 waves of one workgroup as fragment rows v and 7 - v (9 fragments each:
+// 36 MFMAs per step, not the 64 of a packed 64-block wave); these workgroups take longer row
+// chunks so that they finish with the strictly-lower tiles' (k_syrk_blk's off-diagonal
+// groups).  Operands from one staged image (K's column panel t).  WMODE 2 stages sqrt(w)-scaled
+// rows (both operands scaled), WMODE 1 scales the two A fragments of a k-substep.
+template <int V, int WMODE>
+__device__ __forceinline__ void syrk_dt_body(const double* __restrict__ K, int64_t mp,
+                                             const double* __restrict__ w, int t, int64_t rbeg,
+                                             int nsteps, double (*Ka)[BK * SB], double (*ws)[BK],
+                                             double* __restrict__ out) {
+  constexpr int R0 = V, R1 = 7 - V, N0 = R0 + 1, N1 = R1 + 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  d4 acc0[N0], acc1[N1];
+#pragma unroll
+  for (int c = 0; c < N0; ++c) acc0[c] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int c = 0; c < N1; ++c) acc1[c] = d4{0.0, 0.0, 0.0, 0.0};
+  const int lrow = tid >> 4, lc = tid & 15;
+  const double2* gA = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + t * (int64_t)T128) + lc;
+  const int64_t gstep = BK * mp / 2;
+  double2 v[4];
+  double vw = 1.0, vsa = 1.0;
+#define SDT_GLOAD(step)                                                         \
+  {                                                                             \
+    const int64_t o_ = (int64_t)(step) * gstep;                                 \
+    _Pragma("unroll") for (int q = 0; q < 4; ++q) v[q] = gA[o_ + 16 * q];       \
+    if constexpr (WMODE == 1) vw = w[rbeg + (int64_t)(step) * BK + (tid & (BK - 1))]; \
+    if constexpr (WMODE == 2) vsa = w[rbeg + (int64_t)(step) * BK + lrow];      \
+  }
+#define SDT_SSTORE(buf)                                                         \
+  {                                                                             \
+    double2* p_ = reinterpret_cast<double2*>(&Ka[buf][lrow * SB]) + lc;         \
+    _Pragma("unroll") for (int q = 0; q < 4; ++q) {                             \
+      double2 x_ = v[q];                                                        \
+      if constexpr (WMODE == 2) { x_.x *= vsa; x_.y *= vsa; }                   \
+      p_[16 * q] = x_;                                                          \
+    }                                                                           \
+    if constexpr (WMODE == 1) ws[buf][tid & (BK - 1)] = vw;                     \
+  }
+  if (nsteps > 0) {
+    SDT_GLOAD(0);
+    SDT_SSTORE(0);
+  }
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
+    SDT_GLOAD(step + 1 < nsteps ? step + 1 : step);   // one basic block per step
+    const double* Kc = Ka[cur];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int krow = kk * 4 + (lane >> 4);
+      const double* row = Kc + krow * SB + (lane & 15);
+      double a0 = row[R0 * 16], a1 = row[R1 * 16];
+      if constexpr (WMODE == 1) {
+        const double wk = ws[cur][krow];
+        a0 *= wk;
+        a1 *= wk;
+      }
+#pragma unroll
+      for (int c = 0; c < N1; ++c) {
+        const double b = row[c * 16];
+        if (c < N0) acc0[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b, acc0[c], 0, 0, 0);
+        acc1[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b, acc1[c], 0, 0, 0);
+      }
+    }
+    SDT_SSTORE(cur ^ 1);   // on the last step into the idle buffer
+    if constexpr (SGP_SDT_IL && WMODE != 1) mfma_interleave<false, 2, 4, 36>();
+    __syncthreads();
+  }
+#undef SDT_GLOAD
+#undef SDT_SSTORE
+  // fragment (R, c) of tile t -> 64-block (2t + R/4, 2t + c/4) of the slab
+#pragma unroll
+  for (int c = 0; c < N1; ++c)
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      if (hh == 0 && c >= N0) continue;
+      const int R = hh == 0 ? R0 : R1;
+      const d4& a = hh == 0 ? acc0[c] : acc1[c];
+      const int rp = 2 * t + R / 4, cp = 2 * t + c / 4;
+      double* blk = out + (int64_t)(rp * (rp + 1) / 2 + cp) * 4096;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        blk[((R % 4) * 16 + (lane >> 4) + 4 * q) * 64 + (c % 4) * 16 + (lane & 15)] = a[q];
+    }
+}
+
+template <int WMODE>
+__device__ __forceinline__ void syrk_dtile(const double* __restrict__ K, int64_t n_pad,
+                                           int64_t mp, const double* __restrict__ w, int t,
+                                           int64_t sd, int64_t chunk, double (*Ka)[BK * SB],
+                                           double (*ws)[BK], double* __restrict__ out) {
+  const int64_t rbeg = sd * chunk;
+  int64_t rend = rbeg + chunk;
+  if (rend > n_pad) rend = n_pad;
+  const int nsteps = rend > rbeg ? (int)((rend - rbeg) / BK) : 0;
+  switch (threadIdx.x >> 6) {   // wave-uniform
+    case 0: syrk_dt_body<0, WMODE>(K, mp, w, t, rbeg, nsteps, Ka, ws, out); break;
+    case 1: syrk_dt_body<1, WMODE>(K, mp, w, t, rbeg, nsteps, Ka, ws, out); break;
+    case 2: syrk_dt_body<2, WMODE>(K, mp, w, t, rbeg, nsteps, Ka, ws, out); break;
+    default: syrk_dt_body<3, WMODE>(K, mp, w, t, rbeg, nsteps, Ka, ws, out); break;
+  }
+}
+
 // WMODE: how rows are weighted.  0: not (VI; compiled out, the k-loop would otherwise multiply
 // every A fragment by 1.0); 1: by w on the A fragments, between their LDS reads and the MFMAs
 // (16 fp64 VALU per step on the MFMA operand path; any sign: FITC, Laplace's a and the
@@ -155,13 +260,25 @@ __global__ void __launch_bounds__(256, 2)
 k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double* __restrict__ w,
            const double* __restrict__ r, const double* __restrict__ tv,
            int64_t chunk, int ngroups, int nb, double* __restrict__ slab,
-           double* __restrict__ slab_t, double* __restrict__ slab_rr, SyrkTMap tm) {
+           double* __restrict__ slab_t, double* __restrict__ slab_rr, SyrkTMap tm,
+           int64_t nwg_blk, int64_t chunk_d, double* __restrict__ slab_d) {
   __shared__ __attribute__((aligned(16))) double Ka[2][BK * SB];
   __shared__ __attribute__((aligned(16))) double Kb[2][BK * SB];
   __shared__ double ws[2][BK];
   __shared__ double rw[2][BK];   // with_t: (w r)_i or tv_i of the step's rows
 
-  const int64_t nwg = (int64_t)gridDim.x;
+  // the balanced S-only plan's diagonal-tile workgroups follow the packed groups' grid
+  if constexpr (TMODE == 0) {
+    if ((int64_t)blockIdx.x >= nwg_blk) {
+      const int64_t loc = (int64_t)blockIdx.x - nwg_blk;
+      const int t = (int)(loc % nb);
+      const int64_t sd = loc / nb;
+      syrk_dtile<WMODE>(K, n_pad, mp, w, t, sd, chunk_d, Ka, ws,
+                        slab_d + sd * ((int64_t)(2 * nb) * (2 * nb + 1) / 2) * 4096);
+      return;
+    }
+  }
+  const int64_t nwg = nwg_blk;
   const int64_t wgid = xcd_remap(blockIdx.x, nwg);
   const int split = (int)(wgid / ngroups);
   const int64_t gi = wgid % ngroups;
@@ -385,7 +502,8 @@ k_syrk_reduce_grp(double* __restrict__ slab, int splits, int64_t nblk) {
 __global__ void __launch_bounds__(256)
 k_syrk_reduce_blk(const double* __restrict__ slab, int splits, int64_t nblk, int64_t mp,
                   double* __restrict__ red, int stride, const double* __restrict__ rr_src,
-                  double* __restrict__ rr_dst, int packed) {
+                  double* __restrict__ rr_dst, int packed, const double* __restrict__ slab_d,
+                  int splits_d, int stride_d) {
   const int64_t bid = blockIdx.y;
   const int e = blockIdx.x * 256 + threadIdx.x;   // element of the 64 x 64 block
   if (rr_src && bid == 0 && e == 0) *rr_dst = *rr_src;   // a precomputed r^T r
@@ -398,6 +516,12 @@ k_syrk_reduce_blk(const double* __restrict__ slab, int splits, int64_t nblk, int
   // block as it is, its upper fragments zero; k_unpack_lower64 mirrors)
   const bool upper = rp == cp && (e / 64) / 16 < (e % 64) / 16;
   if (upper && !packed) return;
+  // the balanced plan keeps the diagonal 128-tiles' blocks in their own slab region
+  if (slab_d && rp / 2 == cp / 2) {
+    slab = slab_d;
+    splits = splits_d;
+    stride = stride_d;
+  }
   double v = 0.0;
   if (!upper)
     for (int sp = 0; sp < splits; sp += stride) v += slab[((int64_t)sp * nblk + bid) * 4096 + e];
@@ -1488,6 +1612,54 @@ SyrkPlan syrk_plan_blk(int64_t n_pad, int64_t mp) {
   return p;
 }
 
+// Balanced S-only plan (nb >= 3): the strictly-lower 128-tiles as k_syrk_blk's packed groups
+// with S_o row chunks (64 MFMAs per wave-step), the nb diagonal 128-tiles as syrk_dtile
+// workgroups with S_d longer chunks (36 MFMAs per wave-step, no redundant upper fragments), one
+// residency round between them.  Used when its makespan, max(64 chunk_o, 36 chunk_d), beats the
+// packed plan's 64 chunk by more than 2 % (C5's m = 512: 1.143 -> 1.049 n in units of
+// MFMA-steps per row; at m = 1024 the round's integer split counts leave no gain).
+struct SyrkBal {
+  bool on = false;
+  int S_o = 0, S_d = 0;
+  int64_t chunk_o = 0, chunk_d = 0;
+};
+
+static SyrkBal syrk_plan_bal(int64_t n_pad, int64_t mp) {
+  SyrkBal b;
+  const int nb = (int)(mp / T128);
+  if (nb < 3 || !SGP_SYRK_BAL) return b;
+  const int noff = nb * (nb - 1) / 2;
+  constexpr int64_t kSlots = 512;
+  const int64_t max_splits = n_pad / BK > 0 ? n_pad / BK : 1;
+  auto chunk_of = [&](int64_t S) {
+    int64_t c = (n_pad + S - 1) / S;
+    return (c + BK - 1) / BK * BK;
+  };
+  double best = 0.0;
+  for (int64_t So = 1; So * noff < kSlots && So <= max_splits; ++So) {
+    int64_t Sd = (kSlots - So * noff) / nb;
+    if (Sd < 1) break;
+    if (Sd > max_splits) Sd = max_splits;
+    const int64_t co = chunk_of(So), cd = chunk_of(Sd);
+    const double T = std::max(64.0 * (double)co, 36.0 * (double)cd);
+    if (!b.on || T < best) {
+      b.on = true;
+      best = T;
+      b.chunk_o = co;
+      b.chunk_d = cd;
+      b.S_o = (int)((n_pad + co - 1) / co);
+      b.S_d = (int)((n_pad + cd - 1) / cd);
+    }
+  }
+  if (!b.on) return b;
+  // the packed plan: one or more rounds of equal workgroups
+  const SyrkPlan q = syrk_plan_blk(n_pad, mp);
+  const int64_t rounds = ((int64_t)q.splits * q.T + kSlots - 1) / kSlots;
+  const double T_pack = 64.0 * (double)q.chunk * (double)rounds;
+  b.on = best < 0.98 * T_pack;
+  return b;
+}
+
 // k_syrk_s256 (mp = 256): two workgroups per row chunk, as many chunks as fill one residency
 // round
 static SyrkPlan syrk_plan_s256(int64_t n_pad) {
@@ -1517,6 +1689,10 @@ int64_t syrk_slab_doubles_mp(int64_t n_pad, int64_t mp) {
   const int64_t nblk = (int64_t)(2 * q.nb) * (2 * q.nb + 1) / 2;
   int64_t need = (int64_t)q.splits * nblk * 4096 + (int64_t)q.splits * q.nb * T128 + q.splits +
                  n_pad;   // + the sqrt(w) rows of WMODE 2
+  const SyrkBal bal = syrk_plan_bal(n_pad, mp);
+  if (bal.on)
+    need = std::max(need, (int64_t)(bal.S_o + bal.S_d) * nblk * 4096 +
+                              (int64_t)bal.S_o * (q.nb * T128 + 1) + n_pad);
   if (mp == 256) {
     SyrkPlan r = syrk_plan_s256(n_pad);
     need = std::max(need, (int64_t)r.splits * (10 * 4096 + 2 * T128 + 1) + n_pad);   // as laid out
@@ -1542,12 +1718,21 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
       // fragment-balanced k_syrk_s256 (same slab layout and reduction)
     const bool s256 = syrk_use_s256(mp, with_t != 0);
     SyrkPlan q = s256 ? syrk_plan_s256(n_pad) : syrk_plan_blk(n_pad, mp);
+    // S only at nb >= 3: the balanced plan when it beats the packed one (syrk_plan_bal)
+    const SyrkBal bal = (!s256 && !with_t) ? syrk_plan_bal(n_pad, mp) : SyrkBal{};
+    if (bal.on) {
+      q.T = q.nb * (q.nb - 1) / 2;   // the packed kernel's strictly-lower groups only
+      q.splits = bal.S_o;
+      q.chunk = bal.chunk_o;
+    }
     const int64_t nblk = (int64_t)(2 * q.nb) * (2 * q.nb + 1) / 2;
     double* sl_s = slab;
-    double* sl_t = sl_s + (int64_t)q.splits * nblk * 4096;
+    double* sl_d = sl_s + (int64_t)q.splits * nblk * 4096;   // the diagonal tiles' region
+    double* sl_t = sl_d + (bal.on ? (int64_t)bal.S_d * nblk * 4096 : 0);
     double* sl_rr = sl_t + (int64_t)q.splits * q.nb * T128;
     if (sl_rr + q.splits + n_pad > slab + slab_cap) return hipErrorInvalidValue;   // + sqrt(w)
-    const dim3 grid((unsigned)(q.splits * q.T));
+    const int64_t nwg_blk = (int64_t)q.splits * q.T;
+    const dim3 grid((unsigned)(nwg_blk + (bal.on ? (int64_t)bal.S_d * q.nb : 0)));
     SyrkTMap tm{};
     tm.S = 1;
     if ((part & 1) && with_t) {
@@ -1583,7 +1768,7 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
       }
 #define SYRK_T_LAUNCH(tmode_, wmode_, tr_)                                                     \
   hipLaunchKernelGGL((k_syrk_blk<tmode_, wmode_, tr_>), grid, dim3(256), 0, s, K, n_pad, mp, wk, \
-                     r, tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm)
+                     r, tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm, nwg_blk, bal.chunk_d, sl_d)
       if (with_t && tv) {
         if (tr == 2) SYRK_T_LAUNCH(2, 1, 2);
         else if (tr == 4) SYRK_T_LAUNCH(2, 1, 4);
@@ -1604,16 +1789,23 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
     if (part & 2) {
       // many splits (small m): a first pass sums groups of SYRK_RGRP slabs in parallel, the
       // final pass then sums the group totals (fixed order either way: deterministic)
-      int stride = 1;
+      int stride = 1, stride_d = 1;
       if (q.splits > SYRK_RGRP) {
         const unsigned ng = (unsigned)((q.splits + SYRK_RGRP - 1) / SYRK_RGRP);
         hipLaunchKernelGGL(k_syrk_reduce_grp, dim3(4096 / 256, (unsigned)nblk, ng), dim3(256), 0,
                            s, sl_s, q.splits, nblk);
         stride = SYRK_RGRP;
       }
+      if (bal.on && bal.S_d > SYRK_RGRP) {
+        const unsigned ng = (unsigned)((bal.S_d + SYRK_RGRP - 1) / SYRK_RGRP);
+        hipLaunchKernelGGL(k_syrk_reduce_grp, dim3(4096 / 256, (unsigned)nblk, ng), dim3(256), 0,
+                           s, sl_d, bal.S_d, nblk);
+        stride_d = SYRK_RGRP;
+      }
       hipLaunchKernelGGL(k_syrk_reduce_blk, dim3(4096 / 256, (unsigned)nblk), dim3(256), 0, s,
                          sl_s, q.splits, nblk, mp, red, stride, rr_src,
-                         red + (packed ? nblk * 4096 : mp * mp) + mp, packed ? 1 : 0);
+                         red + (packed ? nblk * 4096 : mp * mp) + mp, packed ? 1 : 0,
+                         bal.on ? sl_d : nullptr, bal.S_d, stride_d);
       if (with_t)
         hipLaunchKernelGGL(k_syrk_reduce_t, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s,
                            sl_t, sl_rr, q.splits, q.nb, mp, red);

@@ -18,11 +18,14 @@
 //   SGP_CON_IL_SPREAD   contraction: LDS fragment reads spread over the step instead of up front
 //   SGP_CON_SHMEM       dynamic LDS pad of the gradient-contraction launches
 //   SGP_NRA_LDS         doubles of k_lap_rowpass's row-block image
+//   SGP_SYRK_BAL        0: no balanced S-only SYRK plan (syrk_plan_bal)
+//   SGP_SDT_IL          0: the diagonal-tile SYRK step without the interleave request
 #pragma once
 
 #if (defined(SGP_CON_TRACE) || defined(SGP_CON_NO_EPILOGUE) || defined(SGP_GJ_TRACE) ||      \
      defined(SGP_IL_VMEM0) || defined(SGP_CON_IL_PAT) || defined(SGP_SYRK_IL_PAT) ||          \
-     defined(SGP_CON_IL_SPREAD) || defined(SGP_CON_SHMEM) || defined(SGP_NRA_LDS)) &&         \
+     defined(SGP_CON_IL_SPREAD) || defined(SGP_CON_SHMEM) || defined(SGP_NRA_LDS) ||          \
+     defined(SGP_SYRK_BAL) || defined(SGP_SDT_IL)) &&                                        \
     !defined(SGP_PROBE_BUILD)
 #error "timing probes and experiment knobs are for variant builds only (SGP_PROBE_BUILD)"
 #endif
@@ -44,6 +47,12 @@
 #endif
 #ifndef SGP_NRA_LDS
 #define SGP_NRA_LDS 8192
+#endif
+#ifndef SGP_SYRK_BAL
+#define SGP_SYRK_BAL 1
+#endif
+#ifndef SGP_SDT_IL
+#define SGP_SDT_IL 1
 #endif
 
 // k_contract: stamp k from thread 0 of the workgroup
