@@ -623,6 +623,7 @@ __device__ __forceinline__ void syrk256_body(const double* __restrict__ K,
       }
     }
     S256_SSTORE(cur ^ 1);   // on the last step into the idle buffer
+    if constexpr (SGP_S256_IL) mfma_interleave<false, 2, 8, 68>();
     __syncthreads();
   }
 #undef S256_GLOAD
@@ -1641,7 +1642,7 @@ static SyrkBal syrk_plan_bal(int64_t n_pad, int64_t mp) {
     if (Sd < 1) break;
     if (Sd > max_splits) Sd = max_splits;
     const int64_t co = chunk_of(So), cd = chunk_of(Sd);
-    const double T = std::max(64.0 * (double)co, 36.0 * (double)cd);
+    const double T = std::max(64.0 * (double)co, (double)SGP_SDT_W * (double)cd);
     if (!b.on || T < best) {
       b.on = true;
       best = T;

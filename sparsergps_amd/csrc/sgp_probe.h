@@ -20,12 +20,15 @@
 //   SGP_NRA_LDS         doubles of k_lap_rowpass's row-block image
 //   SGP_SYRK_BAL        0: no balanced S-only SYRK plan (syrk_plan_bal)
 //   SGP_SDT_IL          0: the diagonal-tile SYRK step without the interleave request
+//   SGP_SDT_W           syrk_plan_bal's cost of a diagonal-tile wave-step, in MFMAs (36 issued)
+//   SGP_S256_IL         1: k_syrk_s256's step with an interleave request
 #pragma once
 
-#if (defined(SGP_CON_TRACE) || defined(SGP_CON_NO_EPILOGUE) || defined(SGP_GJ_TRACE) ||      \
+#if (defined(SGP_CON_TRACE) || defined(SGP_CON_NO_EPILOGUE) || defined(SGP_GJ_TRACE) ||       \
      defined(SGP_IL_VMEM0) || defined(SGP_CON_IL_PAT) || defined(SGP_SYRK_IL_PAT) ||          \
      defined(SGP_CON_IL_SPREAD) || defined(SGP_CON_SHMEM) || defined(SGP_NRA_LDS) ||          \
-     defined(SGP_SYRK_BAL) || defined(SGP_SDT_IL)) &&                                        \
+     defined(SGP_SYRK_BAL) || defined(SGP_SDT_IL) || defined(SGP_S256_IL) ||                  \
+     defined(SGP_SDT_W)) &&                                                                   \
     !defined(SGP_PROBE_BUILD)
 #error "timing probes and experiment knobs are for variant builds only (SGP_PROBE_BUILD)"
 #endif
@@ -53,6 +56,12 @@
 #endif
 #ifndef SGP_SDT_IL
 #define SGP_SDT_IL 1
+#endif
+#ifndef SGP_SDT_W
+#define SGP_SDT_W 38
+#endif
+#ifndef SGP_S256_IL
+#define SGP_S256_IL 0
 #endif
 
 // k_contract: stamp k from thread 0 of the workgroup
