@@ -142,18 +142,26 @@ __device__ __forceinline__ void mfma_interleave() {
 // ms), but the same pin made the VI SYRK 10 % and the contraction 1.5 % slower and the omega
 // SYRK 5 % slower (profiles/r3/gload_pin_ab.txt), so only the t variants use it.
 
-// Balanced S-only plan (syrk_plan_bal): a diagonal 128-tile t of S -- 36 lower 16x16 fragments
-// -- split over the 4 waves of one workgroup as fragment rows v and 7 - v (9 fragments each:
-// 36 MFMAs per step, not the 64 of a packed 64-block wave); these workgroups take longer row
-// chunks so that they finish with the strictly-lower tiles' (k_syrk_blk's off-diagonal
-// groups).  Operands from one staged image (K's column panel t).  WMODE 2 stages sqrt(w)-scaled
-// rows (both operands scaled), WMODE 1 scales the two A fragments of a k-substep.
-template <int V, int WMODE>
+// Balanced plan (syrk_plan_bal): a diagonal 128-tile t of S -- 36 lower 16x16 fragments -- split
+// over the 4 waves of one workgroup as fragment rows v and 7 - v (9 fragments each: 36 MFMAs per
+// step, not the 64 of a packed 64-block wave); these workgroups take longer row chunks so that
+// they finish with the strictly-lower tiles' (k_syrk_blk's off-diagonal groups).  Operands from
+// one staged image (K's column panel t).  WMODE 2 stages sqrt(w)-scaled rows (both operands
+// scaled), WMODE 1 scales the two A fragments of a k-substep.  TMODE != 0 (with WMODE 1): the
+// workgroup also forms panel t's slice of t = K^T (w o r) (TMODE 1) or K^T tv (TMODE 2) over its
+// rows from the same image -- column tid % 128, the step's rows tid / 128, +2, ... -- and, for
+// t == 0, rr = sum (w r) r or sum tv r (the off-diagonal groups of k_syrk_blk<.., 3, ..> carry
+// no t work).
+template <int V, int WMODE, int TMODE>
 __device__ __forceinline__ void syrk_dt_body(const double* __restrict__ K, int64_t mp,
-                                             const double* __restrict__ w, int t, int64_t rbeg,
+                                             const double* __restrict__ w,
+                                             const double* __restrict__ r,
+                                             const double* __restrict__ tv, int t, int64_t rbeg,
                                              int nsteps, double (*Ka)[BK * SB], double (*ws)[BK],
+                                             double (*rw)[BK], double& tacc, double& rrp,
                                              double* __restrict__ out) {
   constexpr int R0 = V, R1 = 7 - V, N0 = R0 + 1, N1 = R1 + 1;
+  constexpr bool WITH_T = TMODE != 0;
   const int tid = threadIdx.x, lane = tid & 63;
   d4 acc0[N0], acc1[N1];
 #pragma unroll
@@ -164,15 +172,22 @@ __device__ __forceinline__ void syrk_dt_body(const double* __restrict__ K, int64
   const double2* gA = reinterpret_cast<const double2*>(K + (rbeg + lrow) * mp + t * (int64_t)T128) + lc;
   const int64_t gstep = BK * mp / 2;
   double2 v[4];
-  double vw = 1.0, vsa = 1.0;
+  double vw = 1.0, vsa = 1.0, vrr = 0.0, vr = 0.0;
+  double t4[4] = {0.0, 0.0, 0.0, 0.0};
+  const int tcol = tid & (T128 - 1), trow = tid >> 7;
 #define SDT_GLOAD(step)                                                         \
   {                                                                             \
     const int64_t o_ = (int64_t)(step) * gstep;                                 \
+    const int64_t rr_ = rbeg + (int64_t)(step) * BK + (tid & (BK - 1));        \
     _Pragma("unroll") for (int q = 0; q < 4; ++q) v[q] = gA[o_ + 16 * q];       \
-    if constexpr (WMODE == 1) vw = w[rbeg + (int64_t)(step) * BK + (tid & (BK - 1))]; \
+    if constexpr (WMODE == 1) vw = w[rr_];                                      \
     if constexpr (WMODE == 2) vsa = w[rbeg + (int64_t)(step) * BK + lrow];      \
+    if constexpr (WITH_T) {                                                     \
+      vrr = r[rr_];                                                             \
+      if constexpr (TMODE == 2) vr = tv[rr_];                                   \
+    }                                                                           \
   }
-#define SDT_SSTORE(buf)                                                         \
+#define SDT_SSTORE(buf, fold)                                                   \
   {                                                                             \
     double2* p_ = reinterpret_cast<double2*>(&Ka[buf][lrow * SB]) + lc;         \
     _Pragma("unroll") for (int q = 0; q < 4; ++q) {                             \
@@ -181,15 +196,21 @@ __device__ __forceinline__ void syrk_dt_body(const double* __restrict__ K, int64
       p_[16 * q] = x_;                                                          \
     }                                                                           \
     if constexpr (WMODE == 1) ws[buf][tid & (BK - 1)] = vw;                     \
+    if constexpr (WITH_T) {                                                     \
+      const double rw_ = TMODE == 2 ? vr : vw * vrr;                            \
+      rw[buf][tid & (BK - 1)] = rw_;                                            \
+      rrp = fma(rw_ * (fold), vrr, rrp);                                        \
+    }                                                                           \
   }
   if (nsteps > 0) {
     SDT_GLOAD(0);
-    SDT_SSTORE(0);
+    SDT_SSTORE(0, 1.0);
   }
   __syncthreads();
   for (int step = 0; step < nsteps; ++step) {
     const int cur = step & 1;
-    SDT_GLOAD(step + 1 < nsteps ? step + 1 : step);   // one basic block per step
+    const bool more = step + 1 < nsteps;
+    SDT_GLOAD(more ? step + 1 : step);   // one basic block per step
     const double* Kc = Ka[cur];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
@@ -208,12 +229,21 @@ __device__ __forceinline__ void syrk_dt_body(const double* __restrict__ K, int64
         acc1[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b, acc1[c], 0, 0, 0);
       }
     }
-    SDT_SSTORE(cur ^ 1);   // on the last step into the idle buffer
+    if constexpr (WITH_T) {
+      // the t slice from the current image: rows trow, trow + 2, ... of the step
+#pragma unroll
+      for (int k = 0; k < BK / 2; ++k) {
+        const int q = trow + 2 * k;
+        t4[k & 3] = fma(rw[cur][q], Kc[q * SB + tcol], t4[k & 3]);
+      }
+    }
+    SDT_SSTORE(cur ^ 1, more ? 1.0 : 0.0);   // on the last step into the idle buffer
     if constexpr (SGP_SDT_IL && WMODE != 1) mfma_interleave<false, 2, 4, 36>();
     __syncthreads();
   }
 #undef SDT_GLOAD
 #undef SDT_SSTORE
+  tacc = (t4[0] + t4[1]) + (t4[2] + t4[3]);
   // fragment (R, c) of tile t -> 64-block (2t + R/4, 2t + c/4) of the slab
 #pragma unroll
   for (int c = 0; c < N1; ++c)
@@ -230,20 +260,41 @@ __device__ __forceinline__ void syrk_dt_body(const double* __restrict__ K, int64
     }
 }
 
-template <int WMODE>
+// slab_t / slab_rr: split sd's [nb][128] t partials and its rr partial (TMODE != 0)
+template <int WMODE, int TMODE>
 __device__ __forceinline__ void syrk_dtile(const double* __restrict__ K, int64_t n_pad,
-                                           int64_t mp, const double* __restrict__ w, int t,
+                                           int64_t mp, const double* __restrict__ w,
+                                           const double* __restrict__ r,
+                                           const double* __restrict__ tv, int t, int nb,
                                            int64_t sd, int64_t chunk, double (*Ka)[BK * SB],
-                                           double (*ws)[BK], double* __restrict__ out) {
+                                           double (*ws)[BK], double (*rw)[BK],
+                                           double* __restrict__ out,
+                                           double* __restrict__ slab_t,
+                                           double* __restrict__ slab_rr) {
   const int64_t rbeg = sd * chunk;
   int64_t rend = rbeg + chunk;
   if (rend > n_pad) rend = n_pad;
   const int nsteps = rend > rbeg ? (int)((rend - rbeg) / BK) : 0;
+  double tacc = 0.0, rrp = 0.0;
   switch (threadIdx.x >> 6) {   // wave-uniform
-    case 0: syrk_dt_body<0, WMODE>(K, mp, w, t, rbeg, nsteps, Ka, ws, out); break;
-    case 1: syrk_dt_body<1, WMODE>(K, mp, w, t, rbeg, nsteps, Ka, ws, out); break;
-    case 2: syrk_dt_body<2, WMODE>(K, mp, w, t, rbeg, nsteps, Ka, ws, out); break;
-    default: syrk_dt_body<3, WMODE>(K, mp, w, t, rbeg, nsteps, Ka, ws, out); break;
+    case 0: syrk_dt_body<0, WMODE, TMODE>(K, mp, w, r, tv, t, rbeg, nsteps, Ka, ws, rw, tacc, rrp, out); break;
+    case 1: syrk_dt_body<1, WMODE, TMODE>(K, mp, w, r, tv, t, rbeg, nsteps, Ka, ws, rw, tacc, rrp, out); break;
+    case 2: syrk_dt_body<2, WMODE, TMODE>(K, mp, w, r, tv, t, rbeg, nsteps, Ka, ws, rw, tacc, rrp, out); break;
+    default: syrk_dt_body<3, WMODE, TMODE>(K, mp, w, r, tv, t, rbeg, nsteps, Ka, ws, rw, tacc, rrp, out); break;
+  }
+  if constexpr (TMODE != 0) {
+    // the two row halves of each column, then rr from the BK staging lanes of tile 0
+    const int tid = threadIdx.x;
+    double* tsh = &Ka[0][0];   // every wave is past its last read of the images
+    tsh[tid] = tacc;
+    __syncthreads();
+    if (tid < T128) slab_t[(sd * nb + t) * T128 + tid] = tsh[tid] + tsh[tid + T128];
+    if (t == 0 && tid < 64) {
+      double v = tid < BK ? rrp : 0.0;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (tid == 0) slab_rr[sd] = v;
+    }
   }
 }
 
@@ -267,14 +318,16 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
   __shared__ double ws[2][BK];
   __shared__ double rw[2][BK];   // with_t: (w r)_i or tv_i of the step's rows
 
-  // the balanced S-only plan's diagonal-tile workgroups follow the packed groups' grid
-  if constexpr (TMODE == 0) {
+  // the balanced plan's diagonal-tile workgroups follow the packed groups' grid (with t: they
+  // form it, the off-diagonal groups of WMODE 3 carry none)
+  if constexpr (TMODE == 0 || WMODE == 3) {
     if ((int64_t)blockIdx.x >= nwg_blk) {
       const int64_t loc = (int64_t)blockIdx.x - nwg_blk;
       const int t = (int)(loc % nb);
       const int64_t sd = loc / nb;
-      syrk_dtile<WMODE>(K, n_pad, mp, w, t, sd, chunk_d, Ka, ws,
-                        slab_d + sd * ((int64_t)(2 * nb) * (2 * nb + 1) / 2) * 4096);
+      syrk_dtile<WMODE == 3 ? 1 : WMODE, TMODE>(
+          K, n_pad, mp, w, r, tv, t, nb, sd, chunk_d, Ka, ws, rw,
+          slab_d + sd * ((int64_t)(2 * nb) * (2 * nb + 1) / 2) * 4096, slab_t, slab_rr);
       return;
     }
   }
@@ -290,9 +343,12 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
   // (c_tmap); rr from diagonal group 0.
   const int64_t noff = (int64_t)nb * (nb - 1) / 2;
   const int dg = (gi >= noff) ? (int)(gi - noff) : -1;
-  constexpr bool WITH_T = TMODE != 0;
+  constexpr bool WITH_T = TMODE != 0 && WMODE != 3;   // WMODE 3: t on the diagonal tiles
   constexpr bool with_t = WITH_T;
   static_assert(!(WMODE == 2 && TMODE != 0), "sqrt(w)-scaled images: S only");
+  // WMODE 3 (balanced plan only, every group off-diagonal: rows from image A, columns from
+  // image B): image A staged as w o K, image B as K -- no per-fragment weight, any sign
+  constexpr bool SCALE_A = WMODE == 2 || WMODE == 3, SCALE_B = WMODE == 2;
   // tm.S == 0 (more groups than the table holds, m > 1920): one whole-panel slice per panel,
   // panel a >= 1 on the strictly-lower group (a, 0) and panel 0 on diagonal group 0 -- distinct
   // groups, each holding its panel as image A
@@ -346,7 +402,7 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
     /* one block: every lane stages row tid % BK (16 lanes per row) */          \
     const int64_t rr_ = rbeg + (int64_t)(step) * BK + (tid & (BK - 1));        \
     if constexpr (WMODE == 1) vw = w[rr_];                                      \
-    if constexpr (WMODE == 2) vsa = w[rbeg + (int64_t)(step) * BK + lrow];      \
+    if constexpr (SCALE_A) vsa = w[rbeg + (int64_t)(step) * BK + lrow];        \
     if constexpr (WITH_T) {                                                     \
       vrr = r[rr_];                                                             \
       if constexpr (has_tv) vr = tv[rr_];                                       \
@@ -358,9 +414,11 @@ k_syrk_blk(const double* __restrict__ K, int64_t n_pad, int64_t mp, const double
   {                                                                             \
     double2* pa_ = reinterpret_cast<double2*>(&Ka[buf][lrow * SB]) + lc;        \
     double2* pb_ = reinterpret_cast<double2*>(&Kb[buf][lrow * SB]) + lc;        \
-    if constexpr (WMODE == 2) {                    /* sqrt(w) K in both images */ \
+    if constexpr (SCALE_A) {             /* sqrt(w) K (WMODE 2) or w o K (3) */ \
       va0.x *= vsa; va0.y *= vsa; va1.x *= vsa; va1.y *= vsa;                   \
       va2.x *= vsa; va2.y *= vsa; va3.x *= vsa; va3.y *= vsa;                   \
+    }                                                                           \
+    if constexpr (SCALE_B) {                                                    \
       vb0.x *= vsa; vb0.y *= vsa; vb1.x *= vsa; vb1.y *= vsa;                   \
       vb2.x *= vsa; vb2.y *= vsa; vb3.x *= vsa; vb3.y *= vsa;                   \
     }                                                                           \
@@ -1613,19 +1671,27 @@ SyrkPlan syrk_plan_blk(int64_t n_pad, int64_t mp) {
   return p;
 }
 
-// Balanced S-only plan (nb >= 3): the strictly-lower 128-tiles as k_syrk_blk's packed groups
-// with S_o row chunks (64 MFMAs per wave-step), the nb diagonal 128-tiles as syrk_dtile
-// workgroups with S_d longer chunks (36 MFMAs per wave-step, no redundant upper fragments), one
-// residency round between them.  Used when its makespan, max(64 chunk_o, 36 chunk_d), beats the
-// packed plan's 64 chunk by more than 2 % (C5's m = 512: 1.143 -> 1.049 n in units of
-// MFMA-steps per row; at m = 1024 the round's integer split counts leave no gain).
+// Balanced plan (nb >= 3): the strictly-lower 128-tiles as k_syrk_blk's packed groups with S_o
+// row chunks (64 MFMAs per wave-step), the nb diagonal 128-tiles as syrk_dtile workgroups with
+// S_d longer chunks (36 MFMAs per wave-step, no redundant upper fragments), one residency round
+// between them.  wd: a diagonal-tile wave-step's cost in MFMA slots (36 issued, plus the
+// per-fragment weights and the t slice where they apply).  Unweighted or sqrt(w)-staged S:
+// used when its makespan, max(64 chunk_o, wd chunk_d), beats the packed plan's 64 chunk by
+// more than 2 % (C5's m = 512: 1.143 -> 1.049 n MFMA-steps per row; at m = 1024 the round's
+// integer split counts leave no gain).  force (signed weights or t, WMODE 3): always -- there
+// it moves the per-fragment weights and the t slice off the off-diagonal groups.
 struct SyrkBal {
   bool on = false;
   int S_o = 0, S_d = 0;
   int64_t chunk_o = 0, chunk_d = 0;
 };
 
-static SyrkBal syrk_plan_bal(int64_t n_pad, int64_t mp) {
+static double syrk_dtile_cost(bool weighted, bool with_t) {
+  return (double)SGP_SDT_W + (weighted ? (double)SGP_SDT_WW : 0.0) +
+         (with_t ? (double)SGP_SDT_WT : 0.0);
+}
+
+static SyrkBal syrk_plan_bal(int64_t n_pad, int64_t mp, double wd, bool force) {
   SyrkBal b;
   const int nb = (int)(mp / T128);
   if (nb < 3 || !SGP_SYRK_BAL) return b;
@@ -1642,7 +1708,7 @@ static SyrkBal syrk_plan_bal(int64_t n_pad, int64_t mp) {
     if (Sd < 1) break;
     if (Sd > max_splits) Sd = max_splits;
     const int64_t co = chunk_of(So), cd = chunk_of(Sd);
-    const double T = std::max(64.0 * (double)co, (double)SGP_SDT_W * (double)cd);
+    const double T = std::max(64.0 * (double)co, wd * (double)cd);
     if (!b.on || T < best) {
       b.on = true;
       best = T;
@@ -1652,7 +1718,7 @@ static SyrkBal syrk_plan_bal(int64_t n_pad, int64_t mp) {
       b.S_d = (int)((n_pad + cd - 1) / cd);
     }
   }
-  if (!b.on) return b;
+  if (!b.on || force) return b;
   // the packed plan: one or more rounds of equal workgroups
   const SyrkPlan q = syrk_plan_blk(n_pad, mp);
   const int64_t rounds = ((int64_t)q.splits * q.T + kSlots - 1) / kSlots;
@@ -1690,10 +1756,13 @@ int64_t syrk_slab_doubles_mp(int64_t n_pad, int64_t mp) {
   const int64_t nblk = (int64_t)(2 * q.nb) * (2 * q.nb + 1) / 2;
   int64_t need = (int64_t)q.splits * nblk * 4096 + (int64_t)q.splits * q.nb * T128 + q.splits +
                  n_pad;   // + the sqrt(w) rows of WMODE 2
-  const SyrkBal bal = syrk_plan_bal(n_pad, mp);
-  if (bal.on)
-    need = std::max(need, (int64_t)(bal.S_o + bal.S_d) * nblk * 4096 +
-                              (int64_t)bal.S_o * (q.nb * T128 + 1) + n_pad);
+  // every balanced plan launch_syrk_aug may pick (its split counts depend on the weights / t)
+  for (int v = 0; v < 3; ++v) {   // unweighted / sqrt(w); signed weights; weights and t
+    const SyrkBal bal = syrk_plan_bal(n_pad, mp, syrk_dtile_cost(v > 0, v > 1), v > 0);
+    if (bal.on)
+      need = std::max(need, (int64_t)(bal.S_o + bal.S_d) * nblk * 4096 +
+                                (int64_t)std::max(bal.S_o, bal.S_d) * (q.nb * T128 + 1) + n_pad);
+  }
   if (mp == 256) {
     SyrkPlan r = syrk_plan_s256(n_pad);
     need = std::max(need, (int64_t)r.splits * (10 * 4096 + 2 * T128 + 1) + n_pad);   // as laid out
@@ -1719,8 +1788,16 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
       // fragment-balanced k_syrk_s256 (same slab layout and reduction)
     const bool s256 = syrk_use_s256(mp, with_t != 0);
     SyrkPlan q = s256 ? syrk_plan_s256(n_pad) : syrk_plan_blk(n_pad, mp);
-    // S only at nb >= 3: the balanced plan when it beats the packed one (syrk_plan_bal)
-    const SyrkBal bal = (!s256 && !with_t) ? syrk_plan_bal(n_pad, mp) : SyrkBal{};
+    // nb >= 3: signed weights or t -> WMODE 3 on the balanced plan (the off-diagonal groups
+    // stage w o K as their A image and carry no t; the diagonal tiles keep the per-fragment
+    // weights and form t); unweighted or sqrt(w)-staged S -> the balanced plan when it beats
+    // the packed one (syrk_plan_bal)
+    const bool wsq = w && w_nonneg && !with_t;
+    const bool use3 = !s256 && w && !wsq && SGP_SYRK_W3 && q.nb >= 3;
+    SyrkBal bal;
+    if (use3) bal = syrk_plan_bal(n_pad, mp, syrk_dtile_cost(true, with_t != 0), true);
+    else if (!s256 && !with_t) bal = syrk_plan_bal(n_pad, mp, syrk_dtile_cost(false, false), false);
+    if (use3 && !bal.on) return hipErrorInvalidValue;
     if (bal.on) {
       q.T = q.nb * (q.nb - 1) / 2;   // the packed kernel's strictly-lower groups only
       q.splits = bal.S_o;
@@ -1730,8 +1807,10 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
     double* sl_s = slab;
     double* sl_d = sl_s + (int64_t)q.splits * nblk * 4096;   // the diagonal tiles' region
     double* sl_t = sl_d + (bal.on ? (int64_t)bal.S_d * nblk * 4096 : 0);
-    double* sl_rr = sl_t + (int64_t)q.splits * q.nb * T128;
-    if (sl_rr + q.splits + n_pad > slab + slab_cap) return hipErrorInvalidValue;   // + sqrt(w)
+    // t partials: per row chunk of whichever workgroups form t (WMODE 3: the diagonal tiles)
+    const int t_splits = use3 ? bal.S_d : q.splits;
+    double* sl_rr = sl_t + (int64_t)t_splits * q.nb * T128;
+    if (sl_rr + t_splits + n_pad > slab + slab_cap) return hipErrorInvalidValue;   // + sqrt(w)
     const int64_t nwg_blk = (int64_t)q.splits * q.T;
     const dim3 grid((unsigned)(nwg_blk + (bal.on ? (int64_t)bal.S_d * q.nb : 0)));
     SyrkTMap tm{};
@@ -1759,10 +1838,9 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
       // non-negative weights without t: their square roots scale the staged images (with t
       // the extra staging work made FITC's phase-1 SYRK 4.6 % slower, 17.66 -> 18.47 ms at
       // C3, against 2.7 % faster NR objectives at C5: profiles/r4/syrk_sqrt_rows_ab.txt)
-      const bool wsq = w && w_nonneg && !with_t;
       const double* wk = w;
       if (wsq) {
-        double* sw = sl_rr + q.splits;   // n_pad doubles past the partial sums
+        double* sw = sl_rr + t_splits;   // n_pad doubles past the partial sums
         hipLaunchKernelGGL(k_sqrt_rows, dim3((unsigned)((n_pad + 255) / 256)), dim3(256), 0, s,
                            w, n_pad, sw);
         wk = sw;
@@ -1770,7 +1848,11 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
 #define SYRK_T_LAUNCH(tmode_, wmode_, tr_)                                                     \
   hipLaunchKernelGGL((k_syrk_blk<tmode_, wmode_, tr_>), grid, dim3(256), 0, s, K, n_pad, mp, wk, \
                      r, tv, q.chunk, q.T, q.nb, sl_s, sl_t, sl_rr, tm, nwg_blk, bal.chunk_d, sl_d)
-      if (with_t && tv) {
+      if (use3) {
+        if (with_t && tv) SYRK_T_LAUNCH(2, 3, 2);
+        else if (with_t) SYRK_T_LAUNCH(1, 3, 2);
+        else SYRK_T_LAUNCH(0, 3, 2);
+      } else if (with_t && tv) {
         if (tr == 2) SYRK_T_LAUNCH(2, 1, 2);
         else if (tr == 4) SYRK_T_LAUNCH(2, 1, 4);
         else SYRK_T_LAUNCH(2, 1, 8);
@@ -1809,7 +1891,7 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
                          bal.on ? sl_d : nullptr, bal.S_d, stride_d);
       if (with_t)
         hipLaunchKernelGGL(k_syrk_reduce_t, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s,
-                           sl_t, sl_rr, q.splits, q.nb, mp, red);
+                           sl_t, sl_rr, t_splits, q.nb, mp, red);
     }
     return hipGetLastError();
   }

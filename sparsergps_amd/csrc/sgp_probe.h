@@ -21,6 +21,9 @@
 //   SGP_SYRK_BAL        0: no balanced S-only SYRK plan (syrk_plan_bal)
 //   SGP_SDT_IL          0: the diagonal-tile SYRK step without the interleave request
 //   SGP_SDT_W           syrk_plan_bal's cost of a diagonal-tile wave-step, in MFMAs (36 issued)
+//   SGP_SDT_WW          ... plus this with per-fragment weights
+//   SGP_SDT_WT          ... plus this with the t slice
+//   SGP_SYRK_W3         0: signed-weight / t SYRKs keep per-fragment weights on the packed plan
 //   SGP_S256_IL         1: k_syrk_s256's step with an interleave request
 #pragma once
 
@@ -28,7 +31,8 @@
      defined(SGP_IL_VMEM0) || defined(SGP_CON_IL_PAT) || defined(SGP_SYRK_IL_PAT) ||          \
      defined(SGP_CON_IL_SPREAD) || defined(SGP_CON_SHMEM) || defined(SGP_NRA_LDS) ||          \
      defined(SGP_SYRK_BAL) || defined(SGP_SDT_IL) || defined(SGP_S256_IL) ||                  \
-     defined(SGP_SDT_W)) &&                                                                   \
+     defined(SGP_SDT_W) || defined(SGP_SDT_WW) || defined(SGP_SDT_WT) ||                      \
+     defined(SGP_SYRK_W3)) &&                                                                 \
     !defined(SGP_PROBE_BUILD)
 #error "timing probes and experiment knobs are for variant builds only (SGP_PROBE_BUILD)"
 #endif
@@ -59,6 +63,15 @@
 #endif
 #ifndef SGP_SDT_W
 #define SGP_SDT_W 38
+#endif
+#ifndef SGP_SDT_WW
+#define SGP_SDT_WW 2
+#endif
+#ifndef SGP_SDT_WT
+#define SGP_SDT_WT 6
+#endif
+#ifndef SGP_SYRK_W3
+#define SGP_SYRK_W3 1
 #endif
 #ifndef SGP_S256_IL
 #define SGP_S256_IL 0
