@@ -1,4 +1,4 @@
-"""Row-chunked CPU model of the VI adjoint evaluation -- TEST INFRASTRUCTURE ONLY.
+"""Row-chunked CPU models of the VI, FITC and Laplace adjoint evaluations -- TEST INFRASTRUCTURE ONLY.
 
 The same algebra as ``adjoint_ref.NumpyVIRank`` (which mirrors sgp_vi_phase1/2/finish,
 DESIGN.md sec. 3.1), restated so that its memory is O(chunk * m) instead of O(n * m * d):
@@ -153,6 +153,114 @@ def eval_vi(kernel, theta, X, y, mu, U, delta=1e-6, chunk=8192, n_global=None):
     grad[0] = 2 * e_sig + g22[0] - nn * sig2 / tau2
     grad[1:L + 1] = e_l + np.asarray(g22[1:])
     grad[L + 1] = 2 * tau2 * (c_sum - (c_cnt - delta * c_dg) / tau2) + 2 * tau2 * trW - 2 * T
+    return obj, grad
+
+
+# -------------------------------------------------------------------------------- FITC model
+def eval_fitc(kernel, theta, X, y, mu, U, delta=1e-6, chunk=8192):
+    """FITC objective + d/d log theta with O(chunk * m) memory: the algebra of
+    ``adjoint_ref.eval_fitc`` (which mirrors sgp_fitc_phase1 / phase2 / finish, DESIGN.md
+    sec. 3.2), K12 rebuilt per row chunk in both passes.  References: obj_fun_norm
+    R/laplace_approx_obj_funs.R:6 (on the FITC Z), dlogp_dcov_par
+    R/laplace_approx_gradient.R:720-971.
+
+      pass 1   q_i = k_i^T K22^-1 k_i, Z = sig2 + tau2 + delta - q, w = 1/Z;
+               S += K^T diag(w) K, t += K^T (w r), r^T diag(w) r, sum log Z
+      m x m    Bm = K22 + S, u = Bm^-1 t
+      pass 2   alpha = w (r - K u), p_i = k_i^T Bm^-1 k_i, omega = alpha^2 - (w - w^2 p);
+               S_omega += K^T diag(omega) K, sum omega;
+               G = alpha u^T - diag(w) K Bm^-1 - diag(omega) K K22^-1 contracted with dK/dlog theta
+    Returns (objective, gradient in [sigma, l.., tau] order)."""
+    X = np.asarray(X, dtype=np.float64)
+    U = np.asarray(U, dtype=np.float64)
+    n, d = X.shape
+    m = U.shape[0]
+    r = np.asarray(y, dtype=np.float64) - np.asarray(mu, dtype=np.float64)
+    L, sigma, tau, ls = _params(kernel, theta, d)
+    sig2, tau2 = sigma * sigma, tau * tau
+    center = U.mean(axis=0)
+    Us = _scaled(kernel, U, center, ls)
+    u2 = np.einsum("ij,ij->i", Us, Us)
+    buf = np.empty((min(chunk, n), m))
+    Kuu, dU = _kmat(kernel, U, U, sigma, ls)
+    K22 = Kuu.copy()
+    K22[np.diag_indices(m)] = ((np.diag(Kuu) + tau2) + delta) - tau2
+    K22inv = np.linalg.inv(K22)
+
+    def chunks():
+        for s0 in range(0, n, chunk):
+            s1 = min(n, s0 + chunk)
+            Xs = _scaled(kernel, X[s0:s1], center, ls)
+            x2 = np.einsum("ij,ij->i", Xs, Xs)
+            yield s0, s1, Xs, x2, _kblock(Xs, x2, Us, u2, sig2, out=buf[:s1 - s0])
+
+    # ---- pass 1
+    w = np.empty(n)
+    S = np.zeros((m, m))
+    t = np.zeros(m)
+    rr = 0.0
+    slz = 0.0
+    for s0, s1, _, _, K in chunks():
+        sl = slice(s0, s1)
+        Z = sig2 + tau2 + delta - np.einsum("ij,ij->i", K, K @ K22inv)
+        w[sl] = 1.0 / Z
+        S += K.T @ (w[sl][:, None] * K)
+        wr = w[sl] * r[sl]
+        t += K.T @ wr
+        rr += float(r[sl] @ wr)
+        slz += float(np.sum(np.log(Z)))
+    Bm = K22 + S
+    Binv = np.linalg.inv(Bm)
+    u = Binv @ t
+    ld22 = np.linalg.slogdet(K22)[1]
+    ldB = np.linalg.slogdet(Bm)[1]
+    obj = -0.5 * rr + 0.5 * t @ u - 0.5 * (slz - ld22 + ldB) - n / 2 * math.log(2 * math.pi)
+
+    # ---- pass 2
+    Som = np.zeros((m, m))
+    som = 0.0
+    e_sig = 0.0
+    e_l = np.zeros(L)
+    c_sum = 0.0
+    ukeys = _row_keys(U)
+    usorted = ukeys[np.argsort(ukeys)]
+    for s0, s1, Xs, x2, K in chunks():
+        sl = slice(s0, s1)
+        wc = w[sl]
+        alpha = wc * (r[sl] - K @ u)
+        KB = K @ Binv
+        p = np.einsum("ij,ij->i", K, KB)
+        omega = alpha ** 2 - (wc - wc * wc * p)
+        Som += K.T @ (omega[:, None] * K)
+        som += float(omega.sum())
+        G = np.outer(alpha, u)
+        G -= wc[:, None] * KB
+        G -= omega[:, None] * (K @ K22inv)
+        keys = _row_keys(X[s0:s1])
+        pos = np.searchsorted(usorted, keys)
+        pos[pos >= m] = m - 1
+        for i in np.nonzero(usorted[pos] == keys)[0]:
+            for j in np.nonzero(ukeys == keys[i])[0]:
+                c_sum += G[i, j]
+        G *= K                                                       # W = G o K
+        rs = G.sum(axis=1)
+        cs = G.sum(axis=0)
+        e_sig += float(rs.sum())
+        XW = Xs.T @ G
+        if kernel == "sqexp":
+            e_l[0] += float(x2 @ rs - 2.0 * np.sum(XW * Us.T) + cs @ u2)
+        else:
+            e_l += (Xs * Xs).T @ rs - 2.0 * np.sum(XW * Us.T, axis=1) + (Us * Us).T @ cs
+
+    G22 = -0.5 * np.outer(u, u) + 0.5 * (K22inv - Binv) + 0.5 * K22inv @ Som @ K22inv
+    grad = np.zeros(L + 2)
+    grad[0] = 2 * e_sig + np.sum(G22 * 2 * Kuu) + sig2 * som
+    if kernel == "sqexp":
+        grad[1] = e_l[0] + np.sum(G22 * Kuu * np.sum(dU ** 2, axis=2)) / ls[0] ** 2
+    else:
+        for c in range(L):
+            grad[1 + c] = e_l[c] + np.sum(G22 * Kuu * (dU[:, :, c] / ls[c]) ** 2)
+    grad[L + 1] = 2 * tau2 * c_sum + tau2 * som
     return obj, grad
 
 

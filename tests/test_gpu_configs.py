@@ -9,7 +9,8 @@
 * C2 (configs[1]: sqexp, d = 3) at its own m = 256 and C5 (configs[4]: Poisson, d = 5) at
   its own m = 512 -- from the fixtures at n = 2000 (literal oracle) and at larger n against
   the adjoint models (C2 at its full n = 1e5 against oracle/adjoint_chunked.py; C5 at
-  n = 40 000 against oracle/adjoint_ref.py, whose n x m x d tensors bound n).
+  n = 40 000 against oracle/adjoint_ref.py and at 5e5 against adjoint_chunked; FITC at the
+  C3 shape against adjoint_chunked.eval_fitc).
 """
 import glob
 import os
@@ -166,5 +167,22 @@ def test_c3_headline_shape_against_chunked_adjoint_model(sgp):
     th = np.array(list(P["cov_par"].values()))
     obj, grad = sgp.vi_eval(P["cov_par"], "ard", P["U"], P["X"], P["y"], P["mu"], P["delta"])
     o, g = AC.eval_vi("ard", th, P["X"], P["y"], P["mu"], P["U"], P["delta"])
+    assert abs(obj - o) / abs(o) < 1e-9
+    assert _rel(list(grad.values()), g) < 1e-7
+
+
+def test_fitc_headline_shape_against_chunked_fitc_model(sgp):
+    """The FITC bench workload (--mode fitc: configs[2]'s n = 1e6, m = 1024, d = 8, ARD) against
+    the row-chunked CPU model (oracle/adjoint_chunked.eval_fitc, pinned to the literal
+    obj_fun_norm + dlogp_dcov_par in tests/test_oracle.py; ~30 s of host BLAS).  Exercises the
+    t-carrying and signed-weight SYRKs on the balanced plan at their production split counts.
+    Reference: R/laplace_approx_obj_funs.R:6, R/laplace_approx_gradient.R:720-971."""
+    from oracle import adjoint_chunked as AC
+    from sparsergps_amd.workloads import make_gaussian_problem
+    P = make_gaussian_problem("C3")
+    assert P["X"].shape == (1_000_000, 8) and P["U"].shape == (1024, 8)
+    th = np.array(list(P["cov_par"].values()))
+    obj, grad = sgp.fitc_eval(P["cov_par"], "ard", P["U"], P["X"], P["y"], P["mu"], P["delta"])
+    o, g = AC.eval_fitc("ard", th, P["X"], P["y"], P["mu"], P["U"], P["delta"])
     assert abs(obj - o) / abs(o) < 1e-9
     assert _rel(list(grad.values()), g) < 1e-7

@@ -342,3 +342,24 @@ def test_full_gp_gradient_is_the_objective_derivative_at_zero_mean():
     Si = np.linalg.inv(S)
     extra = 2 * 0.4 ** 2 * (al[5] * al[9] - Si[5, 9])      # (1/2) * 2 entries (5,9), (9,5)
     assert abs(g["tau"] - (fd + extra)) < 1e-6 * abs(fd)
+
+
+@pytest.mark.parametrize("cov_fun,coinc", [("sqexp", False), ("ard", True)])
+def test_chunked_fitc_model_matches_literal(cov_fun, coinc):
+    """oracle/adjoint_chunked.eval_fitc (the full-size FITC checker) equals the literal
+    obj_fun_norm on the FITC Z and dlogp_dcov_par (R/laplace_approx_obj_funs.R:6,
+    R/laplace_approx_gradient.R:720-971); chunk < n exercises the row-chunk loop and the
+    coincidence matching."""
+    from oracle import adjoint_chunked as AC
+    P = O.make_gaussian_problem("C3" if cov_fun == "ard" else "C2", n=301, m=17)
+    U = P["U"].copy()
+    if coinc:
+        U[:3] = P["X"][[0, 150, 300]]
+    cp = P["cov_par"]
+    o = O.fitc_obj_eval(cp, cov_fun, U, P["X"], P["y"], P["mu"], P["delta"])
+    g = O.dlogp_dcov_par(cp, cov_fun, U, P["X"], P["y"], P["mu"], P["delta"])["gradient"]
+    obj, grad = AC.eval_fitc(cov_fun, np.array(list(cp.values())), P["X"], P["y"], P["mu"], U,
+                             P["delta"], chunk=64)
+    gv = np.array(list(g.values()))
+    assert abs(obj - o) / abs(o) < 1e-11
+    assert np.max(np.abs(grad - gv) / np.maximum(1, np.abs(gv))) < 1e-10
