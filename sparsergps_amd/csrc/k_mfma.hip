@@ -859,7 +859,8 @@ k_syrk_reduce_t(const double* __restrict__ slab_t, const double* __restrict__ sl
 // staged K values (iz_i = invz_vec ? invz_vec[i] : invz), optionally written to alpha_out.
 enum { EPI_GRAD = 0, EPI_ROWQUAD = 1 };
 
-template <int DT, int EPI, bool V2 = false, bool KNOT = false, bool FROM_T = false>
+// KU (row quadratic forms without u: the Z pass): false compiles the K u fold out of the k-loop
+template <int DT, int EPI, bool V2 = false, bool KNOT = false, bool FROM_T = false, bool KU = true>
 __global__ void __launch_bounds__(256, 2)
 k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict__ M,
            const double* __restrict__ X, int64_t ldx, int64_t n, int64_t n_pad,
@@ -882,7 +883,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wr = wv >> 1, wc = wv & 1;
-  const bool with_u = (uvec != nullptr) && (ca.alpha_in == nullptr);   // fuse K u into the loop
+  const bool with_u = KU && (uvec != nullptr) && (ca.alpha_in == nullptr);   // fuse K u into the loop
   constexpr bool with_v = V2;   // second rank-1 term (Laplace), compiled in only where used
 
   d4 acc[4][4];
@@ -915,7 +916,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     const int64_t oa_ = (int64_t)(step) * (BK / 2), ob_ = (int64_t)(step) * bstep; \
     va0 = gA[oa_]; va1 = gA[oa_ + 1]; va2 = gA[oa_ + 2]; va3 = gA[oa_ + 3];      \
     vb0 = gB[ob_]; vb1 = gB[ob_ + 16]; vb2 = gB[ob_ + 32]; vb3 = gB[ob_ + 48];   \
-    vuk = uk_src[(int64_t)(step) * BK + (tid & (BK - 1))];                       \
+    if constexpr (KU) vuk = uk_src[(int64_t)(step) * BK + (tid & (BK - 1))];     \
   }
 #define CON_SSTORE(buf)                                                          \
   {                                                                              \
@@ -925,7 +926,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     pa_[0] = va0.x; pa_[1] = va0.y; pa_[2] = va1.x; pa_[3] = va1.y;              \
     pa_[4] = va2.x; pa_[5] = va2.y; pa_[6] = va3.x; pa_[7] = va3.y;              \
     pb_[0] = vb0; pb_[16] = vb1; pb_[32] = vb2; pb_[48] = vb3;                   \
-    s_uk[buf][tid & (BK - 1)] = vuk;   /* 16 lanes per address, one value */     \
+    if constexpr (KU) s_uk[buf][tid & (BK - 1)] = vuk;   /* 16 lanes per address */ \
   }
 #define CON_KU(buf)                                                              \
   {                                                                              \
@@ -954,7 +955,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   __syncthreads();
   for (int step = 0; step < nsteps; ++step) {
     const int cur = step & 1;
-    CON_KU(cur);   // va still holds this step's staged K values
+    if constexpr (KU) CON_KU(cur);   // va still holds this step's staged K values
     CON_GLOAD(step + 1 < nsteps ? step + 1 : step);   // the last step reloads its own slice
     const double* As = lds + cur * (A_SZ + B_SZ);
     const double* Bs = As + A_SZ;
@@ -2087,9 +2088,15 @@ hipError_t launch_rowquad_knm(const KernParams& kp, const double* K, const doubl
   ca.uvec = uvec;
   ca.alpha_out = alpha_out;
   ca.tstore = tstore;
-  hipLaunchKernelGGL((k_contract<8, EPI_ROWQUAD>), dim3((unsigned)nwg), dim3(256), 0, s, kp, K, M,
-                     (const double*)nullptr, (int64_t)0, n, n_pad, (const double*)nullptr,
-                     (int64_t)0, m, mp, ca, (double*)nullptr, 0, rowq_slab);
+  if (uvec != nullptr || SGP_CON_ROWQ_KU)
+    hipLaunchKernelGGL((k_contract<8, EPI_ROWQUAD>), dim3((unsigned)nwg), dim3(256), 0, s, kp, K, M,
+                       (const double*)nullptr, (int64_t)0, n, n_pad, (const double*)nullptr,
+                       (int64_t)0, m, mp, ca, (double*)nullptr, 0, rowq_slab);
+  else   // the Z pass: no K u fold in the k-loop
+    hipLaunchKernelGGL((k_contract<8, EPI_ROWQUAD, false, false, false, false>),
+                       dim3((unsigned)nwg), dim3(256), 0, s, kp, K, M, (const double*)nullptr,
+                       (int64_t)0, n, n_pad, (const double*)nullptr, (int64_t)0, m, mp, ca,
+                       (double*)nullptr, 0, rowq_slab);
   hipLaunchKernelGGL(k_rowq_reduce, dim3((unsigned)((n_pad + 255) / 256)), dim3(256), 0, s,
                      rowq_slab, mp / T128, n_pad, out);
   return hipGetLastError();

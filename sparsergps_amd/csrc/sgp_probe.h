@@ -24,6 +24,7 @@
 //   SGP_SDT_WW          ... plus this with per-fragment weights
 //   SGP_SDT_WT          ... plus this with the t slice
 //   SGP_SYRK_W3         0: signed-weight / t SYRKs keep per-fragment weights on the packed plan
+//   SGP_CON_ROWQ_KU     1: the row-quadratic pass without u keeps the (unused) K u fold
 //   SGP_S256_IL         1: k_syrk_s256's step with an interleave request
 #pragma once
 
@@ -32,7 +33,7 @@
      defined(SGP_CON_IL_SPREAD) || defined(SGP_CON_SHMEM) || defined(SGP_NRA_LDS) ||          \
      defined(SGP_SYRK_BAL) || defined(SGP_SDT_IL) || defined(SGP_S256_IL) ||                  \
      defined(SGP_SDT_W) || defined(SGP_SDT_WW) || defined(SGP_SDT_WT) ||                      \
-     defined(SGP_SYRK_W3)) &&                                                                 \
+     defined(SGP_SYRK_W3) || defined(SGP_CON_ROWQ_KU)) &&                                     \
     !defined(SGP_PROBE_BUILD)
 #error "timing probes and experiment knobs are for variant builds only (SGP_PROBE_BUILD)"
 #endif
@@ -72,6 +73,9 @@
 #endif
 #ifndef SGP_SYRK_W3
 #define SGP_SYRK_W3 1
+#endif
+#ifndef SGP_CON_ROWQ_KU
+#define SGP_CON_ROWQ_KU 0
 #endif
 #ifndef SGP_S256_IL
 #define SGP_S256_IL 0
