@@ -475,6 +475,119 @@ __global__ void __launch_bounds__(256) k_lap_rowpass(const double* __restrict__ 
   if (tid < NS) pa.sc[ch * NS + tid] = s_red[0][tid] + s_red[1][tid] + s_red[2][tid] + s_red[3][tid];
 }
 
+// The same two Newton-step passes without the LDS row image: each wave streams its rows
+// straight into registers (lane l holds columns 2l + 128q, 2l + 128q + 1 of RF rows at a time),
+// forms d_i = K_i x with its lanes' x slice and one wave reduction per row, applies the row
+// update (every lane; lane 0 stores), and folds v_i K_i into its lanes' column sums from the same
+// registers -- no barrier inside the row loop, and 16 waves per CU keep the loads of 64 rows in
+// flight (the LDS-image form stalls a workgroup on each 64 KB block: 4.9 TB/s at C5).  The four
+// waves' column sums are combined in fixed order at the end.  NQM: double2 columns per lane per
+// row (mp / 128 rounded up to 2, 4, 8 or 16), RF rows in flight per wave, OCC waves per SIMD.
+template <int MODE, int NQM, int RF, int OCC>
+__global__ void __launch_bounds__(256, OCC) k_lap_rowstream(const double* __restrict__ K, int64_t n,
+                                                            int64_t n_pad, int64_t mp,
+                                                            int64_t chunk, LapPassArgs pa) {
+  extern __shared__ __attribute__((aligned(16))) double s_part[];   // [4][mp]
+  __shared__ double s_red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nq = (int)(mp / 128);
+  const int64_t ch = blockIdx.x;
+  const int64_t i0 = ch * chunk;
+  const int64_t i1 = (i0 + chunk < n_pad) ? i0 + chunk : n_pad;
+  const double2* K2 = reinterpret_cast<const double2*>(K);
+  const double2* x2 = reinterpret_cast<const double2*>(pa.x);
+  const int64_t mp2 = mp / 2;
+  double2 xr[NQM], acc[NQM];
+#pragma unroll
+  for (int q = 0; q < NQM; ++q) {
+    xr[q] = (q < nq) ? x2[lane + 64 * q] : make_double2(0.0, 0.0);
+    acc[q] = make_double2(0.0, 0.0);
+  }
+  double sc = 0.0;   // the pass's scalar sum over the rows this lane updated
+  for (int64_t g0 = i0 + (int64_t)wv * RF; g0 < i1; g0 += 4 * RF) {
+    double2 kr[RF][NQM];
+#pragma unroll
+    for (int r = 0; r < RF; ++r)
+#pragma unroll
+      for (int q = 0; q < NQM; ++q)
+        kr[r][q] = (g0 + r < i1 && q < nq) ? K2[(g0 + r) * mp2 + lane + 64 * q]
+                                           : make_double2(0.0, 0.0);
+    double d[RF];
+#pragma unroll
+    for (int r = 0; r < RF; ++r) {
+      double s0 = 0.0;
+#pragma unroll
+      for (int q = 0; q < NQM; ++q) {
+        s0 = fma(kr[r][q].x, xr[q].x, s0);
+        s0 = fma(kr[r][q].y, xr[q].y, s0);
+      }
+      d[r] = wave_sum(s0);
+    }
+    // the row updates: lane r < RF takes row g0 + r (one exp per row, not one per lane)
+    double dme = d[0];
+#pragma unroll
+    for (int r = 1; r < RF; ++r) dme = (lane == r) ? d[r] : dme;
+    double vme = 0.0;
+    const int64_t im = g0 + lane;
+    if (lane < RF && im < i1) {
+      if constexpr (MODE == LAP_PASS_A) {   // k_lap_nr_a
+        if (im < n) {
+          const double fi = pa.f[im], yi = pa.y[im], mui = pa.mu[im], zi = pa.Z[im];
+          const double iz = pa.zinv[im];
+          const double e = exp(fi);
+          const double W = -pa.expo * e;
+          const double gi = -pa.expo * e + yi;
+          const double om = 1.0 - zi * W;
+          const double gp = gi + (-iz * (fi - mui) + iz * dme);
+          vme = (1.0 / om) * gp;
+          pa.g[im] = gi;
+          pa.omzw[im] = om;
+          pa.gpsi[im] = gp;
+          if (fabs(gp) > pa.tol) sc += 1.0;
+        } else {
+          pa.g[im] = 0.0;
+          pa.omzw[im] = 1.0;
+          pa.gpsi[im] = 0.0;
+        }
+        pa.y1[im] = dme;
+        pa.v[im] = vme;
+      } else {                              // k_lap_nr_b; tv = (f - mu)/Z at the new f
+        if (im < n) {
+          const double fi = pa.f[im], mui = pa.mu[im], zi = pa.Z[im], iz = pa.zinv[im];
+          const double gi = pa.g_in[im], om = pa.omzw_in[im], y1i = pa.y1_in[im];
+          const double a11 = (zi / om) * gi;
+          const double a12 = (1.0 / om) * (fi - mui);
+          const double a13 = y1i / om;
+          const double a2 = dme / om;
+          const double fn = fi + (a11 - a12 + a13 + a2);
+          pa.f_out[im] = fn;
+          const double rr = fn - mui;
+          vme = iz * rr;
+          sc = fma(vme, rr, sc);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RF; ++r) {
+      const double vi = __shfl(vme, r, 64);   // 0 for rows past i1
+#pragma unroll
+      for (int q = 0; q < NQM; ++q) {
+        acc[q].x = fma(kr[r][q].x, vi, acc[q].x);
+        acc[q].y = fma(kr[r][q].y, vi, acc[q].y);
+      }
+    }
+  }
+  sc = wave_sum(sc);   // lanes 0..RF-1 hold their rows' parts
+#pragma unroll
+  for (int q = 0; q < NQM; ++q)
+    if (q < nq) reinterpret_cast<double2*>(s_part + wv * mp)[lane + 64 * q] = acc[q];
+  if (lane == 0) s_red[wv] = sc;
+  __syncthreads();
+  for (int64_t j = tid; j < mp; j += 256)
+    pa.part[ch * mp + j] = ((s_part[j] + s_part[mp + j]) + s_part[2 * mp + j]) + s_part[3 * mp + j];
+  if (tid == 0) pa.sc[ch] = ((s_red[0] + s_red[1]) + s_red[2]) + s_red[3];
+}
+
 // part[ch][j] = sum_{i in chunk ch} K_ij^2
 __global__ void __launch_bounds__(128) k_colnorm2(const double* __restrict__ K, int64_t n_pad,
                                                   int64_t mp, int64_t chunk,
@@ -636,11 +749,25 @@ hipError_t launch_rowpass(const double* K, int64_t n, int64_t n_pad, int64_t mp,
   const int64_t nch = lap_rowpass_chunks(n_pad, mp);
   if (nch * mp + NS * nch > part_cap) return hipErrorInvalidValue;
   const int64_t chunk = (n_pad + nch - 1) / nch;
-  const size_t shmem = sizeof(double) * (size_t)(NRA_LDS + mp);
   pa.part = part;
   pa.sc = part + nch * mp;
-  hipLaunchKernelGGL(k_lap_rowpass<MODE>, dim3((unsigned)nch), dim3(256), shmem, s, K, n, n_pad,
-                     mp, chunk, pa);
+  if (SGP_LAP_ROWSTREAM) {
+    const size_t shm = sizeof(double) * 4 * (size_t)mp;
+    const dim3 g((unsigned)nch), b(256);
+    const int nq = (int)(mp / 128);
+    // rows in flight per wave and waves per SIMD (SGP_LAP_RS_CFG: probe configurations)
+    constexpr int C = SGP_LAP_RS_CFG;
+    constexpr int F2 = C == 1 ? 4 : C == 2 ? 16 : 8, O2 = C == 1 ? 4 : C == 2 ? 2 : 3;
+    constexpr int F4 = C == 1 ? 2 : C == 2 ? 8 : 4, O4 = O2;
+    if (nq <= 2) hipLaunchKernelGGL((k_lap_rowstream<MODE, 2, F2, O2>), g, b, shm, s, K, n, n_pad, mp, chunk, pa);
+    else if (nq <= 4) hipLaunchKernelGGL((k_lap_rowstream<MODE, 4, F4, O4>), g, b, shm, s, K, n, n_pad, mp, chunk, pa);
+    else if (nq <= 8) hipLaunchKernelGGL((k_lap_rowstream<MODE, 8, 2, 2>), g, b, shm, s, K, n, n_pad, mp, chunk, pa);
+    else hipLaunchKernelGGL((k_lap_rowstream<MODE, 16, 1, 2>), g, b, shm, s, K, n, n_pad, mp, chunk, pa);
+  } else {
+    const size_t shmem = sizeof(double) * (size_t)(NRA_LDS + mp);
+    hipLaunchKernelGGL(k_lap_rowpass<MODE>, dim3((unsigned)nch), dim3(256), shmem, s, K, n, n_pad,
+                       mp, chunk, pa);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   e = launch_colsum(part, nch, mp, out_t, s);

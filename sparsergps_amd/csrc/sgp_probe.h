@@ -25,6 +25,9 @@
 //   SGP_SDT_WT          ... plus this with the t slice
 //   SGP_SYRK_W3         0: signed-weight / t SYRKs keep per-fragment weights on the packed plan
 //   SGP_CON_ROWQ_KU     1: the row-quadratic pass without u keeps the (unused) K u fold
+//   SGP_LAP_ROWSTREAM   0: the Newton-step passes over K12 through the LDS row image
+//   SGP_LAP_RS_CFG      k_lap_rowstream at mp <= 512: 0 (16 / NQM rows per wave, 3 waves per
+//                       SIMD), 1 (half the rows, 4 waves), 2 (twice the rows, 2 waves)
 //   SGP_S256_IL         1: k_syrk_s256's step with an interleave request
 #pragma once
 
@@ -33,7 +36,8 @@
      defined(SGP_CON_IL_SPREAD) || defined(SGP_CON_SHMEM) || defined(SGP_NRA_LDS) ||          \
      defined(SGP_SYRK_BAL) || defined(SGP_SDT_IL) || defined(SGP_S256_IL) ||                  \
      defined(SGP_SDT_W) || defined(SGP_SDT_WW) || defined(SGP_SDT_WT) ||                      \
-     defined(SGP_SYRK_W3) || defined(SGP_CON_ROWQ_KU)) &&                                     \
+     defined(SGP_SYRK_W3) || defined(SGP_CON_ROWQ_KU) || defined(SGP_LAP_ROWSTREAM) ||        \
+     defined(SGP_LAP_RS_CFG)) &&                                                              \
     !defined(SGP_PROBE_BUILD)
 #error "timing probes and experiment knobs are for variant builds only (SGP_PROBE_BUILD)"
 #endif
@@ -76,6 +80,12 @@
 #endif
 #ifndef SGP_CON_ROWQ_KU
 #define SGP_CON_ROWQ_KU 0
+#endif
+#ifndef SGP_LAP_ROWSTREAM
+#define SGP_LAP_ROWSTREAM 1
+#endif
+#ifndef SGP_LAP_RS_CFG
+#define SGP_LAP_RS_CFG 0
 #endif
 #ifndef SGP_S256_IL
 #define SGP_S256_IL 0
