@@ -326,6 +326,8 @@ struct Readback {
   }
 };
 
+constexpr size_t kTimingPoolReserve = 1024;
+
 hipEvent_t pool_event(sgp_ctx* c) {
   if (c->pool_used < c->pool.size()) return c->pool[c->pool_used++];
   hipEvent_t e;
@@ -838,6 +840,13 @@ int sgp_ctx_enable_timing(sgp_ctx* c, int enable) {
     c->timers.clear();
     c->pool_used = 0;
     c->timing_evals = 0;
+    // events for the timed evaluations created here, not one pair per scope inside them
+    // (hipEventCreate on the host between evaluations showed up at C2's 0.66 ms per step)
+    while (c->pool.size() < kTimingPoolReserve) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) break;
+      c->pool.push_back(e);
+    }
   }
   return SGP_OK;
 }
