@@ -291,10 +291,7 @@ __global__ void __launch_bounds__(128) k_gemv_cols(const double* __restrict__ K,
 }
 
 // Newton-step passes over K12 that each replace a row GEMV, a per-row kernel and a column GEMV
-// (two K reads) by one read: per row block of R = 8192 / mp rows staged in LDS (64 KB; the next
-// block's rows and row vectors are loaded into registers while the current one is processed),
-//   d_i = K_i x (one wave per row, four rows of a wave at a time), a per-row update by one
-//   thread per row, then part[ch][j] += sum_i K_ij v_i from the same LDS image.
+// (two K reads) by one read (k_lap_rowstream below):
 // LAP_PASS_A (NR part a): x = x1, the k_lap_nr_a update (y1 = d, g, omzw, gpsi), v = gpsi/omzw,
 //   scalars = [stop-rule count].
 // LAP_PASS_B (NR part b + the next objective's t): x = x2, the k_lap_nr_b update of f
@@ -302,9 +299,7 @@ __global__ void __launch_bounds__(128) k_gemv_cols(const double* __restrict__ K,
 //   k_lap_obj then forms B, rf, tv and the likelihood sums in its own (cheap, fully parallel)
 //   pass and S_B comes from the weighted SYRK without t.
 // One workgroup per row chunk; part[ch][0..mp) and the scalars sc[ch][..] are reduced by
-// launch_colsum (fixed order).  mp <= 2048 (x staged beside the rows).
-constexpr int NRA_LDS = SGP_NRA_LDS;          // doubles of the row-block image
-constexpr int NRA_LD2 = NRA_LDS / 512;        // double2 loads per thread and block
+// launch_colsum (fixed order).  mp <= 2048.
 enum { LAP_PASS_A = 0, LAP_PASS_B = 1 };
 
 struct LapPassArgs {
@@ -319,168 +314,12 @@ struct LapPassArgs {
   double* sc;                                 // [nch][NS]
 };
 
-template <int MODE>
-__global__ void __launch_bounds__(256) k_lap_rowpass(const double* __restrict__ K, int64_t n,
-                                                     int64_t n_pad, int64_t mp, int64_t chunk,
-                                                     LapPassArgs pa) {
-  constexpr int NV = MODE == LAP_PASS_A ? 5 : 8;      // row vectors staged per row
-  constexpr int NS = 1;                                // scalar sums
-  extern __shared__ __attribute__((aligned(16))) double nra_lds[];
-  double* Ks = nra_lds;                 // [R][mp]
-  double* xs = nra_lds + NRA_LDS;       // [mp]
-  constexpr int RMAX = NRA_LDS / 128;   // rows of a block at the smallest mp
-  __shared__ double s_v[RMAX], s_dot[RMAX], s_rv[NV][RMAX];
-  __shared__ double s_red[4][NS];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int R = (int)(NRA_LDS / mp);
-  const int64_t ch = blockIdx.x;
-  const int64_t i0 = ch * chunk;
-  const int64_t i1 = (i0 + chunk < n_pad) ? i0 + chunk : n_pad;
-  for (int64_t j = tid; j < mp; j += 256) xs[j] = pa.x[j];
-  constexpr int NCOL = 8;               // columns per thread: mp <= 2048
-  double acc[NCOL];
-#pragma unroll
-  for (int q = 0; q < NCOL; ++q) acc[q] = 0.0;
-  double sacc[NS];
-#pragma unroll
-  for (int k = 0; k < NS; ++k) sacc[k] = 0.0;
-  double2 t[NRA_LD2];
-  double rv[NV];
-  // block b0's rows (guarded: the chunk's last block may be short) and, for thread r < rows,
-  // row b0 + r's vectors
-  auto load_block = [&](int64_t b0) {
-    const int rows = (int)((b0 + R <= i1) ? R : i1 - b0);
-    const double2* src = reinterpret_cast<const double2*>(K + b0 * mp);
-    const int64_t nv2 = (int64_t)rows * mp / 2;
-#pragma unroll
-    for (int q = 0; q < NRA_LD2; ++q) {
-      const int64_t e = tid + 256 * q;
-      t[q] = (e < nv2) ? src[e] : make_double2(0.0, 0.0);
-    }
-    if (tid < rows && b0 + tid < n) {   // rows past n: the vectors may end at n
-      const int64_t i = b0 + tid;
-      rv[0] = pa.f[i]; rv[1] = pa.y[i]; rv[2] = pa.mu[i]; rv[3] = pa.Z[i]; rv[4] = pa.zinv[i];
-      if constexpr (MODE == LAP_PASS_B) {
-        rv[5] = pa.g_in[i]; rv[6] = pa.omzw_in[i]; rv[7] = pa.y1_in[i];
-      }
-    }
-  };
-  if (i0 < i1) load_block(i0);
-  for (int64_t b0 = i0; b0 < i1; b0 += R) {
-    const int rows = (int)((b0 + R <= i1) ? R : i1 - b0);
-    __syncthreads();                    // the previous block's image and vectors are read
-    {
-      double2* dst = reinterpret_cast<double2*>(Ks);
-#pragma unroll
-      for (int q = 0; q < NRA_LD2; ++q) dst[tid + 256 * q] = t[q];
-      if (tid < rows) {
-#pragma unroll
-        for (int k = 0; k < NV; ++k) s_rv[k][tid] = rv[k];
-      }
-    }
-    __syncthreads();
-    if (b0 + R < i1) load_block(b0 + R);   // in flight while this block is processed
-    // d = K x, one wave per row, four rows of a wave at a time (independent dot chains)
-    for (int r0 = wv; r0 < rows; r0 += 16) {
-      double sd[4] = {0.0, 0.0, 0.0, 0.0};
-      for (int64_t j = lane; j < mp; j += 64) {
-        const double xv = xs[j];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (r0 + 4 * k < rows) sd[k] = fma(Ks[(int64_t)(r0 + 4 * k) * mp + j], xv, sd[k]);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const double w = wave_sum(sd[k]);
-        if (lane == 0 && r0 + 4 * k < rows) s_dot[r0 + 4 * k] = w;
-      }
-    }
-    __syncthreads();
-    // the row update, one thread per row
-    if (tid < rows) {
-      const int64_t i = b0 + tid;
-      const double sd = s_dot[tid];
-      double vi = 0.0;
-      const double fi = s_rv[0][tid], yi = s_rv[1][tid], mui = s_rv[2][tid];
-      const double zi = s_rv[3][tid], iz = s_rv[4][tid];
-      if constexpr (MODE == LAP_PASS_A) {   // k_lap_nr_a
-        if (i < n) {
-          const double e = exp(fi);
-          const double W = -pa.expo * e;
-          const double gi = -pa.expo * e + yi;
-          const double om = 1.0 - zi * W;
-          const double gp = gi + (-iz * (fi - mui) + iz * sd);
-          vi = (1.0 / om) * gp;
-          pa.g[i] = gi;
-          pa.omzw[i] = om;
-          pa.gpsi[i] = gp;
-          if (fabs(gp) > pa.tol) sacc[0] += 1.0;
-        } else {
-          pa.g[i] = 0.0;
-          pa.omzw[i] = 1.0;
-          pa.gpsi[i] = 0.0;
-        }
-        pa.y1[i] = sd;
-        pa.v[i] = vi;
-      } else {                              // k_lap_nr_b; tv = (f - mu)/Z at the new f
-        (void)yi;
-        if (i < n) {
-          const double gi = s_rv[5][tid], om = s_rv[6][tid], y1i = s_rv[7][tid];
-          const double a11 = (zi / om) * gi;
-          const double a12 = (1.0 / om) * (fi - mui);
-          const double a13 = y1i / om;
-          const double a2 = sd / om;
-          const double fn = fi + (a11 - a12 + a13 + a2);
-          pa.f_out[i] = fn;
-          const double r = fn - mui;
-          vi = iz * r;
-          sacc[0] = fma(vi, r, sacc[0]);
-        }
-      }
-      s_v[tid] = vi;
-    }
-    __syncthreads();
-    // K^T v over the block's rows, in row order
-#pragma unroll
-    for (int q = 0; q < NCOL; ++q) {
-      const int64_t j = tid + 256 * q;
-      if (j < mp) {
-        double a = acc[q];
-        int r = 0;
-        for (; r + 4 <= rows; r += 4) {   // the four reads issued together, summed in row order
-          const double k0 = Ks[(int64_t)r * mp + j], k1 = Ks[(int64_t)(r + 1) * mp + j];
-          const double k2 = Ks[(int64_t)(r + 2) * mp + j], k3 = Ks[(int64_t)(r + 3) * mp + j];
-          a = fma(k0, s_v[r], a);
-          a = fma(k1, s_v[r + 1], a);
-          a = fma(k2, s_v[r + 2], a);
-          a = fma(k3, s_v[r + 3], a);
-        }
-        for (; r < rows; ++r) a = fma(Ks[(int64_t)r * mp + j], s_v[r], a);
-        acc[q] = a;
-      }
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < NCOL; ++q) {
-    const int64_t j = tid + 256 * q;
-    if (j < mp) pa.part[ch * mp + j] = acc[q];
-  }
-  // the scalar sums: threads 0..R-1 hold their rows' parts
-#pragma unroll
-  for (int k = 0; k < NS; ++k) {
-    const double w = wave_sum(sacc[k]);
-    if (lane == 0) s_red[wv][k] = w;
-  }
-  __syncthreads();
-  if (tid < NS) pa.sc[ch * NS + tid] = s_red[0][tid] + s_red[1][tid] + s_red[2][tid] + s_red[3][tid];
-}
-
-// The same two Newton-step passes without the LDS row image: each wave streams its rows
-// straight into registers (lane l holds columns 2l + 128q, 2l + 128q + 1 of RF rows at a time),
+// The two Newton-step passes, streamed: each wave loads its rows straight into registers (lane l holds columns 2l + 128q, 2l + 128q + 1 of RF rows at a time),
 // forms d_i = K_i x with its lanes' x slice and one wave reduction per row, applies the row
 // update (every lane; lane 0 stores), and folds v_i K_i into its lanes' column sums from the same
-// registers -- no barrier inside the row loop, and 16 waves per CU keep the loads of 64 rows in
-// flight (the LDS-image form stalls a workgroup on each 64 KB block: 4.9 TB/s at C5).  The four
+// registers -- no barrier inside the row loop (round 3's form staged 64 KB row blocks in LDS
+// behind two barriers per block and stalled on each block's loads: 4.9 against 5.1-5.6 TB/s
+// at C5, profiles/r4/lap_rowstream_ab.txt).  The four
 // waves' column sums are combined in fixed order at the end.  NQM: double2 columns per lane per
 // row (mp / 128 rounded up to 2, 4, 8 or 16), RF rows in flight per wave, OCC waves per SIMD.
 template <int MODE, int NQM, int RF, int OCC>
@@ -727,9 +566,9 @@ hipError_t launch_lap_nr_a(int64_t n, int64_t n_pad, const double* f, const doub
 }
 
 int64_t lap_rowpass_chunks(int64_t n_pad, int64_t mp) {
-  // ~8 row blocks per workgroup, at most LAP_NB x 4 workgroups
-  const int64_t R = NRA_LDS / mp;
-  int64_t nch = (n_pad + 8 * R - 1) / (8 * R);
+  // 65536 / mp rows per workgroup (128 at mp = 512), at most LAP_NB x 4 workgroups
+  const int64_t rows = 65536 / mp;
+  int64_t nch = (n_pad + rows - 1) / rows;
   if (nch > 4 * LAP_NB) nch = 4 * LAP_NB;
   return nch < 1 ? 1 : nch;
 }
@@ -751,7 +590,7 @@ hipError_t launch_rowpass(const double* K, int64_t n, int64_t n_pad, int64_t mp,
   const int64_t chunk = (n_pad + nch - 1) / nch;
   pa.part = part;
   pa.sc = part + nch * mp;
-  if (SGP_LAP_ROWSTREAM) {
+  {
     const size_t shm = sizeof(double) * 4 * (size_t)mp;
     const dim3 g((unsigned)nch), b(256);
     const int nq = (int)(mp / 128);
@@ -763,10 +602,6 @@ hipError_t launch_rowpass(const double* K, int64_t n, int64_t n_pad, int64_t mp,
     else if (nq <= 4) hipLaunchKernelGGL((k_lap_rowstream<MODE, 4, F4, O4>), g, b, shm, s, K, n, n_pad, mp, chunk, pa);
     else if (nq <= 8) hipLaunchKernelGGL((k_lap_rowstream<MODE, 8, 2, 2>), g, b, shm, s, K, n, n_pad, mp, chunk, pa);
     else hipLaunchKernelGGL((k_lap_rowstream<MODE, 16, 1, 2>), g, b, shm, s, K, n, n_pad, mp, chunk, pa);
-  } else {
-    const size_t shmem = sizeof(double) * (size_t)(NRA_LDS + mp);
-    hipLaunchKernelGGL(k_lap_rowpass<MODE>, dim3((unsigned)nch), dim3(256), shmem, s, K, n, n_pad,
-                       mp, chunk, pa);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

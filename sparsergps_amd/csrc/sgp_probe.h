@@ -17,7 +17,6 @@
 //   SGP_SYRK_IL_PAT     the same for the SYRKs
 //   SGP_CON_IL_SPREAD   contraction: LDS fragment reads spread over the step instead of up front
 //   SGP_CON_SHMEM       dynamic LDS pad of the gradient-contraction launches
-//   SGP_NRA_LDS         doubles of k_lap_rowpass's row-block image
 //   SGP_SYRK_BAL        0: no balanced S-only SYRK plan (syrk_plan_bal)
 //   SGP_SDT_IL          0: the diagonal-tile SYRK step without the interleave request
 //   SGP_SDT_W           syrk_plan_bal's cost of a diagonal-tile wave-step, in MFMAs (36 issued)
@@ -25,7 +24,6 @@
 //   SGP_SDT_WT          ... plus this with the t slice
 //   SGP_SYRK_W3         0: signed-weight / t SYRKs keep per-fragment weights on the packed plan
 //   SGP_CON_ROWQ_KU     1: the row-quadratic pass without u keeps the (unused) K u fold
-//   SGP_LAP_ROWSTREAM   0: the Newton-step passes over K12 through the LDS row image
 //   SGP_LAP_RS_CFG      k_lap_rowstream at mp <= 512: 0 (16 / NQM rows per wave, 3 waves per
 //                       SIMD), 1 (half the rows, 4 waves), 2 (twice the rows, 2 waves)
 //   SGP_S256_IL         1: k_syrk_s256's step with an interleave request
@@ -33,10 +31,10 @@
 
 #if (defined(SGP_CON_TRACE) || defined(SGP_CON_NO_EPILOGUE) || defined(SGP_GJ_TRACE) ||       \
      defined(SGP_IL_VMEM0) || defined(SGP_CON_IL_PAT) || defined(SGP_SYRK_IL_PAT) ||          \
-     defined(SGP_CON_IL_SPREAD) || defined(SGP_CON_SHMEM) || defined(SGP_NRA_LDS) ||          \
+     defined(SGP_CON_IL_SPREAD) || defined(SGP_CON_SHMEM) ||                                  \
      defined(SGP_SYRK_BAL) || defined(SGP_SDT_IL) || defined(SGP_S256_IL) ||                  \
      defined(SGP_SDT_W) || defined(SGP_SDT_WW) || defined(SGP_SDT_WT) ||                      \
-     defined(SGP_SYRK_W3) || defined(SGP_CON_ROWQ_KU) || defined(SGP_LAP_ROWSTREAM) ||        \
+     defined(SGP_SYRK_W3) || defined(SGP_CON_ROWQ_KU) ||                                      \
      defined(SGP_LAP_RS_CFG)) &&                                                              \
     !defined(SGP_PROBE_BUILD)
 #error "timing probes and experiment knobs are for variant builds only (SGP_PROBE_BUILD)"
@@ -56,9 +54,6 @@
 #endif
 #ifndef SGP_CON_SHMEM
 #define SGP_CON_SHMEM 0
-#endif
-#ifndef SGP_NRA_LDS
-#define SGP_NRA_LDS 8192
 #endif
 #ifndef SGP_SYRK_BAL
 #define SGP_SYRK_BAL 1
@@ -80,9 +75,6 @@
 #endif
 #ifndef SGP_CON_ROWQ_KU
 #define SGP_CON_ROWQ_KU 0
-#endif
-#ifndef SGP_LAP_ROWSTREAM
-#define SGP_LAP_ROWSTREAM 1
 #endif
 #ifndef SGP_LAP_RS_CFG
 #define SGP_LAP_RS_CFG 0

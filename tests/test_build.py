@@ -56,7 +56,7 @@ def test_stamps_are_path_independent():
             assert B.ROOT not in text and "hipcc" not in text
 
 
-@pytest.mark.parametrize("knob", ["SGP_CON_IL_PAT=3", "SGP_NRA_LDS=4096", "SGP_CON_SHMEM=1"])
+@pytest.mark.parametrize("knob", ["SGP_CON_IL_PAT=3", "SGP_LAP_RS_CFG=1", "SGP_CON_SHMEM=1"])
 def test_experiment_knobs_need_probe_build(knob):
     src = os.path.join(B.CSRC, "sgp_probe.h")
     cmd = [B.hipcc(), "-x", "hip", "--offload-arch=gfx950", "-fsyntax-only", f"-D{knob}", src]
