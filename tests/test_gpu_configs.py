@@ -186,3 +186,38 @@ def test_fitc_headline_shape_against_chunked_fitc_model(sgp):
     o, g = AC.eval_fitc("ard", th, P["X"], P["y"], P["mu"], P["U"], P["delta"])
     assert abs(obj - o) / abs(o) < 1e-9
     assert _rel(list(grad.values()), g) < 1e-7
+
+
+@pytest.mark.parametrize("m,n,cov", [(600, 60_000, "ard"), (384, 40_000, "sqexp"), (1100, 30_000, "ard")])
+def test_fitc_balanced_plans_against_chunked_fitc_model(sgp, m, n, cov):
+    """FITC's t-carrying and signed-weight SYRKs at other balanced-plan shapes (nb = 5, 3 and 9
+    128-tiles; the nb = 4 / 8 shapes are the C5 / C3 tests above) against the row-chunked
+    FITC model.  Reference: R/laplace_approx_obj_funs.R:6, R/laplace_approx_gradient.R:720-971."""
+    from oracle import adjoint_chunked as AC
+    from sparsergps_amd.workloads import make_gaussian_problem
+    P = make_gaussian_problem("C3" if cov == "ard" else "C2", n=n, m=m)
+    th = np.array(list(P["cov_par"].values()))
+    obj, grad = sgp.fitc_eval(P["cov_par"], cov, P["U"], P["X"], P["y"], P["mu"], P["delta"])
+    o, g = AC.eval_fitc(cov, th, P["X"], P["y"], P["mu"], P["U"], P["delta"])
+    assert abs(obj - o) / abs(o) < 1e-9
+    assert _rel(list(grad.values()), g) < 1e-7
+
+
+@pytest.mark.parametrize("m,n", [(384, 30_000), (640, 20_000)])
+def test_laplace_balanced_plans_against_chunked_laplace_model(sgp, m, n):
+    """The Laplace NR objectives (sqrt(w) SYRK with t on the balanced plan), S_a (signed) and the
+    streamed Newton passes at nb = 3 and 5 against the row-chunked Laplace model."""
+    from oracle import adjoint_chunked as AC
+    from sparsergps_amd.workloads import make_poisson_problem
+    P = make_poisson_problem(n=n, m=m)
+    th = np.array(list(P["cov_par"].values()))
+    o, g, f, objs = AC.eval_laplace("sqexp", th, P["X"], P["y"], P["mu"], P["U"], P["f0"], P["a"],
+                                    P["delta"], tol=1e-5)
+    with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=m) as ctx:
+        ctx.lap_set_f(P["f0"])
+        obj, grad, nit = ctx.eval_laplace(th, "sqexp", P["U"], P["delta"], P["a"], 1e-5, 1000)
+        ov = ctx.lap_objective_values()
+    assert nit == len(objs) == len(ov)
+    np.testing.assert_allclose(ov, objs, rtol=1e-9, atol=0)
+    assert abs(obj - o) / abs(o) < 1e-9
+    assert _rel(grad, g) < 1e-7
