@@ -235,7 +235,7 @@ __device__ __forceinline__ void gj_mm64(const double* As, const double* Bs, d4 (
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
+#pragma unroll SGP_GJ_MM_UNROLL
   for (int kk = 0; kk < 16; ++kk) {
     const int kx = kk * 4 + (lane >> 4);
     double af[2], bf[2];

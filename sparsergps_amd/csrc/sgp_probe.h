@@ -26,6 +26,7 @@
 //   SGP_CON_ROWQ_KU     1: the row-quadratic pass without u keeps the (unused) K u fold
 //   SGP_LAP_RS_CFG      k_lap_rowstream at mp <= 512: 0 (16 / NQM rows per wave, 3 waves per
 //                       SIMD), 1 (half the rows, 4 waves), 2 (twice the rows, 2 waves)
+//   SGP_GJ_MM_UNROLL    unroll of gj_mm64's 16 k-substeps (4)
 //   SGP_S256_IL         1: k_syrk_s256's step with an interleave request
 #pragma once
 
@@ -35,7 +36,7 @@
      defined(SGP_SYRK_BAL) || defined(SGP_SDT_IL) || defined(SGP_S256_IL) ||                  \
      defined(SGP_SDT_W) || defined(SGP_SDT_WW) || defined(SGP_SDT_WT) ||                      \
      defined(SGP_SYRK_W3) || defined(SGP_CON_ROWQ_KU) ||                                      \
-     defined(SGP_LAP_RS_CFG)) &&                                                              \
+     defined(SGP_LAP_RS_CFG) || defined(SGP_GJ_MM_UNROLL)) &&                                 \
     !defined(SGP_PROBE_BUILD)
 #error "timing probes and experiment knobs are for variant builds only (SGP_PROBE_BUILD)"
 #endif
@@ -78,6 +79,9 @@
 #endif
 #ifndef SGP_LAP_RS_CFG
 #define SGP_LAP_RS_CFG 0
+#endif
+#ifndef SGP_GJ_MM_UNROLL
+#define SGP_GJ_MM_UNROLL 4
 #endif
 #ifndef SGP_S256_IL
 #define SGP_S256_IL 0
