@@ -26,7 +26,7 @@
 //   SGP_CON_ROWQ_KU     1: the row-quadratic pass without u keeps the (unused) K u fold
 //   SGP_LAP_RS_CFG      k_lap_rowstream at mp <= 512: 0 (16 / NQM rows per wave, 3 waves per
 //                       SIMD), 1 (half the rows, 4 waves), 2 (twice the rows, 2 waves)
-//   SGP_GJ_MM_UNROLL    unroll of gj_mm64's 16 k-substeps (4)
+//   SGP_GJ_MM_UNROLL    unroll of gj_mm64's 16 k-substeps (16; 4 before round 4)
 //   SGP_S256_IL         1: k_syrk_s256's step with an interleave request
 #pragma once
 
@@ -81,7 +81,7 @@
 #define SGP_LAP_RS_CFG 0
 #endif
 #ifndef SGP_GJ_MM_UNROLL
-#define SGP_GJ_MM_UNROLL 4
+#define SGP_GJ_MM_UNROLL 16
 #endif
 #ifndef SGP_S256_IL
 #define SGP_S256_IL 0
