@@ -104,6 +104,30 @@ typedef struct sgp_ctx sgp_ctx;
 int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_t ldx, int d,
                    const double* y, const double* mu, int64_t m_max);
 int sgp_ctx_destroy(sgp_ctx* ctx);
+
+/* Row-sharded context over several GPUs of one node (config C4; BASELINE north_star: "sharding
+ * the n observation rows across the 8 GPUs of one node with an RCCL all-reduce", SURVEY 8(b)'s
+ * sgp_ctx_create(X, y, mu, n, d, ngpus)).  Shard k (k < nshards) holds the contiguous row block
+ * [k*n/N + min(k, n%N), ...) -- sparsergps_amd.dist.shard_rows -- on device devices[k] (NULL:
+ * device k).  The library drives the shards itself: one host thread per distinct device, the
+ * row-sum reductions of every evaluation (VI and FITC: two; Laplace: two per NR iteration and
+ * two for the gradient) summed on each device over its shards (fixed order) and then over the
+ * devices by an in-process RCCL all-reduce (ncclCommInitAll over the distinct devices, on each
+ * device's stream, in place).  A device may repeat (several shards on one GPU).
+ * The handle is used with the ordinary entry points: sgp_eval_vi / sgp_eval_fitc /
+ * sgp_eval_laplace / sgp_lap_nr, sgp_lap_set_f / sgp_lap_get_f / sgp_lap_get_grad_psi (n values
+ * in the global row order) / sgp_lap_objective_values, sgp_posterior_u, sgp_ctx_enable_knot_grad,
+ * sgp_knot_gradient (bounds NULL = the knot bounds of ALL rows), sgp_ctx_row_bounds (all rows),
+ * sgp_ctx_set_data, sgp_ctx_rows (all rows), the three candidate scorers (each VI candidate as an
+ * objective-only evaluation at [U; cand_t], m + 1 <= m_max), the timing calls (shard 0's
+ * record) and sgp_ctx_destroy.  The phase-level entry points (sgp_vi_phase1 ... sgp_lap_step),
+ * sgp_ctx_set_stream, sgp_ctx_set_packed_reduction and sgp_eval_full return SGP_EINVAL.
+ * 1 <= nshards <= min(n, 64). */
+int sgp_ctx_create_multi(sgp_ctx** out, const int* devices, int nshards, const double* X,
+                         int64_t n, int64_t ldx, int d, const double* y, const double* mu,
+                         int64_t m_max);
+/* shards and distinct devices of a context (1 and 1 for sgp_ctx_create's) */
+int sgp_ctx_shards(const sgp_ctx* ctx, int* nshards, int* ndevices);
 /* launch on this hipStream_t; NULL selects the context's own (non-blocking) stream */
 int sgp_ctx_set_stream(sgp_ctx* ctx, void* hip_stream);
 /* replace y / mu (e.g. Laplace pseudo-data); host buffers of length n */

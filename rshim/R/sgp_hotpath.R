@@ -30,8 +30,14 @@
 ## leaves double range; sgp_options(r_det = TRUE) (the default) passes SGP_FLAG_R_DET so the
 ## objective is identical, FALSE uses the factorisation's finite log-determinant.
 
+## Multi-GPU (north star C4): the rows of a fit are split into contiguous blocks over the GPUs of
+## the node and every evaluation's row sums are combined inside libsgp by an RCCL all-reduce
+## (sgp_ctx_create_multi).  sgp_options(ngpus = k) uses devices 0..k-1; ngpus = NULL (the
+## default) uses every visible GPU once each shard keeps >= 125 000 rows (one GPU below that:
+## the replicated m x m work would dominate); sgp_options(devices = c(...)) names the device of
+## each shard explicitly (repeats allowed).
 .sgp <- new.env(parent = emptyenv())
-.sgp$opts <- list(r_det = TRUE)
+.sgp$opts <- list(r_det = TRUE, ngpus = NULL, devices = NULL)
 .sgp$orig <- list()
 
 SGP_FLAG_R_DET <- 1L
@@ -58,6 +64,19 @@ sgp_install <- function(ns = asNamespace("sparseRGPs")) {
 
 ## ---------------------------------------------------------------- context + theta layout
 
+## the device of each row shard (integer(0): one device, SGP_DEVICE)
+.sgp_devices <- function(n) {
+  dv <- .sgp$opts$devices
+  if (!is.null(dv)) return(as.integer(dv))
+  ng <- .sgp$opts$ngpus
+  if (is.null(ng)) {
+    nd <- .Call("sgp_R_device_count")
+    ng <- max(1L, min(nd, n %/% 125000L))
+  }
+  ng <- as.integer(ng)
+  if (ng <= 1L) integer(0) else seq_len(ng) - 1L
+}
+
 ## one device context per data set (X, y, mu uploaded once); reused while xy, y, mu are
 ## identical() and m fits, recreated otherwise
 .sgp_ctx <- function(xy, y, mu, m) {
@@ -65,15 +84,17 @@ sgp_install <- function(ns = asNamespace("sparseRGPs")) {
   y <- as.numeric(y)
   mu <- rep_len(as.numeric(mu), nrow(xy))
   e <- .sgp$ctx
+  devices <- .sgp_devices(nrow(xy))
   if (!is.null(e) && e$m_max >= m && identical(e$xy, xy) && identical(e$y, y) &&
-      identical(e$mu, mu))
+      identical(e$mu, mu) && identical(e$devices, devices))
     return(e$ptr)
   m_max <- max(m, if (is.null(e)) 0L else e$m_max)
   if (!is.null(e)) .Call("sgp_R_ctx_destroy", e$ptr)
   .sgp$ctx <- NULL
   .sgp$last <- NULL
-  ptr <- .Call("sgp_R_ctx_create", xy, y, mu, as.integer(m_max))
-  .sgp$ctx <- list(ptr = ptr, xy = xy, y = y, mu = mu, m_max = m_max, knots = FALSE)
+  ptr <- .Call("sgp_R_ctx_create", xy, y, mu, as.integer(m_max), devices)
+  .sgp$ctx <- list(ptr = ptr, xy = xy, y = y, mu = mu, m_max = m_max, knots = FALSE,
+                   devices = devices)
   ptr
 }
 

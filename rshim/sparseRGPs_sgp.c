@@ -429,18 +429,55 @@ static int kernel_of(SEXP cov_fun) {
   return -1;
 }
 
-/* sgp_R_ctx_create(xy, y, mu, m_max): X, y, mu to HBM once per fit (sgp_ctx_create) */
-SEXP sgp_R_ctx_create(SEXP xy, SEXP y, SEXP mu, SEXP m_max) {
+/* sgp_R_ctx_create(xy, y, mu, m_max, devices): X, y, mu to HBM once per fit.
+ * devices = NULL or length 0: one device (SGP_DEVICE, default 0; sgp_ctx_create);
+ * otherwise the device index of each row shard (sgp_ctx_create_multi: the rows split into
+ * length(devices) contiguous blocks, the reductions of every evaluation summed inside libsgp
+ * over the devices by an RCCL all-reduce -- north star C4).  rshim/R/sgp_hotpath.R picks them
+ * (from the R options ngpus / devices). */
+SEXP sgp_R_ctx_create(SEXP xy, SEXP y, SEXP mu, SEXP m_max, SEXP devices) {
   SEXP xr = PROTECT(as_real(xy)), yr = PROTECT(as_real(y)), mr = PROTECT(as_real(mu));
+  SEXP dr = PROTECT(Rf_isNull(devices) ? R_NilValue : as_real(devices));
   const int n = nrows_of(xr), d = ncols_of(xr);
   if (Rf_length(yr) != n || Rf_length(mr) != n) Rf_error("y and mu must have nrow(xy) values");
+  const int nsh = Rf_isNull(dr) ? 0 : Rf_length(dr);
+  if (nsh > 64) Rf_error("at most 64 row shards (got %d devices)", nsh);
   sgp_ctx* c = NULL;
-  check(sgp_ctx_create(&c, sgp_dev(), REAL(xr), n, n, d, REAL(yr), REAL(mr),
-                       (int64_t)Rf_asInteger(m_max)));
+  if (nsh == 0) {
+    check(sgp_ctx_create(&c, sgp_dev(), REAL(xr), n, n, d, REAL(yr), REAL(mr),
+                         (int64_t)Rf_asInteger(m_max)));
+  } else {
+    int dv[64];
+    for (int k = 0; k < nsh; ++k) {
+      const double v = REAL(dr)[k];
+      if (!(v >= 0.0) || v != floor(v)) Rf_error("devices must be non-negative integers");
+      dv[k] = (int)v;
+    }
+    check(sgp_ctx_create_multi(&c, dv, nsh, REAL(xr), n, n, d, REAL(yr), REAL(mr),
+                               (int64_t)Rf_asInteger(m_max)));
+  }
   SEXP p = PROTECT(R_MakeExternalPtr(c, R_NilValue, R_NilValue));
   R_RegisterCFinalizerEx(p, ctx_finalize, TRUE);
-  UNPROTECT(4);
+  UNPROTECT(5);
   return p;
+}
+
+/* visible HIP devices (0 without any) */
+SEXP sgp_R_device_count(void) {
+  int cnt = 0;
+  if (sgp_device_count(&cnt) != SGP_OK) cnt = 0;
+  return Rf_ScalarInteger(cnt);
+}
+
+/* c(row shards, distinct devices) of a context */
+SEXP sgp_R_ctx_shards(SEXP ctx) {
+  int ns = 0, nd = 0;
+  check(sgp_ctx_shards(ctx_of(ctx), &ns, &nd));
+  SEXP out = PROTECT(Rf_allocVector(REALSXP, 2));
+  REAL(out)[0] = ns;
+  REAL(out)[1] = nd;
+  UNPROTECT(1);
+  return out;
 }
 
 SEXP sgp_R_ctx_destroy(SEXP ctx) {
@@ -682,7 +719,9 @@ static const R_CallMethodDef CallEntries[] = {
     {"_sparseRGPs_make_cov_matC", (DL_FUNC)&_sparseRGPs_make_cov_matC, 5},
     {"_sparseRGPs_make_cov_mat_ardC", (DL_FUNC)&_sparseRGPs_make_cov_mat_ardC, 6},
     /* the fused hot path (rshim/R/sgp_hotpath.R) */
-    {"sgp_R_ctx_create", (DL_FUNC)&sgp_R_ctx_create, 4},
+    {"sgp_R_ctx_create", (DL_FUNC)&sgp_R_ctx_create, 5},
+    {"sgp_R_device_count", (DL_FUNC)&sgp_R_device_count, 0},
+    {"sgp_R_ctx_shards", (DL_FUNC)&sgp_R_ctx_shards, 1},
     {"sgp_R_ctx_destroy", (DL_FUNC)&sgp_R_ctx_destroy, 1},
     {"sgp_R_set_data", (DL_FUNC)&sgp_R_set_data, 3},
     {"sgp_R_eval", (DL_FUNC)&sgp_R_eval, 7},

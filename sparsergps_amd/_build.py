@@ -22,8 +22,9 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libsgp.so")
 VARIANT_ROOT = os.path.join(ROOT, "tools", "ab")
-SOURCES = ["capi.hip", "k_cov.hip", "k_mfma.hip", "k_dense.hip", "k_lap.hip"]
-HEADERS = ["sgp_internal.h", "sgp_probe.h", os.path.join("..", "..", "include", "sgp.h")]
+SOURCES = ["capi.hip", "k_cov.hip", "k_mfma.hip", "k_dense.hip", "k_lap.hip", "multi.hip"]
+HEADERS = ["sgp_internal.h", "sgp_probe.h", "sgp_multi.h",
+           os.path.join("..", "..", "include", "sgp.h")]
 ARCH = "gfx950"
 
 
@@ -54,7 +55,8 @@ def _compile_cmd(cc, src, obj, defs=(), csrc=CSRC):
     return [cc, *_compile_flags(src, defs), "-c", os.path.join(csrc, src), "-o", obj]
 
 
-LINK_FLAGS = [f"--offload-arch={ARCH}", "-shared", "-fPIC"]
+# librccl: the in-process all-reduces of sgp_ctx_create_multi contexts (multi.hip)
+LINK_FLAGS = [f"--offload-arch={ARCH}", "-shared", "-fPIC", "-lrccl", "-lpthread"]
 
 
 def _link_cmd(cc, objs, out):
@@ -97,9 +99,14 @@ def _obj_stale(obj, key, src, csrc=CSRC):
     return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
 
 
+def _sources(csrc=CSRC):
+    # an A/B build of an older revision compiles the translation units that revision has
+    return [s for s in SOURCES if csrc == CSRC or os.path.exists(os.path.join(csrc, s))]
+
+
 def _plan(outdir, defs, csrc=CSRC):
     objs, todo = [], []
-    for src in SOURCES:
+    for src in _sources(csrc):
         obj = os.path.join(outdir, src.replace(".hip", ".o"))
         objs.append(obj)
         if _obj_stale(obj, _obj_key(src, defs), src, csrc):
@@ -119,7 +126,7 @@ def _build_into(outdir, lib, defs, force, verbose, csrc=CSRC):
     os.makedirs(outdir, exist_ok=True)
     objs, todo = _plan(outdir, defs, csrc)
     if force:
-        todo = list(zip(SOURCES, objs))
+        todo = list(zip(_sources(csrc), objs))
     procs = []
     for src, obj in todo:
         cmd = _compile_cmd(cc, src, obj, defs, csrc)
@@ -178,9 +185,12 @@ def build_variant(name: str, defs=(), force: bool = False, verbose: bool = False
         # the revision's sources (csrc + include/sgp.h) exported under tools/ab/<name>/src
         src_root = os.path.join(outdir, "src")
         os.makedirs(src_root, exist_ok=True)
-        for path in ["sparsergps_amd/csrc/" + f for f in SOURCES + HEADERS[:2]] + ["include/sgp.h"]:
-            out = subprocess.run(["git", "-C", ROOT, "show", f"{rev}:{path}"],
-                                 stdout=subprocess.PIPE, stderr=subprocess.PIPE, check=True).stdout
+        for path in ["sparsergps_amd/csrc/" + f for f in SOURCES + HEADERS[:3]] + ["include/sgp.h"]:
+            res = subprocess.run(["git", "-C", ROOT, "show", f"{rev}:{path}"],
+                                 stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+            if res.returncode != 0:   # a file the revision does not have yet
+                continue
+            out = res.stdout
             dst = os.path.join(src_root, path)
             os.makedirs(os.path.dirname(dst), exist_ok=True)
             old = open(dst, "rb").read() if os.path.exists(dst) else None

@@ -40,6 +40,10 @@ PROTOTYPES = {
                                       C.c_int]),
     "sgp_ctx_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, c_double_p, C.c_int64, C.c_int64,
                                  C.c_int, c_double_p, c_double_p, C.c_int64]),
+    "sgp_ctx_create_multi": (C.c_int, [C.POINTER(C.c_void_p), c_int_p, C.c_int, c_double_p,
+                                       C.c_int64, C.c_int64, C.c_int, c_double_p, c_double_p,
+                                       C.c_int64]),
+    "sgp_ctx_shards": (C.c_int, [C.c_void_p, c_int_p, c_int_p]),
     "sgp_ctx_destroy": (C.c_int, [C.c_void_p]),
     "sgp_ctx_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "sgp_ctx_set_data": (C.c_int, [C.c_void_p, c_double_p, c_double_p]),

@@ -20,6 +20,7 @@
 
 #include "../../include/sgp.h"
 #include "sgp_internal.h"
+#include "sgp_multi.h"
 
 namespace {
 
@@ -42,6 +43,26 @@ void set_err(const char* fmt, ...) {
       return SGP_EHIP;                                                                     \
     }                                                                                      \
   } while (0)
+
+// Entry points a multi-device context (sgp_ctx_create_multi) answers through multi.hip, and the
+// ones it refuses (their reductions and streams are internal to it)
+#define MULTI_FWD(c, call)                   \
+  do {                                       \
+    if ((c) && (c)->multi) return (call);    \
+  } while (0)
+#define MULTI_REFUSE(c, name)                                                                  \
+  do {                                                                                         \
+    if ((c) && (c)->multi) {                                                                   \
+      set_err("%s is not available on a multi-device context (sgp_ctx_create_multi runs its " \
+              "reductions inside the library)", name);                                         \
+      return SGP_EINVAL;                                                                       \
+    }                                                                                          \
+  } while (0)
+
+int multi_bad_args() {
+  set_err("invalid arguments");
+  return SGP_EINVAL;
+}
 
 inline int64_t round_up(int64_t v, int64_t q) { return (v + q - 1) / q * q; }
 
@@ -175,6 +196,9 @@ struct Timer {
 }  // namespace
 
 struct sgp_ctx {
+  // a row-sharded multi-device context (sgp_ctx_create_multi): the entry points below forward
+  // to multi.hip, and none of the members after this one is used
+  MultiCtx* multi = nullptr;
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
@@ -534,6 +558,14 @@ int check_eval_args(sgp_ctx* c, int kernel, const double* theta, const double* U
 
 }  // namespace
 
+// multi.hip's hooks (sgp_multi.h)
+void sgp_internal_set_err(const char* msg) { set_err("%s", msg); }
+
+void sgp_internal_forget_eval(sgp_ctx* c) {
+  c->last_mode = 0;
+  c->lap_gpsi_valid = false;
+}
+
 // =========================================================================== public API
 extern "C" {
 
@@ -802,6 +834,11 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
 
 int sgp_ctx_destroy(sgp_ctx* c) {
   if (!c) return SGP_OK;
+  if (c->multi) {
+    multi_destroy(c->multi);
+    delete c;
+    return SGP_OK;
+  }
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->aux) (void)hipStreamSynchronize(c->aux);
@@ -811,13 +848,65 @@ int sgp_ctx_destroy(sgp_ctx* c) {
   return SGP_OK;
 }
 
+// Row-sharded multi-device context: shards = contiguous row blocks as dist.shard_rows, one per
+// entry of `devices` (NULL: 0 .. nshards - 1; entries may repeat), reductions inside the library
+// (multi.hip: device-side sums over a device's shards, RCCL all-reduce over the devices)
+int sgp_ctx_create_multi(sgp_ctx** out, const int* devices, int nshards, const double* X,
+                         int64_t n, int64_t ldx, int d, const double* y, const double* mu,
+                         int64_t m_max) {
+  if (!out || !X || !y || !mu || n < 1 || ldx < n || d < 1 || d > SGP_MAXD || m_max < 1 ||
+      nshards < 1 || nshards > SGP_MAX_SHARDS || n < nshards) {
+    set_err("invalid sgp_ctx_create_multi arguments (n=%lld, d=%d, m_max=%lld, nshards=%d; "
+            "1 <= nshards <= min(n, %d))", (long long)n, d, (long long)m_max, nshards,
+            SGP_MAX_SHARDS);
+    return SGP_EINVAL;
+  }
+  *out = nullptr;
+  if (devices)
+    for (int k = 0; k < nshards; ++k)
+      if (devices[k] < 0) {
+        set_err("sgp_ctx_create_multi: device %d of shard %d", devices[k], k);
+        return SGP_EINVAL;
+      }
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  for (int k = 0; k < nshards; ++k) {
+    const int dv = devices ? devices[k] : k;
+    if (dv >= ndev) {
+      set_err("sgp_ctx_create_multi: shard %d on device %d, but %d device(s) are visible", k, dv,
+              ndev);
+      return SGP_EINVAL;
+    }
+  }
+  MultiCtx* mc = nullptr;
+  const int st = multi_create(&mc, devices, nshards, X, n, ldx, d, y, mu, m_max);
+  if (st) return st;
+  sgp_ctx* c = new sgp_ctx();
+  c->multi = mc;
+  c->n = n;
+  c->d = d;
+  c->m_max = m_max;
+  *out = c;
+  return SGP_OK;
+}
+
+int sgp_ctx_shards(const sgp_ctx* c, int* nshards, int* ndevices) {
+  if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
+  if (c->multi) return multi_shards(c->multi, nshards, ndevices);
+  if (nshards) *nshards = 1;
+  if (ndevices) *ndevices = 1;
+  return SGP_OK;
+}
+
 int sgp_ctx_set_stream(sgp_ctx* c, void* s) {
+  MULTI_REFUSE(c, "sgp_ctx_set_stream");
   if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
   c->stream = s ? (hipStream_t)s : c->own;
   return SGP_OK;
 }
 
 int sgp_ctx_set_data(sgp_ctx* c, const double* y, const double* mu) {
+  MULTI_FWD(c, y && mu ? multi_set_data(c->multi, y, mu) : multi_bad_args());
   if (!c || !y || !mu) { set_err("invalid arguments"); return SGP_EINVAL; }
   HIPCHK(hipSetDevice(c->device));
   std::vector<double> hr((size_t)c->n_pad, 0.0);
@@ -834,6 +923,7 @@ int sgp_ctx_set_data(sgp_ctx* c, const double* y, const double* mu) {
 int64_t sgp_ctx_rows(const sgp_ctx* c) { return c ? c->n : -1; }
 
 int sgp_ctx_enable_timing(sgp_ctx* c, int enable) {
+  MULTI_FWD(c, sgp_ctx_enable_timing(multi_lead(c->multi), enable));
   if (!c) return SGP_EINVAL;
   c->timing = enable != 0;
   if (c->timing) {
@@ -852,15 +942,20 @@ int sgp_ctx_enable_timing(sgp_ctx* c, int enable) {
 }
 
 int sgp_ctx_timing_filter(sgp_ctx* c, const char* name) {
+  MULTI_FWD(c, sgp_ctx_timing_filter(multi_lead(c->multi), name));
   if (!c) return SGP_EINVAL;
   c->timing_only = name ? name : "";
   return SGP_OK;
 }
 
-int64_t sgp_ctx_timing_evals(const sgp_ctx* c) { return c ? c->timing_evals : -1; }
+int64_t sgp_ctx_timing_evals(const sgp_ctx* c) {
+  if (c && c->multi) return sgp_ctx_timing_evals(multi_lead(c->multi));
+  return c ? c->timing_evals : -1;
+}
 
 int sgp_ctx_timings(sgp_ctx* c, char* names, int64_t names_len, double* ms, int max_n,
                     int* count) {
+  MULTI_FWD(c, sgp_ctx_timings(multi_lead(c->multi), names, names_len, ms, max_n, count));
   if (!c || !count) return SGP_EINVAL;
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -909,6 +1004,7 @@ int64_t sgp_vi_red1_packed_count(int64_t m) {
 }
 
 int sgp_ctx_set_packed_reduction(sgp_ctx* c, int enable) {
+  MULTI_REFUSE(c, "sgp_ctx_set_packed_reduction");
   if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
   if (c->phase != 0) { set_err("cannot change the reduction layout inside an evaluation"); return SGP_EINVAL; }
   if (enable && !c->Sfull) {
@@ -983,6 +1079,7 @@ static int knot_finish(sgp_ctx* c, const double* knot_red, const double* uvec, c
 }
 
 int sgp_ctx_enable_knot_grad(sgp_ctx* c, int enable) {
+  MULTI_FWD(c, multi_enable_knot_grad(c->multi, enable));
   if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
   if (!enable) { c->knot_on = false; return SGP_OK; }
   HIPCHK(hipSetDevice(c->device));
@@ -997,6 +1094,7 @@ int sgp_ctx_enable_knot_grad(sgp_ctx* c, int enable) {
 }
 
 int sgp_ctx_row_bounds(sgp_ctx* c, double* lo, double* hi) {
+  MULTI_FWD(c, lo && hi ? multi_row_bounds(c->multi, lo, hi) : multi_bad_args());
   if (!c || !lo || !hi) { set_err("invalid arguments"); return SGP_EINVAL; }
   for (int q = 0; q < c->d; ++q) {
     lo[q] = c->xmin[(size_t)q];
@@ -1006,6 +1104,7 @@ int sgp_ctx_row_bounds(sgp_ctx* c, double* lo, double* hi) {
 }
 
 int sgp_knot_gradient(sgp_ctx* c, const double* bounds, double* grad_knot) {
+  MULTI_FWD(c, grad_knot ? multi_knot_gradient(c->multi, bounds, grad_knot) : multi_bad_args());
   if (!c || !grad_knot) { set_err("invalid arguments"); return SGP_EINVAL; }
   const int64_t m = c->m, d = c->d;
   if (c->knot_raw.size() != (size_t)(m * d) || c->last_mode == 0) {
@@ -1052,6 +1151,7 @@ static int k22_stage(sgp_ctx* c, double diag_sub) {
 
 int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
                   int64_t ldu, double delta, double* red1) {
+  MULTI_REFUSE(c, "sgp_vi_phase1");
   KernParams kp;
   int st = check_eval_args(c, kernel, theta, U, m, ldu, delta, &kp);
   if (st) return st;
@@ -1125,7 +1225,7 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_lo, 0));
   }
   {
-    // S into red1, and r^T r (the context's constant; the words past it are not read)
+    // S into red1, and r^T r (the context's constant; the 7 words past it zeroed)
     Scope t(c, "syrk_reduce");
     HIPCHK(launch_syrk_aug(c->K, c->n_pad, mpv, c->r, nullptr, c->slab_syrk, c->slab_syrk_cap,
                            red1, c->stream, 2, nullptr, 0, c->rr_dev, c->pack_red1));
@@ -1213,6 +1313,7 @@ static int bm_stage(sgp_ctx* c, const double* S, double s_scale, bool k22_ordere
 
 int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned flags,
                   double* red2) {
+  MULTI_REFUSE(c, "sgp_vi_phase2");
   if (!c || !red1 || !red2) { set_err("invalid arguments"); return SGP_EINVAL; }
   if (c->phase != 1) { set_err("sgp_vi_phase2 called before sgp_vi_phase1"); return SGP_EINVAL; }
   if (n_global < c->n) { set_err("n_global < local rows"); return SGP_EINVAL; }
@@ -1300,6 +1401,7 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
 }
 
 int sgp_vi_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
+  MULTI_REFUSE(c, "sgp_vi_finish");
   const bool obj_only = c && (c->flags & SGP_FLAG_OBJ_ONLY);
   if (!c || !red2 || !obj || (!grad && !obj_only)) {
     set_err("invalid arguments");
@@ -1363,6 +1465,7 @@ int sgp_vi_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
 
 int sgp_eval_vi(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
                 int64_t ldu, double delta, unsigned flags, double* obj, double* grad) {
+  MULTI_FWD(c, obj && (grad || (flags & SGP_FLAG_OBJ_ONLY)) ? multi_eval_vi(c->multi, kernel, theta, U, m, ldu, delta, flags, obj, grad) : multi_bad_args());
   if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
   int st = sgp_vi_phase1(c, kernel, theta, U, m, ldu, delta, c->red1);
   if (st) return st;
@@ -1391,6 +1494,7 @@ static int64_t fitc_rec_off(int64_t mp) { return mp * mp + mp + 8; }
 
 int sgp_fitc_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
                     int64_t ldu, double delta, double* red1) {
+  MULTI_REFUSE(c, "sgp_fitc_phase1");
   KernParams kp;
   int st = check_eval_args(c, kernel, theta, U, m, ldu, delta, &kp);
   if (st) return st;
@@ -1440,6 +1544,7 @@ int sgp_fitc_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U
 
 int sgp_fitc_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned flags,
                     double* red2) {
+  MULTI_REFUSE(c, "sgp_fitc_phase2");
   if (!c || !red1 || !red2) { set_err("invalid arguments"); return SGP_EINVAL; }
   if (c->phase != 11) { set_err("sgp_fitc_phase2 called before sgp_fitc_phase1"); return SGP_EINVAL; }
   if (n_global < c->n) { set_err("n_global < local rows"); return SGP_EINVAL; }
@@ -1516,6 +1621,7 @@ int sgp_fitc_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned f
 }
 
 int sgp_fitc_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
+  MULTI_REFUSE(c, "sgp_fitc_finish");
   const bool obj_only = c && (c->flags & SGP_FLAG_OBJ_ONLY);
   if (!c || !red2 || !obj || (!grad && !obj_only)) {
     set_err("invalid arguments");
@@ -1582,6 +1688,7 @@ int sgp_fitc_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
 
 int sgp_eval_fitc(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
                   int64_t ldu, double delta, unsigned flags, double* obj, double* grad) {
+  MULTI_FWD(c, obj && (grad || (flags & SGP_FLAG_OBJ_ONLY)) ? multi_eval_fitc(c->multi, kernel, theta, U, m, ldu, delta, flags, obj, grad) : multi_bad_args());
   if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
   int st = sgp_fitc_phase1(c, kernel, theta, U, m, ldu, delta, c->red1);
   if (st) return st;
@@ -1634,6 +1741,7 @@ static int lap_ensure(sgp_ctx* c) {
 }
 
 int sgp_lap_set_f(sgp_ctx* c, const double* f, double fill) {
+  MULTI_FWD(c, multi_lap_set_f(c->multi, f, fill));
   if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
   HIPCHK(hipSetDevice(c->device));
   int st = lap_ensure(c);
@@ -1647,6 +1755,7 @@ int sgp_lap_set_f(sgp_ctx* c, const double* f, double fill) {
 }
 
 int sgp_lap_get_grad_psi(sgp_ctx* c, double* out) {
+  MULTI_FWD(c, out ? multi_lap_get_grad_psi(c->multi, out) : multi_bad_args());
   if (!c || !out) { set_err("invalid arguments"); return SGP_EINVAL; }
   if (!c->lap_gpsi_valid) {
     set_err("no Newton-Raphson step has run since the mode was last set");
@@ -1659,6 +1768,7 @@ int sgp_lap_get_grad_psi(sgp_ctx* c, double* out) {
 }
 
 int sgp_lap_get_f(sgp_ctx* c, double* f) {
+  MULTI_FWD(c, f ? multi_lap_get_f(c->multi, f) : multi_bad_args());
   if (!c || !f) { set_err("invalid arguments"); return SGP_EINVAL; }
   HIPCHK(hipSetDevice(c->device));
   int st = lap_ensure(c);
@@ -1685,6 +1795,7 @@ static int lap_obj_partials(sgp_ctx* c, double* red, int64_t o) {
 int sgp_lap_begin(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
                   int64_t ldu, double delta, double expo, double tol, int maxit, unsigned flags,
                   double* red_out, int64_t* count) {
+  MULTI_REFUSE(c, "sgp_lap_begin");
   KernParams kp;
   int st = check_eval_args(c, kernel, theta, U, m, ldu, delta, &kp);
   if (st) return st;
@@ -1792,6 +1903,7 @@ static int lap_consume_obj(sgp_ctx* c, const double* red, int64_t o, bool first,
 
 int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* count, int* done,
                  double* obj, double* grad, int* nr_iters) {
+  MULTI_REFUSE(c, "sgp_lap_step");
   if (!c || !red_in || !red_out || !count || !done || red_in == red_out) {
     set_err("invalid arguments (red_in and red_out must be distinct device buffers)");
     return SGP_EINVAL;
@@ -2010,6 +2122,7 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
 }
 
 int sgp_lap_objective_values(sgp_ctx* c, double* out, int max_n, int* count) {
+  MULTI_FWD(c, sgp_lap_objective_values(multi_lead(c->multi), out, max_n, count));
   if (!c || !count) { set_err("invalid arguments"); return SGP_EINVAL; }
   int k = 0;
   for (double v : c->lap_objs) {
@@ -2024,6 +2137,7 @@ int sgp_lap_objective_values(sgp_ctx* c, double* out, int max_n, int* count) {
 int sgp_eval_laplace(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
                      int64_t ldu, double delta, double expo, double tol, int maxit, double* obj,
                      double* grad, int* nr_iters) {
+  MULTI_FWD(c, multi_eval_laplace(c->multi, kernel, theta, U, m, ldu, delta, expo, tol, maxit, 0u, obj, grad, nr_iters));
   if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
   HIPCHK(hipSetDevice(c->device));
   int st = lap_ensure(c);
@@ -2044,6 +2158,7 @@ int sgp_eval_laplace(sgp_ctx* c, int kernel, const double* theta, const double* 
 int sgp_lap_nr(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
                int64_t ldu, double delta, double expo, double tol, int maxit, double* obj,
                int* nr_iters) {
+  MULTI_FWD(c, multi_eval_laplace(c->multi, kernel, theta, U, m, ldu, delta, expo, tol, maxit, SGP_FLAG_OBJ_ONLY, obj, nullptr, nr_iters));
   if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
   HIPCHK(hipSetDevice(c->device));
   int st = lap_ensure(c);
@@ -2072,6 +2187,7 @@ int sgp_lap_nr(sgp_ctx* c, int kernel, const double* theta, const double* U, int
 //          G = 1/2 a a^T - 1/2 Sigma11^-1; tau's derivative is 2 tau^2 on coincident pairs.
 int sgp_eval_full(sgp_ctx* c, int kernel, const double* theta, double delta, unsigned flags,
                   double* obj, double* grad) {
+  MULTI_REFUSE(c, "sgp_eval_full (the full GP needs every row on one device)");
   if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
   const bool obj_only = (flags & SGP_FLAG_OBJ_ONLY) != 0;
   if (!obj || (!grad && !obj_only)) { set_err("invalid arguments"); return SGP_EINVAL; }
@@ -2155,6 +2271,7 @@ int sgp_eval_full(sgp_ctx* c, int kernel, const double* theta, double delta, uns
 //   Laplace (newtrap_sparseGP.R:137-176): u_mean = muu + K22 (K22+S_Z)^-1 t_Z(f_hat),
 //     u_var = K22 (K22 + S_B(W_prev))^-1 K22   (= Sigma22 + TT + TT (Sigma22 - TT)^-1 TT)
 int sgp_posterior_u(sgp_ctx* c, const double* muu, double* u_mean, double* u_var) {
+  MULTI_FWD(c, sgp_posterior_u(multi_lead(c->multi), muu, u_mean, u_var));
   if (!c || !muu || !u_mean || !u_var) { set_err("invalid arguments"); return SGP_EINVAL; }
   if (c->last_mode == 0) { set_err("no completed evaluation in this context"); return SGP_EINVAL; }
   HIPCHK(hipSetDevice(c->device));
@@ -2350,6 +2467,7 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
 int sgp_vi_candidates(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
                       int64_t ldu, double delta, unsigned flags, const double* cand, int64_t T,
                       int64_t ldc, double* obj_out) {
+  MULTI_FWD(c, cand && T >= 1 && ldc >= T && obj_out ? multi_vi_candidates(c->multi, kernel, theta, U, m, ldu, delta, flags, cand, T, ldc, obj_out) : multi_bad_args());
   if (!c || !cand || T < 1 || ldc < T || !obj_out) {
     set_err("invalid sgp_vi_candidates arguments");
     return SGP_EINVAL;
@@ -2482,6 +2600,7 @@ static void bordered_knots(const double* U, int64_t m, int64_t ldu, int d, const
 int sgp_fitc_candidates(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
                         int64_t ldu, double delta, unsigned flags, const double* cand, int64_t T,
                         int64_t ldc, double* obj_out) {
+  MULTI_FWD(c, U && cand && T >= 1 && ldc >= T && obj_out && m >= 1 && ldu >= m ? multi_fitc_candidates(c->multi, kernel, theta, U, m, ldu, delta, flags, cand, T, ldc, obj_out) : multi_bad_args());
   if (!c || !U || !cand || T < 1 || ldc < T || !obj_out || m < 1 || ldu < m) {
     set_err("invalid sgp_fitc_candidates arguments");
     return SGP_EINVAL;
@@ -2513,6 +2632,7 @@ int sgp_fitc_candidates(sgp_ctx* c, int kernel, const double* theta, const doubl
 int sgp_lap_candidates(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
                        int64_t ldu, double delta, double expo, double tol, int maxit,
                        const double* cand, int64_t T, int64_t ldc, double* obj_out) {
+  MULTI_FWD(c, U && cand && T >= 1 && ldc >= T && obj_out && m >= 1 && ldu >= m ? multi_lap_candidates(c->multi, kernel, theta, U, m, ldu, delta, expo, tol, maxit, cand, T, ldc, obj_out) : multi_bad_args());
   if (!c || !U || !cand || T < 1 || ldc < T || !obj_out || m < 1 || ldu < m) {
     set_err("invalid sgp_lap_candidates arguments");
     return SGP_EINVAL;

@@ -564,7 +564,9 @@ k_syrk_reduce_blk(const double* __restrict__ slab, int splits, int64_t nblk, int
                   int splits_d, int stride_d) {
   const int64_t bid = blockIdx.y;
   const int e = blockIdx.x * 256 + threadIdx.x;   // element of the 64 x 64 block
-  if (rr_src && bid == 0 && e == 0) *rr_dst = *rr_src;   // a precomputed r^T r
+  // a precomputed r^T r, and the 7 padding words after it zeroed (VI's red1 tail: a multi-GPU
+  // all-reduce sums them, so they must not be whatever the buffer held)
+  if (rr_src && bid == 0 && e < 8) rr_dst[e] = e == 0 ? *rr_src : 0.0;
   int rp = (int)((sqrtf(8.0f * (float)bid + 1.0f) - 1.0f) * 0.5f);
   while ((int64_t)(rp + 1) * (rp + 2) / 2 <= bid) ++rp;
   while ((int64_t)rp * (rp + 1) / 2 > bid) --rp;
@@ -1794,11 +1796,13 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
     // weights and form t); unweighted or sqrt(w)-staged S -> the balanced plan when it beats
     // the packed one (syrk_plan_bal)
     const bool wsq = w && w_nonneg && !with_t;
-    const bool use3 = !s256 && w && !wsq && SGP_SYRK_W3 && q.nb >= 3;
+    bool use3 = !s256 && w && !wsq && SGP_SYRK_W3 && q.nb >= 3;
     SyrkBal bal;
     if (use3) bal = syrk_plan_bal(n_pad, mp, syrk_dtile_cost(true, with_t != 0), true);
     else if (!s256 && !with_t) bal = syrk_plan_bal(n_pad, mp, syrk_dtile_cost(false, false), false);
-    if (use3 && !bal.on) return hipErrorInvalidValue;
+    // no balanced plan fits one residency round once the strictly-lower groups alone fill it
+    // (nb >= 32, m > 3968): the per-fragment weights on the packed plan (WMODE 1) instead
+    if (use3 && !bal.on) use3 = false;
     if (bal.on) {
       q.T = q.nb * (q.nb - 1) / 2;   // the packed kernel's strictly-lower groups only
       q.splits = bal.S_o;

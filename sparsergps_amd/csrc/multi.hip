@@ -1,0 +1,751 @@
+// Row-sharded multi-device contexts: one process, several GPUs of one node, RCCL over xGMI.
+//
+// BASELINE.json north_star / SURVEY.md sec. 8(b) and config C4: "sharding the n observation
+// rows across the 8 GPUs of one node with an RCCL all-reduce over xGMI for the Qnn-diag trace
+// term and log-likelihood accumulators", driven from host-side R through the C ABI
+// (R/optimize_gp.R:297-315 -> R/vi_functions.R:733-771 for VI, R/laplace_gradient_ascent.R:
+// 1568-1603 for FITC, R/newtrap_sparseGP.R:6-186 for Laplace).  Every n-indexed sum of the
+// reference's objective and gradient (R/vi_functions.R:87-118, 227-253;
+// R/laplace_approx_obj_funs.R:6-52; R/laplace_approx_gradient.R:25-553, 720-1135) is
+// row-separable, so an evaluation is the one-device evaluation split at its reduction points
+// (the sgp_vi_phase* / sgp_fitc_phase* / sgp_lap_begin+step entry points of capi.hip) with the
+// partial sums added up between them:
+//
+//   shard s (rows [r0_s, r1_s) on device dev_s)   phase / step -> partial buffer
+//   device g: k_sum_parts over its shards, fixed shard order    -> red_g   (on g's stream)
+//   all devices: ncclAllReduce(red_g, in place, sum)            -> every device holds the total
+//   shard s: the next phase / step reads red_g
+//
+// One host worker thread per distinct device issues its shards' work and its collective, so the
+// devices start together (a single issuing thread would stagger them by the host cost of each
+// phase); a host barrier before every collective lets all workers abandon an evaluation together
+// when one fails (none is then left waiting inside a collective).  A device may hold several
+// shards (a repeated entry in `devices`): their partials are summed by k_sum_parts before the
+// collective, which is how the 8-shard composition of C4 is tested on a one-GPU box.  All
+// decisions (the Laplace NR stop rule) are functions of the summed buffers, so every shard takes
+// the same path; the replicated m x m state of shard 0 answers the posterior, knot-gradient and
+// objective-history queries.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "sgp_internal.h"
+#include "sgp_multi.h"
+
+namespace {
+
+constexpr int ABORTED = -1;   // a worker that stopped because another one failed
+
+struct Shard {
+  sgp_ctx* ctx = nullptr;
+  int device = 0;
+  int group = 0;
+  int64_t row0 = 0, rows = 0;
+  double* part = nullptr;     // partial sums (only when its device holds more than one shard)
+};
+
+struct Group {
+  int device = 0;
+  std::vector<int> shards;
+  hipStream_t stream = nullptr;
+  ncclComm_t comm = nullptr;
+  double* red[2] = {nullptr, nullptr};   // summed buffers (ping-pong)
+  // results of the last job (every group computes the same; group 0's are returned)
+  int status = SGP_OK;
+  std::string err;
+  double obj = 0.0;
+  std::vector<double> grad;
+  int nr_iters = 0;
+};
+
+struct PartPtrs {
+  const double* p[SGP_MAX_SHARDS];
+  int k;
+};
+
+// out[i] = sum_q parts[q][i] in shard order (deterministic)
+__global__ void __launch_bounds__(256) k_sum_parts(PartPtrs pp, int64_t count, double* out) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < count;
+       i += (int64_t)gridDim.x * 256) {
+    double v = pp.p[0][i];
+    for (int q = 1; q < pp.k; ++q) v += pp.p[q][i];
+    out[i] = v;
+  }
+}
+
+std::string hip_msg(hipError_t e, const char* what) {
+  char b[256];
+  snprintf(b, sizeof(b), "HIP error '%s' in %s", hipGetErrorString(e), what);
+  return b;
+}
+
+}  // namespace
+
+struct MultiCtx {
+  std::vector<Shard> shards;
+  std::vector<Group> groups;
+  int64_t n = 0, m_max = 0, cap = 0;
+  int d = 0;
+  bool knot_on = false;
+  std::vector<double> xmin, xmax;   // column ranges of all rows
+
+  // ---- worker pool: one thread per group
+  std::vector<std::thread> threads;
+  std::mutex mu;
+  std::condition_variable cv_job, cv_done;
+  std::function<int(int)> job;
+  uint64_t job_gen = 0;
+  int pending = 0;
+  bool quit = false;
+
+  // ---- barrier with a vote (all ok? any / all done?)
+  std::mutex bmu;
+  std::condition_variable bcv;
+  int b_count = 0;
+  uint64_t b_gen = 0;
+  bool b_all_ok = true, b_any = false, b_all = true;
+  bool r_ok = true, r_any = false, r_all = true;
+
+  void worker(int g) {
+    uint64_t seen = 0;
+    for (;;) {
+      std::function<int(int)> f;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv_job.wait(lk, [&] { return quit || job_gen != seen; });
+        if (quit) return;
+        seen = job_gen;
+        f = job;
+      }
+      Group& gr = groups[(size_t)g];
+      gr.err.clear();
+      gr.status = f(g);
+      if (gr.status != SGP_OK && gr.status != ABORTED) gr.err = sgp_last_error();
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        if (--pending == 0) cv_done.notify_all();
+      }
+    }
+  }
+
+  void start_workers() {
+    for (int g = 0; g < (int)groups.size(); ++g) threads.emplace_back([this, g] { worker(g); });
+  }
+
+  void stop_workers() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      quit = true;
+    }
+    cv_job.notify_all();
+    for (std::thread& t : threads) t.join();
+    threads.clear();
+  }
+
+  // run f(g) on every group's worker and wait; the first real error is reported
+  int run_all(std::function<int(int)> f) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      job = std::move(f);
+      pending = (int)groups.size();
+      ++job_gen;
+    }
+    cv_job.notify_all();
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv_done.wait(lk, [&] { return pending == 0; });
+    }
+    int st = SGP_OK;
+    for (const Group& g : groups)
+      if (g.status != SGP_OK && g.status != ABORTED) {
+        sgp_internal_set_err(g.err.c_str());
+        return g.status;
+      }
+    for (const Group& g : groups)
+      if (g.status == ABORTED) st = SGP_EHIP;
+    if (st) sgp_internal_set_err("multi-device evaluation aborted");
+    return st;
+  }
+
+  // every worker arrives with its status (and a done flag); returns false for all when any
+  // worker failed, and sets *any_done / *all_done from the votes
+  bool arrive(bool ok, bool done = false, bool* any_done = nullptr, bool* all_done = nullptr) {
+    std::unique_lock<std::mutex> lk(bmu);
+    const uint64_t gen = b_gen;
+    b_all_ok = b_all_ok && ok;
+    b_any = b_any || done;
+    b_all = b_all && done;
+    if (++b_count == (int)groups.size()) {
+      r_ok = b_all_ok;
+      r_any = b_any;
+      r_all = b_all;
+      b_all_ok = true;
+      b_any = false;
+      b_all = true;
+      b_count = 0;
+      ++b_gen;
+      bcv.notify_all();
+    } else {
+      bcv.wait(lk, [&] { return b_gen != gen; });
+    }
+    if (any_done) *any_done = r_any;
+    if (all_done) *all_done = r_all;
+    return r_ok;
+  }
+
+  sgp_ctx* ctx(const Group& g, int q) { return shards[(size_t)g.shards[(size_t)q]].ctx; }
+  // where shard q of group g writes its partial sums (straight into the summed buffer when
+  // it is the device's only shard)
+  double* out_of(Group& g, int q, double* red) {
+    return g.shards.size() == 1 ? red : shards[(size_t)g.shards[(size_t)q]].part;
+  }
+
+  // the device's shards' partials -> red (fixed shard order)
+  void sum_parts(Group& g, double* red, int64_t count, int& st) {
+    if (st != SGP_OK || g.shards.size() < 2 || count <= 0) return;
+    PartPtrs pp{};
+    pp.k = (int)g.shards.size();
+    for (int q = 0; q < pp.k; ++q) pp.p[q] = shards[(size_t)g.shards[(size_t)q]].part;
+    int64_t nb = (count + 255) / 256;
+    if (nb > 4096) nb = 4096;
+    hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)nb), dim3(256), 0, g.stream, pp, count, red);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      sgp_internal_set_err(hip_msg(e, "k_sum_parts").c_str());
+      st = SGP_EHIP;
+    }
+  }
+
+  // the all-reduce over the devices, in place on the device's stream
+  void all_reduce(Group& g, double* red, int64_t count, int& st) {
+    if (st != SGP_OK || count <= 0) return;
+    const ncclResult_t r = ncclAllReduce(red, red, (size_t)count, ncclDouble, ncclSum, g.comm,
+                                         g.stream);
+    if (r != ncclSuccess) {
+      char b[256];
+      snprintf(b, sizeof(b), "RCCL all-reduce failed: %s", ncclGetErrorString(r));
+      sgp_internal_set_err(b);
+      st = SGP_EHIP;
+    }
+  }
+
+  // partials summed on the device, a barrier, then the collective.  false: some worker failed
+  // before the barrier, stop now (nobody enters the collective).  A failure of the collective
+  // itself is left in st and stops every worker at the next barrier (or ends the job), so no
+  // worker is ever left waiting at a barrier the failed one will not reach.
+  bool reduce(Group& g, double* red, int64_t count, int& st) {
+    sum_parts(g, red, count, st);
+    if (!arrive(st == SGP_OK)) return false;
+    all_reduce(g, red, count, st);
+    return true;
+  }
+
+  int set_dev(const Group& g) {
+    const hipError_t e = hipSetDevice(g.device);
+    if (e != hipSuccess) {
+      sgp_internal_set_err(hip_msg(e, "hipSetDevice").c_str());
+      return SGP_EHIP;
+    }
+    return SGP_OK;
+  }
+
+  void release() {
+    if (!threads.empty()) stop_workers();
+    for (Group& g : groups) {
+      (void)hipSetDevice(g.device);
+      if (g.stream) (void)hipStreamSynchronize(g.stream);
+    }
+    for (Shard& s : shards) {
+      if (s.ctx) sgp_ctx_destroy(s.ctx);
+      s.ctx = nullptr;
+    }
+    for (Group& g : groups) {
+      (void)hipSetDevice(g.device);
+      if (g.comm) ncclCommDestroy(g.comm);
+      for (double*& p : g.red)
+        if (p) (void)hipFree(p);
+      if (g.stream) (void)hipStreamDestroy(g.stream);
+    }
+    for (Shard& s : shards)
+      if (s.part) {
+        (void)hipSetDevice(s.device);
+        (void)hipFree(s.part);
+      }
+    groups.clear();
+    shards.clear();
+  }
+};
+
+// ------------------------------------------------------------------------------ creation
+int multi_create(MultiCtx** out, const int* devices, int nshards, const double* X, int64_t n,
+                 int64_t ldx, int d, const double* y, const double* mu, int64_t m_max) {
+  *out = nullptr;
+  MultiCtx* mc = new MultiCtx();
+  mc->n = n;
+  mc->d = d;
+  mc->m_max = m_max;
+  // every reduction an evaluation issues fits one buffer (ARD has the most parameters)
+  const int64_t extra = sgp_knot_red_extra(d, m_max);
+  int64_t cap = sgp_lap_red_count(SGP_KERNEL_ARD, d, m_max);
+  cap = std::max<int64_t>(cap, sgp_fitc_red2_count(SGP_KERNEL_ARD, d, m_max) + extra);
+  cap = std::max<int64_t>(cap, sgp_vi_red1_count(m_max));
+  cap = std::max<int64_t>(cap, sgp_vi_red2_count(SGP_KERNEL_ARD, d) + extra);
+  mc->cap = cap;
+  // shards: contiguous row blocks as dist.shard_rows(n, N, k); groups: distinct devices in
+  // order of first appearance
+  const int64_t base = n / nshards, rem = n % nshards;
+  int64_t r0 = 0;
+  for (int k = 0; k < nshards; ++k) {
+    Shard s;
+    s.device = devices ? devices[k] : k;
+    s.row0 = r0;
+    s.rows = base + (k < rem ? 1 : 0);
+    r0 += s.rows;
+    int g = 0;
+    while (g < (int)mc->groups.size() && mc->groups[(size_t)g].device != s.device) ++g;
+    if (g == (int)mc->groups.size()) {
+      Group gr;
+      gr.device = s.device;
+      mc->groups.push_back(gr);
+    }
+    s.group = g;
+    mc->groups[(size_t)g].shards.push_back(k);
+    mc->shards.push_back(s);
+  }
+  mc->xmin.assign((size_t)d, 0.0);
+  mc->xmax.assign((size_t)d, 0.0);
+  for (int q = 0; q < d; ++q) {
+    double lo = X[q * ldx], hi = X[q * ldx];
+    for (int64_t i = 1; i < n; ++i) {
+      const double v = X[i + q * ldx];
+      lo = v < lo ? v : lo;
+      hi = v > hi ? v : hi;
+    }
+    mc->xmin[(size_t)q] = lo;
+    mc->xmax[(size_t)q] = hi;
+  }
+  // per device: stream, summed buffers, the shards' partial buffers
+  int st = SGP_OK;
+  for (Group& g : mc->groups) {
+    hipError_t e = hipSetDevice(g.device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking);
+    for (int b = 0; b < 2 && e == hipSuccess; ++b)
+      e = hipMalloc(reinterpret_cast<void**>(&g.red[b]), sizeof(double) * (size_t)cap);
+    for (size_t q = 0; q < g.shards.size() && g.shards.size() > 1 && e == hipSuccess; ++q)
+      e = hipMalloc(reinterpret_cast<void**>(&mc->shards[(size_t)g.shards[q]].part),
+                    sizeof(double) * (size_t)cap);
+    for (int b = 0; b < 2 && e == hipSuccess; ++b)
+      e = hipMemset(g.red[b], 0, sizeof(double) * (size_t)cap);
+    if (e != hipSuccess) {
+      sgp_internal_set_err(hip_msg(e, "multi-device context set-up").c_str());
+      st = e == hipErrorOutOfMemory ? SGP_ENOMEM : SGP_EHIP;
+      break;
+    }
+  }
+  // one RCCL communicator per distinct device, all in this process
+  if (!st) {
+    std::vector<ncclComm_t> comms(mc->groups.size());
+    std::vector<int> devs;
+    for (const Group& g : mc->groups) devs.push_back(g.device);
+    const ncclResult_t r = ncclCommInitAll(comms.data(), (int)devs.size(), devs.data());
+    if (r != ncclSuccess) {
+      char b[256];
+      snprintf(b, sizeof(b), "ncclCommInitAll over %d devices failed: %s", (int)devs.size(),
+               ncclGetErrorString(r));
+      sgp_internal_set_err(b);
+      st = SGP_EHIP;
+    } else {
+      for (size_t g = 0; g < comms.size(); ++g) mc->groups[g].comm = comms[g];
+    }
+  }
+  if (st) {
+    mc->release();
+    delete mc;
+    return st;
+  }
+  mc->start_workers();
+  // the shards' contexts, created by their device's worker (uploads run side by side)
+  st = mc->run_all([&](int gi) {
+    Group& g = mc->groups[(size_t)gi];
+    int s2 = mc->set_dev(g);
+    for (size_t q = 0; q < g.shards.size() && !s2; ++q) {
+      Shard& s = mc->shards[(size_t)g.shards[q]];
+      s2 = sgp_ctx_create(&s.ctx, s.device, X + s.row0, s.rows, ldx, d, y + s.row0, mu + s.row0,
+                          m_max);
+      if (!s2) s2 = sgp_ctx_set_stream(s.ctx, g.stream);
+      if (!s2) s2 = sgp_ctx_set_packed_reduction(s.ctx, 1);   // all-reduce #1: 53 % of S
+    }
+    return s2;
+  });
+  if (st) {
+    mc->release();
+    delete mc;
+    return st;
+  }
+  *out = mc;
+  return SGP_OK;
+}
+
+void multi_destroy(MultiCtx* mc) {
+  if (!mc) return;
+  mc->release();
+  delete mc;
+}
+
+int multi_shards(const MultiCtx* mc, int* nshards, int* ndevices) {
+  if (nshards) *nshards = (int)mc->shards.size();
+  if (ndevices) *ndevices = (int)mc->groups.size();
+  return SGP_OK;
+}
+
+sgp_ctx* multi_lead(MultiCtx* mc) { return mc->shards[0].ctx; }
+
+int multi_set_data(MultiCtx* mc, const double* y, const double* mu) {
+  for (Shard& s : mc->shards) {
+    const int st = sgp_ctx_set_data(s.ctx, y + s.row0, mu + s.row0);
+    if (st) return st;
+  }
+  return SGP_OK;
+}
+
+// ------------------------------------------------------------------------------ VI / FITC
+namespace {
+
+struct EvalArgs {
+  int kernel;
+  const double* theta;
+  const double* U;
+  int64_t m, ldu;
+  double delta;
+  unsigned flags;
+  // Laplace
+  double expo = 1.0, tol = 0.0;
+  int maxit = 0;
+};
+
+// VI (fitc = false) or FITC: phase 1 -> all-reduce #1 -> phase 2 -> all-reduce #2 -> finish
+int two_phase_job(MultiCtx* mc, int gi, const EvalArgs& a, bool fitc) {
+  Group& g = mc->groups[(size_t)gi];
+  int st = mc->set_dev(g);
+  const int k = (int)g.shards.size();
+  const int npar = sgp_num_params(a.kernel, mc->d);
+  const bool obj_only = (a.flags & SGP_FLAG_OBJ_ONLY) != 0;
+  const int64_t c1 = fitc ? sgp_fitc_red1_count(a.m) : sgp_vi_red1_packed_count(a.m);
+  for (int q = 0; q < k && !st; ++q) {
+    double* o = mc->out_of(g, q, g.red[0]);
+    st = fitc ? sgp_fitc_phase1(mc->ctx(g, q), a.kernel, a.theta, a.U, a.m, a.ldu, a.delta, o)
+              : sgp_vi_phase1(mc->ctx(g, q), a.kernel, a.theta, a.U, a.m, a.ldu, a.delta, o);
+  }
+  if (!mc->reduce(g, g.red[0], c1, st)) return st ? st : ABORTED;
+  for (int q = 0; q < k && !st; ++q) {
+    double* o = mc->out_of(g, q, g.red[1]);
+    st = fitc ? sgp_fitc_phase2(mc->ctx(g, q), g.red[0], mc->n, a.flags, o)
+              : sgp_vi_phase2(mc->ctx(g, q), g.red[0], mc->n, a.flags, o);
+  }
+  // the objective alone leaves the second buffer unwritten: nothing to sum
+  const int64_t extra = mc->knot_on ? sgp_knot_red_extra(mc->d, a.m) : 0;
+  const int64_t c2 = obj_only ? 0
+                              : (fitc ? sgp_fitc_red2_count(a.kernel, mc->d, a.m)
+                                      : sgp_vi_red2_count(a.kernel, mc->d)) + extra;
+  if (!mc->reduce(g, g.red[1], c2, st)) return st ? st : ABORTED;
+  if (st) return st;
+  g.grad.assign((size_t)(npar > 0 ? npar : 1), 0.0);
+  std::vector<double> tmp(g.grad.size());
+  for (int q = 0; q < k && !st; ++q) {
+    double o = 0.0;
+    double* gp = obj_only ? nullptr : (q == 0 ? g.grad.data() : tmp.data());
+    st = fitc ? sgp_fitc_finish(mc->ctx(g, q), g.red[1], &o, gp)
+              : sgp_vi_finish(mc->ctx(g, q), g.red[1], &o, gp);
+    if (q == 0) g.obj = o;
+  }
+  return st;
+}
+
+int copy_result(MultiCtx* mc, int st, double* obj, double* grad, int npar) {
+  if (st) return st;
+  const Group& g = mc->groups[0];
+  *obj = g.obj;
+  if (grad)
+    for (int p = 0; p < npar; ++p) grad[p] = g.grad[(size_t)p];
+  return SGP_OK;
+}
+
+}  // namespace
+
+int multi_eval_vi(MultiCtx* mc, int kernel, const double* theta, const double* U, int64_t m,
+                  int64_t ldu, double delta, unsigned flags, double* obj, double* grad) {
+  const EvalArgs a{kernel, theta, U, m, ldu, delta, flags};
+  const int st = mc->run_all([&](int gi) { return two_phase_job(mc, gi, a, false); });
+  return copy_result(mc, st, obj, (flags & SGP_FLAG_OBJ_ONLY) ? nullptr : grad,
+                     sgp_num_params(kernel, mc->d));
+}
+
+int multi_eval_fitc(MultiCtx* mc, int kernel, const double* theta, const double* U, int64_t m,
+                    int64_t ldu, double delta, unsigned flags, double* obj, double* grad) {
+  const EvalArgs a{kernel, theta, U, m, ldu, delta, flags};
+  const int st = mc->run_all([&](int gi) { return two_phase_job(mc, gi, a, true); });
+  return copy_result(mc, st, obj, (flags & SGP_FLAG_OBJ_ONLY) ? nullptr : grad,
+                     sgp_num_params(kernel, mc->d));
+}
+
+// ------------------------------------------------------------------------------ Laplace
+namespace {
+
+// sgp_lap_begin -> all-reduce -> (sgp_lap_step -> all-reduce)* until done: the NR iterations'
+// two exchanges and the gradient's two
+int laplace_job(MultiCtx* mc, int gi, const EvalArgs& a) {
+  Group& g = mc->groups[(size_t)gi];
+  int st = mc->set_dev(g);
+  const int k = (int)g.shards.size();
+  const int npar = sgp_num_params(a.kernel, mc->d);
+  int64_t count = -1;
+  for (int q = 0; q < k && !st; ++q) {
+    int64_t cq = 0;
+    st = sgp_lap_begin(mc->ctx(g, q), a.kernel, a.theta, a.U, a.m, a.ldu, a.delta, a.expo, a.tol,
+                       a.maxit, a.flags, mc->out_of(g, q, g.red[0]), &cq);
+    if (!st && count >= 0 && cq != count) {
+      sgp_internal_set_err("Laplace shards disagree on the reduction size");
+      st = SGP_EINVAL;
+    }
+    count = cq;
+  }
+  if (!mc->reduce(g, g.red[0], count, st)) return st ? st : ABORTED;
+  g.grad.assign((size_t)(npar > 0 ? npar : 1), 0.0);
+  std::vector<double> tmp(g.grad.size());
+  int cur = 0;
+  for (;;) {
+    bool done = false;
+    int64_t cnt = -1;
+    for (int q = 0; q < k && !st; ++q) {
+      int64_t cq = 0;
+      int dq = 0, it = 0;
+      double o = 0.0;
+      st = sgp_lap_step(mc->ctx(g, q), g.red[cur], mc->out_of(g, q, g.red[cur ^ 1]), &cq, &dq,
+                        &o, q == 0 ? g.grad.data() : tmp.data(), &it);
+      if (st) break;
+      if ((q > 0 && ((dq != 0) != done || cq != cnt))) {
+        sgp_internal_set_err("Laplace shards disagree on the NR state");
+        st = SGP_EINVAL;
+        break;
+      }
+      done = dq != 0;
+      cnt = cq;
+      if (q == 0) {
+        g.obj = o;
+        g.nr_iters = it;
+      }
+    }
+    if (st) {
+      mc->arrive(false, done);
+      return st;
+    }
+    if (done) {
+      // every device must stop here too (the stop rule reads summed buffers only)
+      bool any = false, all = false;
+      if (!mc->arrive(true, true, &any, &all)) return ABORTED;
+      if (!all) {
+        sgp_internal_set_err("Laplace devices disagree on the NR stop rule");
+        return SGP_EINVAL;
+      }
+      return SGP_OK;
+    }
+    // the partials -> the other buffer, summed over the device's shards and the devices (this
+    // device votes "not done" at the barrier; a collective failure stops every worker at the
+    // next barrier, after the next steps are skipped)
+    mc->sum_parts(g, g.red[cur ^ 1], cnt, st);
+    bool any = false;
+    if (!mc->arrive(st == SGP_OK, false, &any)) return st ? st : ABORTED;
+    if (any) {
+      sgp_internal_set_err("Laplace devices disagree on the NR stop rule");
+      return SGP_EINVAL;
+    }
+    mc->all_reduce(g, g.red[cur ^ 1], cnt, st);
+    cur ^= 1;
+  }
+}
+
+}  // namespace
+
+int multi_eval_laplace(MultiCtx* mc, int kernel, const double* theta, const double* U,
+                       int64_t m, int64_t ldu, double delta, double expo, double tol, int maxit,
+                       unsigned flags, double* obj, double* grad, int* nr_iters) {
+  EvalArgs a{kernel, theta, U, m, ldu, delta, flags};
+  a.expo = expo;
+  a.tol = tol;
+  a.maxit = maxit;
+  const int st = mc->run_all([&](int gi) { return laplace_job(mc, gi, a); });
+  if (st) return st;
+  const Group& g = mc->groups[0];
+  if (obj) *obj = g.obj;
+  if (nr_iters) *nr_iters = g.nr_iters;
+  if (grad && !(flags & SGP_FLAG_OBJ_ONLY))
+    for (int p = 0; p < sgp_num_params(kernel, mc->d); ++p) grad[p] = g.grad[(size_t)p];
+  return SGP_OK;
+}
+
+// the latent vector f in the global row order
+int multi_lap_set_f(MultiCtx* mc, const double* f, double fill) {
+  for (Shard& s : mc->shards) {
+    const int st = sgp_lap_set_f(s.ctx, f ? f + s.row0 : nullptr, fill);
+    if (st) return st;
+  }
+  return SGP_OK;
+}
+
+int multi_lap_get_f(MultiCtx* mc, double* f) {
+  for (Shard& s : mc->shards) {
+    const int st = sgp_lap_get_f(s.ctx, f + s.row0);
+    if (st) return st;
+  }
+  return SGP_OK;
+}
+
+int multi_lap_get_grad_psi(MultiCtx* mc, double* out) {
+  for (Shard& s : mc->shards) {
+    const int st = sgp_lap_get_grad_psi(s.ctx, out + s.row0);
+    if (st) return st;
+  }
+  return SGP_OK;
+}
+
+// ------------------------------------------------------------------------------ knots
+int multi_enable_knot_grad(MultiCtx* mc, int enable) {
+  for (Shard& s : mc->shards) {
+    const int st = sgp_ctx_enable_knot_grad(s.ctx, enable);
+    if (st) return st;
+  }
+  mc->knot_on = enable != 0;
+  return SGP_OK;
+}
+
+int multi_row_bounds(MultiCtx* mc, double* lo, double* hi) {
+  for (int q = 0; q < mc->d; ++q) {
+    lo[q] = mc->xmin[(size_t)q];
+    hi[q] = mc->xmax[(size_t)q];
+  }
+  return SGP_OK;
+}
+
+// bounds NULL: the reference's knot_bounds over ALL rows (vi_functions.R:175-178), not shard 0's
+int multi_knot_gradient(MultiCtx* mc, const double* bounds, double* grad_knot) {
+  std::vector<double> b;
+  if (!bounds) {
+    const int d = mc->d;
+    b.assign((size_t)(2 * d), 0.0);
+    for (int q = 0; q < d; ++q) {
+      const double diff = mc->xmax[(size_t)q] - mc->xmin[(size_t)q];
+      b[(size_t)q] = mc->xmin[(size_t)q] - diff / 10;
+      b[(size_t)(d + q)] = mc->xmax[(size_t)q] + diff / 10;
+    }
+    bounds = b.data();
+  }
+  return sgp_knot_gradient(multi_lead(mc), bounds, grad_knot);
+}
+
+// ------------------------------------------------------------------------------ candidates
+namespace {
+
+void bordered(const double* U, int64_t m, int64_t ldu, int d, const double* cand, int64_t t,
+              int64_t ldc, std::vector<double>& Ub) {
+  Ub.resize((size_t)((m + 1) * d));
+  for (int q = 0; q < d; ++q) {
+    for (int64_t k = 0; k < m; ++k) Ub[(size_t)(k + q * (m + 1))] = U[k + q * ldu];
+    Ub[(size_t)(m + q * (m + 1))] = cand[t + q * ldc];
+  }
+}
+
+void forget_all(MultiCtx* mc) {
+  for (Shard& s : mc->shards) sgp_internal_forget_eval(s.ctx);
+}
+
+}  // namespace
+
+// VI / FITC meta-model values: the objective-only evaluation at [U; cand_t] over all shards
+// (NaN = the reference's try-error).  A VI candidate costs one objective-only evaluation here
+// rather than the bordered Schur update of the one-device scorer.
+static int cand_loop(MultiCtx* mc, bool fitc, int kernel, const double* theta, const double* U,
+                     int64_t m, int64_t ldu, double delta, unsigned flags, const double* cand,
+                     int64_t T, int64_t ldc, double* obj_out) {
+  if (m + 1 > mc->m_max) {
+    char b[160];
+    snprintf(b, sizeof(b), "m + 1 = %lld knots exceed the context's m_max = %lld",
+             (long long)(m + 1), (long long)mc->m_max);
+    sgp_internal_set_err(b);
+    return SGP_EINVAL;
+  }
+  std::vector<double> Ub;
+  int st = SGP_OK;
+  for (int64_t t = 0; t < T && !st; ++t) {
+    bordered(U, m, ldu, mc->d, cand, t, ldc, Ub);
+    double o = 0.0;
+    st = fitc ? multi_eval_fitc(mc, kernel, theta, Ub.data(), m + 1, m + 1, delta,
+                                flags | SGP_FLAG_OBJ_ONLY, &o, nullptr)
+              : multi_eval_vi(mc, kernel, theta, Ub.data(), m + 1, m + 1, delta,
+                              flags | SGP_FLAG_OBJ_ONLY, &o, nullptr);
+    if (st == SGP_ENOTPD) {
+      obj_out[t] = NAN;
+      st = SGP_OK;
+    } else if (!st) {
+      obj_out[t] = o;
+    }
+  }
+  forget_all(mc);
+  return st;
+}
+
+int multi_vi_candidates(MultiCtx* mc, int kernel, const double* theta, const double* U,
+                        int64_t m, int64_t ldu, double delta, unsigned flags, const double* cand,
+                        int64_t T, int64_t ldc, double* obj_out) {
+  return cand_loop(mc, false, kernel, theta, U, m, ldu, delta, flags, cand, T, ldc, obj_out);
+}
+
+int multi_fitc_candidates(MultiCtx* mc, int kernel, const double* theta, const double* U,
+                          int64_t m, int64_t ldu, double delta, unsigned flags,
+                          const double* cand, int64_t T, int64_t ldc, double* obj_out) {
+  return cand_loop(mc, true, kernel, theta, U, m, ldu, delta, flags, cand, T, ldc, obj_out);
+}
+
+// Laplace: newtrap_sparseGP at [U; cand_t] from the same f every time (the fit's fmax), f
+// restored afterwards
+int multi_lap_candidates(MultiCtx* mc, int kernel, const double* theta, const double* U,
+                         int64_t m, int64_t ldu, double delta, double expo, double tol,
+                         int maxit, const double* cand, int64_t T, int64_t ldc,
+                         double* obj_out) {
+  if (m + 1 > mc->m_max) {
+    char b[160];
+    snprintf(b, sizeof(b), "m + 1 = %lld knots exceed the context's m_max = %lld",
+             (long long)(m + 1), (long long)mc->m_max);
+    sgp_internal_set_err(b);
+    return SGP_EINVAL;
+  }
+  std::vector<double> f0((size_t)mc->n);
+  int st = multi_lap_get_f(mc, f0.data());
+  if (st) return st;
+  std::vector<double> Ub;
+  for (int64_t t = 0; t < T && !st; ++t) {
+    bordered(U, m, ldu, mc->d, cand, t, ldc, Ub);
+    if (t > 0) st = multi_lap_set_f(mc, f0.data(), 0.0);
+    if (st) break;
+    double o = 0.0;
+    int it = 0;
+    st = multi_eval_laplace(mc, kernel, theta, Ub.data(), m + 1, m + 1, delta, expo, tol, maxit,
+                            SGP_FLAG_OBJ_ONLY, &o, nullptr, &it);
+    if (st == SGP_ENOTPD) {
+      obj_out[t] = NAN;
+      st = SGP_OK;
+    } else if (!st) {
+      obj_out[t] = o;
+    }
+  }
+  const int st2 = multi_lap_set_f(mc, f0.data(), 0.0);
+  forget_all(mc);
+  return st ? st : st2;
+}

@@ -38,7 +38,10 @@ def param_names(cov_fun, d, lnames=None):
 class SparseGPContext:
     """Device-resident rows (X, y - mu) plus work space for up to ``m_max`` knots."""
 
-    def __init__(self, xy, y, mu, m_max, device=None, stream=None):
+    def __init__(self, xy, y, mu, m_max, device=None, stream=None, devices=None):
+        """devices: a list of device indices, one per row shard (repeats allowed) -- a
+        row-sharded multi-device context (sgp_ctx_create_multi: the reductions, RCCL over the
+        distinct devices included, run inside libsgp); None: one device."""
         if mu is None:
             raise ValueError("SparseGPContext: mu is required (mean(y) for VI / FITC, "
                              "log mean(y) for Poisson Laplace)")
@@ -51,9 +54,17 @@ class SparseGPContext:
         self.m_max = int(m_max)
         self.device = _device() if device is None else int(device)
         h = C.c_void_p()
-        _lib.check(self._lib.sgp_ctx_create(C.byref(h), self.device, _lib.dptr(X), self.n,
-                                            self.n, self.d, _lib.dptr(y), _lib.dptr(mu),
-                                            self.m_max))
+        self.devices = None
+        if devices is not None:
+            self.devices = [int(v) for v in devices]
+            dv = (C.c_int * len(self.devices))(*self.devices)
+            _lib.check(self._lib.sgp_ctx_create_multi(C.byref(h), dv, len(self.devices),
+                                                      _lib.dptr(X), self.n, self.n, self.d,
+                                                      _lib.dptr(y), _lib.dptr(mu), self.m_max))
+        else:
+            _lib.check(self._lib.sgp_ctx_create(C.byref(h), self.device, _lib.dptr(X), self.n,
+                                                self.n, self.d, _lib.dptr(y), _lib.dptr(mu),
+                                                self.m_max))
         self._h = h
         if stream is not None:
             self.set_stream(stream)
@@ -64,6 +75,12 @@ class SparseGPContext:
         if self._h is None:
             raise RuntimeError("SparseGPContext is closed")
         return self._h
+
+    def shards(self):
+        """(row shards, distinct devices) of this context"""
+        ns, nd = C.c_int(0), C.c_int(0)
+        _lib.check(self._lib.sgp_ctx_shards(self.handle, C.byref(ns), C.byref(nd)))
+        return ns.value, nd.value
 
     def set_stream(self, stream):
         """stream: an int hipStream_t handle (e.g. torch.cuda.current_stream().cuda_stream)."""

@@ -146,6 +146,15 @@ static void einval_checks(void) {
   EINVAL_(sgp_ctx_create(&ctx, 0, x, 4, 4, 33, x, x, 4));
   EINVAL_(sgp_ctx_create(&ctx, 0, x, 4, 4, 1, NULL, x, 4));
   EINVAL_(sgp_ctx_create(NULL, 0, x, 4, 4, 1, x, x, 4));
+  {
+    const int dv[3] = {0, -1, 0};
+    EINVAL_(sgp_ctx_create_multi(&ctx, NULL, 0, x, 4, 4, 1, x, x, 4));
+    EINVAL_(sgp_ctx_create_multi(&ctx, NULL, 5, x, 4, 4, 1, x, x, 4));
+    EINVAL_(sgp_ctx_create_multi(&ctx, dv, 3, x, 4, 4, 1, x, x, 4));
+    EINVAL_(sgp_ctx_create_multi(&ctx, NULL, 2, x, 4, 4, 33, x, x, 4));
+    EINVAL_(sgp_ctx_create_multi(NULL, NULL, 2, x, 4, 4, 1, x, x, 4));
+    EINVAL_(sgp_ctx_shards(NULL, NULL, NULL));
+  }
   CHECK(ctx == NULL, "ctx written on failure");
   EINVAL_(sgp_make_cov(0, 1, x, 4, 2, NULL, 0, 0, 2, th, 1e-6, buf, 4));
   EINVAL_(sgp_make_cov(0, 1, x, -1, 1, NULL, 0, 0, 2, th, 1e-6, buf, 4));

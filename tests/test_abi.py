@@ -124,3 +124,30 @@ def test_product_path_fails_loudly_without_gpu():
         S.make_cov_matC(np.ones((3, 1)), None, {"sigma": 1, "l": 1, "tau": 0.1}, "sqexp", 1e-6)
     with pytest.raises(RuntimeError):
         S.SparseGPContext(np.ones((3, 1)), np.ones(3), 0.0, 4)
+
+
+def test_multi_context_argument_validation(lib):
+    """sgp_ctx_create_multi's argument checks run before any device call (SGP_EINVAL with a
+    message), so they are testable here; with valid arguments and no GPU it fails loudly."""
+    from sparsergps_amd import _lib
+    X = np.zeros((10, 2), order="F")
+    y = np.zeros(10)
+    h = C.c_void_p()
+
+    def create(devs, nshards, n=10, d=2, m_max=8, x=X):
+        dv = None if devs is None else (C.c_int * len(devs))(*devs)
+        return lib.sgp_ctx_create_multi(C.byref(h), dv, nshards, _lib.dptr(x), n, n, d,
+                                        _lib.dptr(y), _lib.dptr(y), m_max)
+
+    for args in ((None, 0), (None, 65), ([0] * 11, 11), (None, 2, 10, 0), (None, 2, 10, 2, 0),
+                 (None, 2, 10, 33)):
+        assert create(*args) == _lib.SGP_EINVAL, args
+        assert b"sgp_ctx_create_multi" in lib.sgp_last_error()
+    assert create([0, -1], 2) == _lib.SGP_EINVAL and b"device -1" in lib.sgp_last_error()
+    assert h.value is None
+    n = C.c_int(0)
+    if lib.sgp_device_count(C.byref(n)) != _lib.SGP_OK or n.value == 0:
+        assert create([0, 0], 2) == _lib.SGP_EHIP     # no device: no context, no fallback
+        assert h.value is None
+    ns, nd = C.c_int(0), C.c_int(0)
+    assert lib.sgp_ctx_shards(None, C.byref(ns), C.byref(nd)) == _lib.SGP_EINVAL

@@ -1,0 +1,239 @@
+"""The in-library multi-device context (sgp_ctx_create_multi, multi.hip) on the GPU.
+
+The north star's C4 path -- the n rows sharded over the GPUs of one node, the row sums combined
+by an RCCL all-reduce -- driven entirely by libsgp (no torch, no Python collective), as an R
+process calling the .Call shim uses it.  On a one-GPU box:
+* devices = [0]: one shard, its reductions through the in-library RCCL all-reduce (a one-rank
+  communicator from ncclCommInitAll) -- against the golden fixtures (literal oracle) and the
+  one-device context;
+* devices = [0] * N: N row shards on one GPU; their partial sums are added on the device
+  (k_sum_parts, fixed order) before the all-reduce.  At C4's own split (8 x 125 000 rows of
+  configs[2]) the result must equal the n = 1e6 answer: the row-chunked CPU model
+  (oracle/adjoint_chunked, pinned to the literal oracle by tests/test_oracle.py) and the one-
+  context run.
+Reference: the n-indexed sums of R/vi_functions.R:87-118, 227-253 (VI),
+R/laplace_approx_obj_funs.R:6-52 + R/laplace_approx_gradient.R:720-1135 (FITC),
+R/newtrap_sparseGP.R:6-186 + R/laplace_approx_gradient.R:25-553 (Laplace); callers
+R/optimize_gp.R:297-315, 376-394, 459-493.
+"""
+import glob
+import os
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+OBJ_RTOL, GRAD_RTOL = 1e-9, 1e-7     # against the oracle / its fixtures (verdict r4 item 1)
+SAME_RTOL = 1e-11                    # one context vs the shards of the same rows
+
+
+@pytest.fixture(scope="module")
+def sgp():
+    import sparsergps_amd as S
+    from sparsergps_amd import _lib
+    _lib.require_gpu()
+    return S
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b) / np.maximum(1.0, np.abs(b))))
+
+
+def _cp(z):
+    return OrderedDict(zip([str(s) for s in z["names"]], z["theta"]))
+
+
+GAUSS = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLD, "gauss_*.npz")))
+POIS = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLD, "poisson_*.npz")))
+
+
+@pytest.mark.parametrize("name", GAUSS)
+def test_one_device_rccl_against_golden(sgp, name):
+    """devices = [0]: VI and FITC through the in-library RCCL path vs the frozen oracle."""
+    z = np.load(os.path.join(GOLD, name))
+    th, cf = np.asarray(z["theta"], dtype=np.float64), str(z["cov_fun"])
+    delta = float(z["delta"])
+    with sgp.SparseGPContext(z["X"], z["y"], z["mu"], m_max=z["U"].shape[0],
+                             devices=[0]) as ctx, \
+            sgp.SparseGPContext(z["X"], z["y"], z["mu"], m_max=z["U"].shape[0]) as one:
+        assert ctx.shards() == (1, 1)
+        for ev, key in (("eval_vi", "vi"), ("eval_fitc", "fitc")):
+            o, g = getattr(ctx, ev)(th, cf, z["U"], delta)
+            assert abs(o - float(z[f"{key}_obj"])) / abs(float(z[f"{key}_obj"])) < OBJ_RTOL, ev
+            assert _rel(g, z[f"{key}_grad"]) < GRAD_RTOL, ev
+            o1, g1 = getattr(one, ev)(th, cf, z["U"], delta)
+            assert abs(o - o1) / abs(o1) < SAME_RTOL and _rel(g, g1) < SAME_RTOL, ev
+
+
+@pytest.mark.parametrize("name", POIS)
+def test_one_device_rccl_laplace_against_golden(sgp, name):
+    z = np.load(os.path.join(GOLD, name))
+    th = np.asarray(z["theta"], dtype=np.float64)
+    with sgp.SparseGPContext(z["X"], z["y"], z["mu"], m_max=z["U"].shape[0],
+                             devices=[0]) as ctx:
+        ctx.lap_set_f(z["f0"])
+        o, g, it = ctx.eval_laplace(th, "sqexp", z["U"], float(z["delta"]), float(z["a"]), 1e-5)
+        tr = z["obj_trace"]
+        assert it == len(tr)
+        np.testing.assert_allclose(ctx.lap_objective_values(), tr, rtol=1e-9, atol=0)
+        assert np.max(np.abs(ctx.lap_get_f() - z["ff"])) < 1e-8
+        assert _rel(g, z["grad"]) < GRAD_RTOL
+
+
+def _shards_vs_one(sgp, P, cov, devices, knots=False):
+    th = np.array(list(P["cov_par"].values()))
+    m = P["U"].shape[0]
+    out = {}
+    for key, dv in (("one", None), ("multi", devices)):
+        with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=m + 1, devices=dv) as c:
+            if knots:
+                c.enable_knot_grad(True)
+            r = {"vi": c.eval_vi(th, cov, P["U"], P["delta"])}
+            if knots:
+                r["vi_knots"] = c.knot_gradient(None)
+                r["vi_post"] = c.posterior_u(np.zeros(m))
+            r["fitc"] = c.eval_fitc(th, cov, P["U"], P["delta"])
+            if knots:
+                r["fitc_knots"] = c.knot_gradient(None)
+            r["vi_obj_only"] = c.eval_vi(th, cov, P["U"], P["delta"], obj_only=True)[0]
+            out[key] = r
+    return out
+
+
+@pytest.mark.parametrize("devices", [[0] * 8, [0] * 3])
+def test_shards_on_one_device_match_one_context(sgp, devices):
+    """Ragged row blocks (n not a multiple of the shard count) on one GPU, sqexp and ARD, with
+    knot gradients (global knot bounds) and the knot posterior: the shard sums equal the one-
+    context evaluation."""
+    from sparsergps_amd.workloads import make_gaussian_problem
+    for cfg, cov in (("C2", "sqexp"), ("C3", "ard")):
+        P = make_gaussian_problem(cfg, n=20_003, m=200)
+        r = _shards_vs_one(sgp, P, cov, devices, knots=True)
+        a, b = r["multi"], r["one"]
+        for k in ("vi", "fitc"):
+            assert abs(a[k][0] - b[k][0]) / abs(b[k][0]) < SAME_RTOL, (cfg, k)
+            assert _rel(a[k][1], b[k][1]) < SAME_RTOL, (cfg, k)
+            assert _rel(a[k + "_knots"], b[k + "_knots"]) < 1e-9, (cfg, k)
+        assert abs(a["vi_obj_only"] - b["vi_obj_only"]) / abs(b["vi_obj_only"]) < SAME_RTOL
+        assert _rel(a["vi_post"][0], b["vi_post"][0]) < 1e-9
+        assert _rel(a["vi_post"][1], b["vi_post"][1]) < 1e-9
+
+
+def test_laplace_shards_match_one_context(sgp):
+    """Poisson Laplace on 5 ragged shards of one GPU: the NR iteration count, every NR objective,
+    the mode (gathered in row order), grad psi and the gradient equal the one-context run; the
+    candidate scorer restores f."""
+    from sparsergps_amd.workloads import make_poisson_problem
+    P = make_poisson_problem(n=30_001, m=256)
+    th = np.array(list(P["cov_par"].values()))
+    res = {}
+    for key, dv in (("one", None), ("multi", [0] * 5)):
+        with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=257, devices=dv) as c:
+            c.lap_set_f(P["f0"])
+            o, g, it = c.eval_laplace(th, "sqexp", P["U"], P["delta"], P["a"], 1e-5, 1000)
+            res[key] = dict(o=o, g=g, it=it, ov=c.lap_objective_values(), f=c.lap_get_f(),
+                            gp=c.lap_get_grad_psi(), post=c.posterior_u(np.zeros(256)))
+            f_before = res[key]["f"]
+            res[key]["cand"] = c.lap_candidates(th, "sqexp", P["U"], P["X"][:3], P["delta"],
+                                                P["a"], 1e-5, 1000)
+            np.testing.assert_array_equal(c.lap_get_f(), f_before)
+            res[key]["nr"] = c.lap_nr(th, "sqexp", P["U"], P["delta"], P["a"], 1e-5, 1000)
+    a, b = res["multi"], res["one"]
+    assert a["it"] == b["it"] and len(a["ov"]) == len(b["ov"])
+    np.testing.assert_allclose(a["ov"], b["ov"], rtol=1e-11, atol=0)
+    assert abs(a["o"] - b["o"]) / abs(b["o"]) < SAME_RTOL
+    assert _rel(a["g"], b["g"]) < 1e-10
+    assert np.max(np.abs(a["f"] - b["f"])) < 1e-10
+    assert np.max(np.abs(a["gp"] - b["gp"])) < 1e-9
+    assert _rel(a["post"][0], b["post"][0]) < 1e-9
+    np.testing.assert_allclose(a["cand"], b["cand"], rtol=1e-10)
+    assert a["nr"][1] == b["nr"][1] and abs(a["nr"][0] - b["nr"][0]) / abs(b["nr"][0]) < 1e-11
+
+
+def test_candidates_on_shards(sgp):
+    """VI and FITC OAT scoring on a sharded context equal the one-device scorers (VI: bordered
+    Schur complements there, objective-only evaluations at [U; x*] here)."""
+    from sparsergps_amd.workloads import make_gaussian_problem
+    P = make_gaussian_problem("C2", n=12_000, m=64)
+    th = np.array(list(P["cov_par"].values()))
+    cand = np.random.default_rng(3).uniform(0, 10, size=(5, 3))
+    res = {}
+    for key, dv in (("one", None), ("multi", [0] * 4)):
+        with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=65, devices=dv) as c:
+            res[key] = (c.vi_candidates(th, "sqexp", P["U"], cand, P["delta"]),
+                        c.fitc_candidates(th, "sqexp", P["U"], cand, P["delta"]))
+    for q in range(2):
+        np.testing.assert_allclose(res["multi"][q], res["one"][q], rtol=1e-9)
+
+
+def test_refused_entry_points_and_recovery(sgp):
+    """The phase-level entry points are internal to a multi-device context; a failed
+    evaluation (non-positive tau) leaves it usable."""
+    import ctypes as C
+    from sparsergps_amd import _lib
+    from sparsergps_amd.workloads import make_gaussian_problem
+    P = make_gaussian_problem("C2", n=5_000, m=32)
+    th = np.array(list(P["cov_par"].values()))
+    L = _lib.lib()
+    with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=32, devices=[0, 0]) as c:
+        red = np.zeros(10)
+        st = L.sgp_vi_phase1(c.handle, 0, _lib.dptr(th), _lib.dptr(np.asfortranarray(P["U"])),
+                             32, 32, 1e-6, C.c_void_p(red.ctypes.data))
+        assert st == _lib.SGP_EINVAL and b"multi-device" in L.sgp_last_error()
+        assert L.sgp_ctx_set_stream(c.handle, None) == _lib.SGP_EINVAL
+        assert L.sgp_ctx_set_packed_reduction(c.handle, 1) == _lib.SGP_EINVAL
+        with pytest.raises(_lib.SGPError):
+            c.eval_full(th, "sqexp", P["delta"])
+        with pytest.raises(_lib.SGPError):
+            c.eval_vi(np.array([1.0, 1.0, -0.5]), "sqexp", P["U"], P["delta"])
+        o, g = c.eval_vi(th, "sqexp", P["U"], P["delta"])
+    with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=32) as one:
+        o1, g1 = one.eval_vi(th, "sqexp", P["U"], P["delta"])
+    assert abs(o - o1) / abs(o1) < SAME_RTOL and _rel(g, g1) < SAME_RTOL
+
+
+def test_c4_eight_shard_composition_vi(sgp):
+    """C4 on one GPU: configs[2] (n = 1e6, m = 1024, d = 8, ARD) as 8 shards of 125 000 rows on
+    device 0 -- VI objective and gradient at n = 1e6 against the row-chunked CPU model and the
+    one-context run.  Reference: R/vi_functions.R:87-118, 227-253."""
+    from oracle import adjoint_chunked as AC
+    from sparsergps_amd.workloads import make_gaussian_problem
+    P = make_gaussian_problem("C4")
+    assert P["X"].shape == (1_000_000, 8) and P["U"].shape == (1024, 8)
+    th = np.array(list(P["cov_par"].values()))
+    with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=1024, devices=[0] * 8) as c:
+        assert c.shards() == (8, 1)
+        o8, g8 = c.eval_vi(th, "ard", P["U"], P["delta"])
+    with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=1024) as c:
+        o1, g1 = c.eval_vi(th, "ard", P["U"], P["delta"])
+    o, g = AC.eval_vi("ard", th, P["X"], P["y"], P["mu"], P["U"], P["delta"])
+    print(f"\n[C4 VI] 8 shards vs one context: obj {abs(o8 - o1) / abs(o1):.3e}, "
+          f"grad {_rel(g8, g1):.3e}; vs chunked model: obj {abs(o8 - o) / abs(o):.3e}, "
+          f"grad {_rel(g8, g):.3e}")
+    assert abs(o8 - o) / abs(o) < OBJ_RTOL and _rel(g8, g) < GRAD_RTOL
+    assert abs(o8 - o1) / abs(o1) < 1e-12
+    assert _rel(g8, g1) < SAME_RTOL
+
+
+def test_c4_eight_shard_composition_fitc(sgp):
+    """FITC at the same 8-way split of configs[2]'s rows (two reductions of m^2 + ... doubles)
+    against the row-chunked FITC model and the one-context run.  Reference:
+    R/laplace_approx_obj_funs.R:6-52, R/laplace_approx_gradient.R:720-1135."""
+    from oracle import adjoint_chunked as AC
+    from sparsergps_amd.workloads import make_gaussian_problem
+    P = make_gaussian_problem("C4")
+    th = np.array(list(P["cov_par"].values()))
+    with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=1024, devices=[0] * 8) as c:
+        o8, g8 = c.eval_fitc(th, "ard", P["U"], P["delta"])
+    with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=1024) as c:
+        o1, g1 = c.eval_fitc(th, "ard", P["U"], P["delta"])
+    o, g = AC.eval_fitc("ard", th, P["X"], P["y"], P["mu"], P["U"], P["delta"])
+    print(f"\n[C4 FITC] 8 shards vs one context: obj {abs(o8 - o1) / abs(o1):.3e}, "
+          f"grad {_rel(g8, g1):.3e}; vs chunked model: obj {abs(o8 - o) / abs(o):.3e}, "
+          f"grad {_rel(g8, g):.3e}")
+    assert abs(o8 - o) / abs(o) < OBJ_RTOL and _rel(g8, g) < GRAD_RTOL
+    assert abs(o8 - o1) / abs(o1) < 1e-12
+    assert _rel(g8, g1) < SAME_RTOL

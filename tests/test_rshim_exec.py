@@ -56,7 +56,7 @@ def _err(R, name, *args):
 # ------------------------------------------------------------------------------ CPU
 def test_registration(R):
     fix = json.load(open(os.path.join(GOLD, "rcpp_registry.json")))
-    assert R.n_routines == 35          # 20 reference routines + 15 fused
+    assert R.n_routines == 37          # 20 reference routines + 17 fused
     assert [tuple(e) for e in R.routines[:20]] == [tuple(e) for e in fix["call_entries"]]
     assert R.L.mock_dynamic_symbols() == 0             # R_useDynamicSymbols(dll, FALSE)
 
@@ -178,6 +178,11 @@ def test_filler_messages_and_errors_without_device(R):
     # the fused routines reject anything that is not a context
     assert "not an sgp context" in _err(R, "sgp_R_eval", 1.0, 0.0, "sqexp", [1.0, 1.0, 0.5],
                                         x, 1e-6, 0.0)
+    # the multi-device context's device list is checked before any device call
+    y4 = np.zeros(4)
+    assert "non-negative integers" in _err(R, "sgp_R_ctx_create", x, y4, y4, 8.0, [0.0, -1.0])
+    assert "non-negative integers" in _err(R, "sgp_R_ctx_create", x, y4, y4, 8.0, [0.5])
+    assert "at most 64" in _err(R, "sgp_R_ctx_create", x, y4, y4, 8.0, [0.0] * 65)
 
 
 def test_every_host_routine_ran(R):
@@ -237,7 +242,7 @@ def test_vi_fitc_routines(gR):
     X, U, y, mu, th = z["X"], z["U"], z["y"], z["mu"], z["theta"]
     cf, delta, m, d = str(z["cov_fun"]), float(z["delta"]), z["U"].shape[0], X.shape[1]
     cp = dict(zip([str(s) for s in z["names"]], th))
-    ctx = R.call("sgp_R_ctx_create", X, y, mu, float(m + 1))
+    ctx = R.call("sgp_R_ctx_create", X, y, mu, float(m + 1), None)
     for meth, key in ((0, "vi"), (1, "fitc")):
         out = R.call("sgp_R_eval", ctx, float(meth), cf, th, U, delta, 0.0).py()
         assert abs(out["objective"][0] - z[f"{key}_obj"]) <= 1e-6 * abs(z[f"{key}_obj"])
@@ -285,7 +290,7 @@ def test_laplace_routines(gR):
     z = np.load(os.path.join(GOLD, "poisson_c5_small.npz"))
     X, U, y, mu, th = z["X"], z["U"], z["y"], z["mu"], z["theta"]
     delta, a, m = float(z["delta"]), float(z["a"]), U.shape[0]
-    ctx = R.call("sgp_R_ctx_create", X, y, mu, float(m + 1))
+    ctx = R.call("sgp_R_ctx_create", X, y, mu, float(m + 1), None)
     R.call("sgp_R_lap_set_f", ctx, z["f0"])
     out = R.call("sgp_R_eval_laplace", ctx, "sqexp", th, U, delta, a, 1e-5, 1000.0,
                  R.lgl(True)).py()
@@ -355,13 +360,53 @@ def test_full_gp_routine(gR):
     y = np.sin(X).sum(1) + rng.normal(0, 0.3, 120)
     mu = np.full(120, y.mean())
     cp = {"sigma": 1.1, "l": 1.6, "tau": 0.4}
-    ctx = R.call("sgp_R_ctx_create", X, y, mu, 120.0)
+    ctx = R.call("sgp_R_ctx_create", X, y, mu, 120.0, None)
     out = R.call("sgp_R_eval_full", ctx, "sqexp", [1.1, 1.6, 0.4], 1e-6, 0.0).py()
     ro = O.full_obj_eval(cp, "sqexp", X, y, mu)
     rg = O.dlogp_dcov_par_full(cp, "sqexp", X, y, mu)["gradient"]
     assert abs(out["objective"][0] - ro) <= 1e-6 * abs(ro)
     np.testing.assert_allclose(out["gradient"], [rg[k] for k in cp], rtol=1e-6, atol=1e-8)
     R.call("sgp_R_ctx_destroy", ctx)
+
+
+@pytest.mark.gpu
+def test_multi_device_context_routines(gR):
+    """An R process on the multi-device path (sgp_hotpath.R's .sgp_devices -> sgp_R_ctx_create
+    with one device index per row shard -> sgp_ctx_create_multi, RCCL inside libsgp): three
+    shards on device 0 give the one-device answers through the same .Call routines, VI, FITC
+    and Poisson Laplace."""
+    R = gR
+    assert R.call("sgp_R_device_count").py()[0] >= 1
+    z = np.load(os.path.join(GOLD, "gauss_c3_small.npz"))
+    X, U, y, mu, th = z["X"], z["U"], z["y"], z["mu"], z["theta"]
+    cf, delta, m = str(z["cov_fun"]), float(z["delta"]), z["U"].shape[0]
+    one = R.call("sgp_R_ctx_create", X, y, mu, float(m + 1), None)
+    multi = R.call("sgp_R_ctx_create", X, y, mu, float(m + 1), [0.0, 0.0, 0.0])
+    assert list(R.call("sgp_R_ctx_shards", multi).py()) == [3.0, 1.0]
+    assert list(R.call("sgp_R_ctx_shards", one).py()) == [1.0, 1.0]
+    for meth, key in ((0, "vi"), (1, "fitc")):
+        a = R.call("sgp_R_eval", multi, float(meth), cf, th, U, delta, 0.0).py()
+        b = R.call("sgp_R_eval", one, float(meth), cf, th, U, delta, 0.0).py()
+        assert abs(a["objective"][0] - b["objective"][0]) <= 1e-11 * abs(b["objective"][0])
+        np.testing.assert_allclose(a["gradient"], b["gradient"], rtol=1e-10, atol=1e-10)
+        assert abs(a["objective"][0] - z[f"{key}_obj"]) <= 1e-9 * abs(z[f"{key}_obj"])
+    R.call("sgp_R_ctx_destroy", multi)
+    R.call("sgp_R_ctx_destroy", one)
+    z = np.load(os.path.join(GOLD, "poisson_c5_small.npz"))
+    X, U, y, mu, th = z["X"], z["U"], z["y"], z["mu"], z["theta"]
+    delta, a, m = float(z["delta"]), float(z["a"]), U.shape[0]
+    multi = R.call("sgp_R_ctx_create", X, y, mu, float(m + 1), [0.0, 0.0])
+    R.call("sgp_R_lap_set_f", multi, z["f0"])
+    out = R.call("sgp_R_eval_laplace", multi, "sqexp", th, U, delta, a, 1e-5, 1000.0,
+                 R.lgl(True)).py()
+    tr = z["obj_trace"]
+    assert out["nr_iter"][0] == len(tr)
+    np.testing.assert_allclose(R.call("sgp_R_lap_objective_values", multi).py(), tr, rtol=1e-9)
+    np.testing.assert_allclose(R.call("sgp_R_lap_get_f", multi).py(), z["ff"], rtol=1e-7,
+                               atol=1e-9)
+    np.testing.assert_allclose(out["gradient"], z["grad"], rtol=1e-7, atol=1e-8)
+    R.call("sgp_R_ctx_destroy", multi)
+    _GPU_DONE.append("test_multi_device_context_routines")
 
 
 @pytest.mark.gpu
@@ -373,6 +418,6 @@ def test_every_device_routine_ran(gR):
     if len(_GPU_DONE) < 5:
         pytest.skip("only a subset of this module's GPU tests ran")
     dev = [n for n, _ in gR.routines if n.startswith("sgp_R_") or "cov_mat" in n or "dsig_" in n]
-    assert len(dev) == 19
+    assert len(dev) == 21
     missing = [n for n in dev if n not in gR.called]
     assert not missing, missing

@@ -17,7 +17,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "sparsergps_amd", "csrc")
 OUT = os.path.join(ROOT, "build", "asan")
-SOURCES = ["capi.hip", "k_cov.hip", "k_mfma.hip", "k_dense.hip", "k_lap.hip"]
+from sparsergps_amd._build import SOURCES  # noqa: E402  (every translation unit)
 SAN = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
        "-Xarch_host", "-fno-sanitize-recover=all", "-Xarch_host", "-fno-omit-frame-pointer"]
 
@@ -46,7 +46,7 @@ def test_host_abi_under_asan_ubsan():
     drv = os.path.join(ROOT, "tests", "sanitize", "host_driver.c")
     res = subprocess.run([cc, "-O1", "-g", "-x", "c++", *SAN, "-I", os.path.join(ROOT, "include"),
                           drv, "-x", "none", *objs, "--offload-arch=gfx950",
-                          "-fsanitize=address,undefined", "-o", exe],
+                          "-fsanitize=address,undefined", "-lrccl", "-lpthread", "-o", exe],
                          stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     assert res.returncode == 0, res.stdout.decode(errors="replace")[-4000:]
     env = dict(os.environ)
