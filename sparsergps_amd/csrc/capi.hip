@@ -1294,21 +1294,17 @@ static int k22_launch(sgp_ctx* c, double diag_sub) {
   return st ? st : k22_factor(c, false);
 }
 
-// Binv (holding K22 + S * s_scale) inverted in place (one Gauss-Jordan launch per pivot).
-static int bm_factor_launches(sgp_ctx* c, hipStream_t s) {
-  const int64_t mp = c->mp;
-  HIPCHK(dense_spd_inverse(c->Binv, mp, c->Xt, c->T1, c->dinv, c->logdB, c->status + 1, s));
-  HIPCHK(launch_sum_small(c->logdB, mp / SGP_DB, c->sc + SC_LDB, s));
-  return SGP_OK;
-}
-
+// Binv = (K22 + S * s_scale)^-1 (one Gauss-Jordan launch per pivot; the sum is formed by the
+// chain's first pivot and step as they read K22 and S)
 static int bm_stage(sgp_ctx* c, const double* S, double s_scale, bool k22_ordered = false) {
-  const int64_t mp = c->mp, mm = mp * mp;
+  const int64_t mp = c->mp;
   Scope t(c, "dense_bm");
   if (!k22_ordered)   // Bm needs K22, not its inverse (VI: ordered through phase 1's ev_lo)
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22m, 0));
-  HIPCHK(dense_axpby(1.0, c->K22, s_scale, S, c->Binv, mm, c->stream));
-  return bm_factor_launches(c, c->stream);
+  HIPCHK(dense_spd_inverse_sum(c->K22, s_scale, S, c->Binv, mp, c->Xt, c->dinv, c->logdB,
+                               c->status + 1, c->stream));
+  HIPCHK(launch_sum_small(c->logdB, mp / SGP_DB, c->sc + SC_LDB, c->stream));
+  return SGP_OK;
 }
 
 int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned flags,
@@ -1863,17 +1859,14 @@ static int lap_consume_obj(sgp_ctx* c, const double* red, int64_t o, bool first,
   const int64_t mp = c->mp, mm = mp * mp;
   {
     Scope t(c, "lap_dense");
-    if (first) {   // (K22 + S_Z)^-1 is fixed for the whole NR run (Z depends on theta only)
-      HIPCHK(dense_axpby(1.0, c->K22, 1.0, red, c->Bm, mm, c->stream));
-      HIPCHK(dense_spd_inverse(c->Bm, mp, c->Xt, c->T1, c->dinv, c->logdB, c->status + 1,
-                               c->stream));
-    }
+    if (first)   // (K22 + S_Z)^-1 is fixed for the whole NR run (Z depends on theta only)
+      HIPCHK(dense_spd_inverse_sum(c->K22, 1.0, red, c->Bm, mp, c->Xt, c->dinv, c->logdB,
+                                   c->status + 1, c->stream));
     if (!first)   // newtrap_sparseGP's u posterior uses the W of the last update's start
       HIPCHK(hipMemcpyAsync(c->Cprev, c->Binv, sizeof(double) * mm, hipMemcpyDeviceToDevice,
                             c->stream));
-    HIPCHK(dense_axpby(1.0, c->K22, 1.0, red + o, c->Binv, mm, c->stream));
-    HIPCHK(dense_spd_inverse(c->Binv, mp, c->Xt, c->T1, c->dinv, c->logdB, c->status + 2,
-                             c->stream));
+    HIPCHK(dense_spd_inverse_sum(c->K22, 1.0, red + o, c->Binv, mp, c->Xt, c->dinv, c->logdB,
+                                 c->status + 2, c->stream));
     HIPCHK(launch_sum_small(c->logdB, mp / SGP_DB, c->sc + SC_LDB, c->stream));
     HIPCHK(dense_gemv(c->Bm, mp, red + o + mm, 1.0, lmv(c, LM_X1), c->stream));
     HIPCHK(launch_dot(red + o + mm, lmv(c, LM_X1), mp, c->slab_small, c->sc + SC_TU, c->stream));

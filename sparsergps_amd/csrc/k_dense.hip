@@ -100,7 +100,8 @@ __device__ __forceinline__ double row_bcast_f64(double v, int k) {
 __device__ __forceinline__ void gj_pivot_body(const double* B, int64_t ldb, int64_t gofs,
                                               double* __restrict__ P,
                                               double* __restrict__ logd_slot,
-                                              int* __restrict__ status, double* lds) {
+                                              int* __restrict__ status, double* lds,
+                                              const double* B2 = nullptr, double beta = 0.0) {
   double* Es0 = lds;                          // [2][64][GJP_LD]  column panel W_:K (old)
   double* Fs = lds + 2 * 64 * GJP_LD;         // [64][GJP_LD]     F = W_:K Q (own rows per wave)
   double* Qs = Fs + 64 * GJP_LD;              // [16][GJP_LD]     Q = -inv(W_KK)
@@ -112,6 +113,13 @@ __device__ __forceinline__ void gj_pivot_body(const double* B, int64_t ldb, int6
   for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[ct][q] = B[(16 * wv + lr + 4 * q) * ldb + 16 * ct + lc];
+  if (B2) {   // the block of B + beta B2 (the first pivot of dense_spd_inverse_sum)
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        acc[ct][q] = fma(beta, B2[(16 * wv + lr + 4 * q) * ldb + 16 * ct + lc], acc[ct][q]);
+  }
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb) {
     double* Es = Es0 + (kb & 1) * 64 * GJP_LD;
@@ -211,10 +219,12 @@ __device__ __forceinline__ void gj_pivot_body(const double* B, int64_t ldb, int6
 __global__ void __launch_bounds__(256) k_gj_pivot(const double* __restrict__ A, int64_t lda,
                                                   int k, double* __restrict__ P,
                                                   double* __restrict__ logd,
-                                                  int* __restrict__ status) {
+                                                  int* __restrict__ status,
+                                                  const double* __restrict__ A2, double beta) {
   __shared__ double lds[GJ_PIVOT_LDS];
   const int64_t o = (int64_t)k * 64;
-  gj_pivot_body(A + o * lda + o, lda, o, P, logd + k, status, lds);
+  gj_pivot_body(A + o * lda + o, lda, o, P, logd + k, status, lds, A2 ? A2 + o * lda + o : nullptr,
+                beta);
 }
 
 // One Gauss-Jordan step k, out of place (Ao -> An), every 64x64 tile (i, j) in one launch:
@@ -261,6 +271,25 @@ __device__ __forceinline__ void gj_ld(double (&v)[16], const double* G, int64_t 
     v[q] = G[(int64_t)(e >> 6) * ldg + (e & 63)];
   }
 }
+// the same tile of G + beta G2 (step 0 of dense_spd_inverse_sum: the matrix is formed as it is
+// read, no separate axpby launch); SUM = false is gj_ld
+template <bool SUM>
+__device__ __forceinline__ void gj_ld2(double (&v)[16], const double* G, const double* G2,
+                                       double beta, int64_t ldg) {
+  if constexpr (!SUM) {
+    gj_ld(v, G, ldg);
+  } else {
+    double w[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = threadIdx.x + 256 * q;
+      v[q] = G[(int64_t)(e >> 6) * ldg + (e & 63)];
+      w[q] = G2[(int64_t)(e >> 6) * ldg + (e & 63)];
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = fma(beta, w[q], v[q]);
+  }
+}
 __device__ __forceinline__ void gj_st(double* S, const double (&v)[16]) {
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
@@ -269,12 +298,15 @@ __device__ __forceinline__ void gj_st(double* S, const double (&v)[16]) {
   }
 }
 
+// SUM (step 0 of dense_spd_inverse_sum): Ao is read as Ao + beta A2.
+template <bool SUM>
 __global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
                                                  double* __restrict__ An, int64_t lda, int k,
                                                  int nb, const double* __restrict__ Pk,
                                                  double* __restrict__ Pn,
                                                  double* __restrict__ logd,
-                                                 int* __restrict__ status) {
+                                                 int* __restrict__ status,
+                                                 const double* __restrict__ A2, double beta) {
   __shared__ double lds[2 * 64 * GJ_LS];
   double* S0 = lds;
   double* S1 = lds + 64 * GJ_LS;
@@ -294,7 +326,7 @@ __global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
       return;
     }
     gj_ld(v0, Pk, 64);
-    gj_ld(v1, Ao + ok * lda + oj, lda);
+    gj_ld2<SUM>(v1, Ao + ok * lda + oj, A2 + ok * lda + oj, beta, lda);
     gj_st(S0, v0);
     gj_st(S1, v1);
     __syncthreads();
@@ -311,7 +343,7 @@ __global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
         }
     return;
   }
-  gj_ld(v0, Ao + oi * lda + ok, lda);            // C_i = Ao_ik
+  gj_ld2<SUM>(v0, Ao + oi * lda + ok, A2 + oi * lda + ok, beta, lda);   // C_i = Ao_ik
   gj_ld(v1, Pk, 64);
   if (j == k) {
     gj_st(S0, v0);
@@ -332,7 +364,7 @@ __global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
   }
   // the remaining operands (Ao_kj, and Ao_ij in the accumulator layout) are loaded now as well
   double v2[16], aij[2][2][4];
-  gj_ld(v2, Ao + ok * lda + oj, lda);
+  gj_ld2<SUM>(v2, Ao + ok * lda + oj, A2 + ok * lda + oj, beta, lda);
 #pragma unroll
   for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
@@ -342,6 +374,7 @@ __global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
         const int r = wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
         const int c = wc * 32 + fn * 16 + (lane & 15);
         aij[fm][fn][q] = Ao[(oi + r) * lda + oj + c];
+        if constexpr (SUM) aij[fm][fn][q] = fma(beta, A2[(oi + r) * lda + oj + c], aij[fm][fn][q]);
       }
   gj_st(S0, v0);
   gj_st(S1, v1);
@@ -600,19 +633,44 @@ hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* Cb, doubl
   // R: mp x mp ping-pong buffer; P: nb 64x64 pivot inverses (mp * 64 doubles); Cb unused.
   (void)Cb;
   const int nb = (int)(mp / SGP_DB);
-  hipLaunchKernelGGL(k_gj_pivot, dim3(1), dim3(256), 0, s, A, mp, 0, P, logd, status);
+  hipLaunchKernelGGL(k_gj_pivot, dim3(1), dim3(256), 0, s, A, mp, 0, P, logd, status,
+                     (const double*)nullptr, 0.0);
   double* src = A;
   double* dst = R;
   for (int k = 0; k < nb; ++k) {
     double* Pn = (k + 1 < nb) ? P + (int64_t)(k + 1) * 4096 : P;
-    hipLaunchKernelGGL(k_gj_step, dim3(nb, nb), dim3(256), gj_step_pad(), s, src, dst, mp, k, nb,
-                       P + (int64_t)k * 4096, Pn, logd, status);
+    hipLaunchKernelGGL(k_gj_step<false>, dim3(nb, nb), dim3(256), gj_step_pad(), s, src, dst, mp,
+                       k, nb, P + (int64_t)k * 4096, Pn, logd, status, (const double*)nullptr,
+                       0.0);
     double* t = src;
     src = dst;
     dst = t;
   }
   if (src != A)
     return hipMemcpyAsync(A, src, sizeof(double) * mp * mp, hipMemcpyDeviceToDevice, s);
+  return hipGetLastError();
+}
+
+hipError_t dense_spd_inverse_sum(const double* A0, double beta, const double* B0, double* out,
+                                 int64_t mp, double* R, double* P, double* logd, int* status,
+                                 hipStream_t s) {
+  // out = inv(A0 + beta B0): step 0 forms the matrix as it reads it (no axpby launch, ~6 us of
+  // the C2 critical path); step k writes buf[(nb - 1 - k) % 2] (buf = {out, R}), so the last
+  // step always lands in out and no copy follows
+  const int nb = (int)(mp / SGP_DB);
+  double* buf[2] = {out, R};
+  hipLaunchKernelGGL(k_gj_pivot, dim3(1), dim3(256), 0, s, A0, mp, 0, P, logd, status, B0, beta);
+  for (int k = 0; k < nb; ++k) {
+    double* Pn = (k + 1 < nb) ? P + (int64_t)(k + 1) * 4096 : P;
+    double* dst = buf[(nb - 1 - k) % 2];
+    if (k == 0)
+      hipLaunchKernelGGL(k_gj_step<true>, dim3(nb, nb), dim3(256), gj_step_pad(), s, A0, dst,
+                         mp, k, nb, P, Pn, logd, status, B0, beta);
+    else
+      hipLaunchKernelGGL(k_gj_step<false>, dim3(nb, nb), dim3(256), gj_step_pad(), s,
+                         (const double*)buf[(nb - k) % 2], dst, mp, k, nb,
+                         P + (int64_t)k * 4096, Pn, logd, status, (const double*)nullptr, 0.0);
+  }
   return hipGetLastError();
 }
 

@@ -233,6 +233,11 @@ hipError_t launch_gemm64(bool transA, bool transB, bool lower_only, int64_t M, i
 // log det A = 2 * sum_k logd[k].  Work: R (64 x mp), Cb (mp x 64), P (64 x 64).
 hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* Cb, double* P,
                              double* logd, int* status, hipStream_t s);
+// out = inv(A0 + beta B0), the sum formed by the chain's first pivot and step as they read it
+// (out, R distinct from A0 and B0)
+hipError_t dense_spd_inverse_sum(const double* A0, double beta, const double* B0, double* out,
+                                 int64_t mp, double* R, double* P, double* logd, int* status,
+                                 hipStream_t s);
 // C = a*A + b*B elementwise over mp x mp
 hipError_t dense_axpby(double a, const double* A, double b, const double* B, double* C,
                        int64_t count, hipStream_t s);

@@ -394,6 +394,7 @@ int mock_call(const char* name, int nargs, SEXP* a, SEXP* out) {
   SEXP r;
   switch (nargs) {
 #define A(i) a[i]
+    case 0: r = ((SEXP(*)(void))f)(); break;
     case 1: r = ((SEXP(*)(SEXP))f)(A(0)); break;
     case 2: r = ((SEXP(*)(SEXP, SEXP))f)(A(0), A(1)); break;
     case 3: r = ((SEXP(*)(SEXP, SEXP, SEXP))f)(A(0), A(1), A(2)); break;

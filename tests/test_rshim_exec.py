@@ -178,7 +178,12 @@ def test_filler_messages_and_errors_without_device(R):
     # the fused routines reject anything that is not a context
     assert "not an sgp context" in _err(R, "sgp_R_eval", 1.0, 0.0, "sqexp", [1.0, 1.0, 0.5],
                                         x, 1e-6, 0.0)
-    # the multi-device context's device list is checked before any device call
+    # visible devices (0 here: no GPU), and the multi-device context's device list is checked
+    # before any device call
+    from sparsergps_amd import _lib
+    n = _lib.C.c_int(0)
+    if _lib.lib().sgp_device_count(_lib.C.byref(n)) != 0 or n.value == 0:
+        assert R.call("sgp_R_device_count").py()[0] == 0
     y4 = np.zeros(4)
     assert "non-negative integers" in _err(R, "sgp_R_ctx_create", x, y4, y4, 8.0, [0.0, -1.0])
     assert "non-negative integers" in _err(R, "sgp_R_ctx_create", x, y4, y4, 8.0, [0.5])
