@@ -165,8 +165,10 @@ def test_candidates_on_shards(sgp):
         with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=65, devices=dv) as c:
             res[key] = (c.vi_candidates(th, "sqexp", P["U"], cand, P["delta"]),
                         c.fitc_candidates(th, "sqexp", P["U"], cand, P["delta"]))
-    for q in range(2):
-        np.testing.assert_allclose(res["multi"][q], res["one"][q], rtol=1e-9)
+    # VI: two different algorithms for the same bordered ELBO (Schur update vs a rebuild), ~4e4
+    # in magnitude: they agree to a few 1e-10 relative; FITC: the same algorithm on both sides
+    np.testing.assert_allclose(res["multi"][0], res["one"][0], rtol=1e-8)
+    np.testing.assert_allclose(res["multi"][1], res["one"][1], rtol=1e-10)
 
 
 def test_refused_entry_points_and_recovery(sgp):
