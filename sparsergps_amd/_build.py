@@ -55,8 +55,9 @@ def _compile_cmd(cc, src, obj, defs=(), csrc=CSRC):
     return [cc, *_compile_flags(src, defs), "-c", os.path.join(csrc, src), "-o", obj]
 
 
-# librccl: the in-process all-reduces of sgp_ctx_create_multi contexts (multi.hip)
-LINK_FLAGS = [f"--offload-arch={ARCH}", "-shared", "-fPIC", "-lrccl", "-lpthread"]
+# libdl: librccl is opened by the first sgp_ctx_create_multi context (multi.hip: reusing an
+# RCCL the process already has, e.g. torch's; not a load-time dependency)
+LINK_FLAGS = [f"--offload-arch={ARCH}", "-shared", "-fPIC", "-ldl", "-lpthread"]
 
 
 def _link_cmd(cc, objs, out):

@@ -25,6 +25,7 @@
 // decisions (the Laplace NR stop rule) are functions of the summed buffers, so every shard takes
 // the same path; the replicated m x m state of shard 0 answers the posterior, knot-gradient and
 // objective-history queries.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdio.h>
@@ -43,6 +44,48 @@
 namespace {
 
 constexpr int ABORTED = -1;   // a worker that stopped because another one failed
+
+// RCCL, bound at the first multi-device context rather than at load time: a process that also
+// runs torch.distributed carries torch's own librccl (NEEDED as "librccl.so", SONAME
+// librccl.so.1).  Linking ROCm's librccl.so.1 into libsgp put a second copy in such a process
+// whenever libsgp was loaded first (the names differ, so the loader does not share them); with
+// the symbols interposed across the two copies their exit-time destructors freed the same
+// objects ("double free or corruption" after a GPU test run).  Here an already loaded RCCL is
+// reused (RTLD_NOLOAD), and otherwise ROCm's is opened RTLD_LOCAL, so it never interposes.
+struct Rccl {
+  ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                             hipStream_t) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  const char* (*error_string)(ncclResult_t) = nullptr;
+  bool ok = false;
+  std::string err;
+};
+
+const Rccl& rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    void* h = nullptr;
+    for (const char* nm : {"librccl.so.1", "librccl.so"})
+      if (!h) h = dlopen(nm, RTLD_NOW | RTLD_NOLOAD);
+    for (const char* nm : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"})
+      if (!h) h = dlopen(nm, RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      const char* e = dlerror();
+      x.err = std::string("cannot load librccl (the multi-device context's collectives): ") +
+              (e ? e : "unknown error");
+      return x;
+    }
+    x.comm_init_all = reinterpret_cast<decltype(x.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
+    x.all_reduce = reinterpret_cast<decltype(x.all_reduce)>(dlsym(h, "ncclAllReduce"));
+    x.comm_destroy = reinterpret_cast<decltype(x.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    x.error_string = reinterpret_cast<decltype(x.error_string)>(dlsym(h, "ncclGetErrorString"));
+    x.ok = x.comm_init_all && x.all_reduce && x.comm_destroy && x.error_string;
+    if (!x.ok) x.err = "librccl lacks ncclCommInitAll / ncclAllReduce / ncclCommDestroy";
+    return x;
+  }();
+  return r;
+}
 
 struct Shard {
   sgp_ctx* ctx = nullptr;
@@ -227,11 +270,11 @@ struct MultiCtx {
   // the all-reduce over the devices, in place on the device's stream
   void all_reduce(Group& g, double* red, int64_t count, int& st) {
     if (st != SGP_OK || count <= 0) return;
-    const ncclResult_t r = ncclAllReduce(red, red, (size_t)count, ncclDouble, ncclSum, g.comm,
-                                         g.stream);
+    const ncclResult_t r = rccl().all_reduce(red, red, (size_t)count, ncclDouble, ncclSum, g.comm,
+                                             g.stream);
     if (r != ncclSuccess) {
       char b[256];
-      snprintf(b, sizeof(b), "RCCL all-reduce failed: %s", ncclGetErrorString(r));
+      snprintf(b, sizeof(b), "RCCL all-reduce failed: %s", rccl().error_string(r));
       sgp_internal_set_err(b);
       st = SGP_EHIP;
     }
@@ -269,7 +312,7 @@ struct MultiCtx {
     }
     for (Group& g : groups) {
       (void)hipSetDevice(g.device);
-      if (g.comm) ncclCommDestroy(g.comm);
+      if (g.comm) rccl().comm_destroy(g.comm);
       for (double*& p : g.red)
         if (p) (void)hipFree(p);
       if (g.stream) (void)hipStreamDestroy(g.stream);
@@ -351,15 +394,19 @@ int multi_create(MultiCtx** out, const int* devices, int nshards, const double* 
     }
   }
   // one RCCL communicator per distinct device, all in this process
+  if (!st && !rccl().ok) {
+    sgp_internal_set_err(rccl().err.c_str());
+    st = SGP_EHIP;
+  }
   if (!st) {
     std::vector<ncclComm_t> comms(mc->groups.size());
     std::vector<int> devs;
     for (const Group& g : mc->groups) devs.push_back(g.device);
-    const ncclResult_t r = ncclCommInitAll(comms.data(), (int)devs.size(), devs.data());
+    const ncclResult_t r = rccl().comm_init_all(comms.data(), (int)devs.size(), devs.data());
     if (r != ncclSuccess) {
       char b[256];
       snprintf(b, sizeof(b), "ncclCommInitAll over %d devices failed: %s", (int)devs.size(),
-               ncclGetErrorString(r));
+               rccl().error_string(r));
       sgp_internal_set_err(b);
       st = SGP_EHIP;
     } else {
