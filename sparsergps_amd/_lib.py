@@ -152,7 +152,10 @@ def lib(auto_build: bool = True):
         if not os.path.exists(path):
             raise RuntimeError(f"libsgp.so not found at {path}; run sparsergps_amd._build.build()")
         h = C.CDLL(path, mode=C.RTLD_GLOBAL)
+        ab = path != LIB
         for name, (res, args) in PROTOTYPES.items():
+            if ab and not hasattr(h, name):   # an A/B library of an older revision
+                continue
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args
