@@ -740,7 +740,7 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
     return SGP_EHIP;
   }
   c->slab_syrk_cap = syrk_slab_doubles(np_, mp);
-  c->slab_con_cap = contract_record_slots(np_, mp) * (SGP_MAXD + 5);   // nrec <= L + 5
+  c->slab_con_cap = (np_ / SGP_TILE) * (mp / SGP_TILE) * (SGP_MAXD + 5);   // nrec <= L + 5
   st = st ? st : dalloc(&c->X, np_ * d);
   st = st ? st : dalloc(&c->r, np_);
   st = st ? st : dalloc(&c->K, np_ * mp);

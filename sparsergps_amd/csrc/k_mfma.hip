@@ -878,23 +878,8 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   __shared__ double s_uk[2][BK];   // u slice of the staged k-step (fused alpha)
 
   const int64_t ntj = mp / T128;
-  const int64_t ntile = (n_pad / T128) * ntj;
-  const int64_t nrs = gridDim.x;   // record slots: one per workgroup
-  const int nsteps = (int)(mp / BK);
-  // split-K tail (ConArgs::tail_s): workgroups past nfull take k-steps [st0, st1) of a tail tile
-  const bool tail = (EPI == EPI_GRAD) && !KNOT && !FROM_T && ca.tail_s > 0 &&
-                    (int64_t)blockIdx.x >= ca.nfull;
-  int64_t wgid;
-  int part = 0, st0 = 0, st1 = nsteps;
-  if (tail) {
-    const int64_t loc = (int64_t)blockIdx.x - ca.nfull;
-    wgid = ca.nfull + loc / ca.tail_s;
-    part = (int)(loc % ca.tail_s);
-    st0 = (int)((int64_t)part * nsteps / ca.tail_s);
-    st1 = (int)((int64_t)(part + 1) * nsteps / ca.tail_s);
-  } else {
-    wgid = xcd_remap(blockIdx.x, ca.tail_s > 0 ? ca.nfull : ntile);
-  }
+  const int64_t nwg = (n_pad / T128) * ntj;
+  const int64_t wgid = xcd_remap(blockIdx.x, nwg);
   const int64_t ti = wgid / ntj, tj = wgid % ntj;
   const int64_t i0 = ti * T128, j0 = tj * T128;
 
@@ -918,6 +903,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   const double2* gB = reinterpret_cast<const double2*>(M + (int64_t)bk * mp + j0) + bc;
   const int64_t bstep = BK * mp / 2;
   double2 va0, va1, va2, va3, vb0, vb1, vb2, vb3;
+  const int nsteps = (int)(mp / BK);
   // alpha folded into the k-loop: each thread dots the 8 K values it stages with u.
   double ku = 0.0, vuk = 0.0;
   // the step is one basic block (mfma_interleave): the u slice is fetched, staged and folded
@@ -966,13 +952,13 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
           acc[fm][fn][q] = ca.tin[(i0 + wr * 64 + fm * 16 + (lane >> 4) + 4 * q) * mp + j0 +
                                   wc * 64 + fn * 16 + (lane & 15)];
   } else {
-  CON_GLOAD(st0);
+  CON_GLOAD(0);
   CON_SSTORE(0);
   __syncthreads();
-  for (int step = st0; step < st1; ++step) {
-    const int cur = (step - st0) & 1;
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
     if constexpr (KU) CON_KU(cur);   // va still holds this step's staged K values
-    CON_GLOAD(step + 1 < st1 ? step + 1 : step);   // the last step reloads its own slice
+    CON_GLOAD(step + 1 < nsteps ? step + 1 : step);   // the last step reloads its own slice
     const double* As = lds + cur * (A_SZ + B_SZ);
     const double* Bs = As + A_SZ;
 #pragma unroll
@@ -1012,34 +998,16 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   double* s_us = s_xs + T128 * 16;          // 128 x 9 ([col][c], scaled; odd stride: 16
                                             // columns on distinct banks)
   ku += __shfl_xor(ku, 1, 64);                       // the two halves of row `arow`
-  if (tail && with_u && part == 0) {
-    // a tail part's k-loop saw a slice of the row only: the full K_i . u (32 rows per wave,
-    // coalesced row reads, fixed-order wave sums) into s_alpha as a staging slot
-    for (int rr = 0; rr < 32; ++rr) {
-      const int row = wv * 32 + rr;
-      const double* kr = K + (i0 + row) * mp;
-      double t = 0.0;
-      for (int64_t j = lane; j < mp; j += 64) t = fma(kr[j], uvec[j], t);
-      t = wave_sum(t);
-      if (lane == 0) s_alpha[row] = t;
-    }
-    __syncthreads();
-    ku = s_alpha[arow];
-    __syncthreads();
-  }
   double a2 = 0.0;                                    // alpha^2, counted once (tj == 0)
-  // the rank-1 terms alpha u^T, beta v^T and the alpha records belong to part 0 only
-  const bool rank1 = !tail || part == 0;
   if ((tid & 1) == 0) {
     const int64_t i = i0 + arow;
     const double iz = ca.invz_vec ? ca.invz_vec[i] : ca.invz;
-    const double al = !rank1 ? 0.0
-                      : ca.alpha_in ? ca.alpha_in[i]
-                                    : (with_u ? (r[i] - ku) * iz : 0.0);   // padded rows -> 0
+    const double al = ca.alpha_in ? ca.alpha_in[i]
+                                  : (with_u ? (r[i] - ku) * iz : 0.0);   // padded rows -> 0
     s_alpha[arow] = al;
     s_rs[arow] = ca.rs_vec ? ca.rs * ca.rs_vec[i] : ca.rs;
-    s_beta[arow] = (with_v && rank1) ? ca.beta_in[i] : 0.0;
-    if (tj == 0 && rank1) {
+    s_beta[arow] = with_v ? ca.beta_in[i] : 0.0;
+    if (tj == 0) {
       if (ca.count_a2 && i < n) a2 = al * al;
       if (ca.alpha_out) ca.alpha_out[i] = al;
     }
@@ -1308,8 +1276,8 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
       red[wv][4 + L] = v;
     }
     __syncthreads();
-    if (tid < nrec)   // field-major [nrec][slots]: coalesced for the reduction (launch_rowsum)
-      slab[tid * nrs + blockIdx.x] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+    if (tid < nrec)   // field-major [nrec][nwg]: coalesced for the reduction (launch_rowsum)
+      slab[tid * nwg + wgid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
     SGP_PROBE_CON_STAMP(2);
   }
 }
@@ -2056,54 +2024,13 @@ static void launch_con_from_t(bool v2, bool kn, const KernParams& kp, const doub
                        ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
 }
 
-// workgroup slots of one residency round of the contraction (2 per CU)
-static int64_t con_slots() {
-  static int64_t slots = 0;
-  if (slots == 0) {
-    int dev = 0, cus = 256;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-      cus = prop.multiProcessorCount;
-    slots = 2 * (int64_t)cus;
-  }
-  return slots;
-}
-
-// Split-K tail: the tiles past the last whole residency round (C2: 1564 tiles = 3 rounds of 512
-// + 28) ran alone on 28 of the 512 slots for a whole tile time.  Split over up to SGP_CON_TAIL
-// parts each, they finish in ~1/S of the k-loop plus one epilogue.
-static void con_tail_plan(int64_t ntile, int64_t mp, ConArgs& c, int64_t* grid) {
-  *grid = ntile;
-  const int64_t slots = con_slots();
-  const int64_t ntail = ntile % slots;
-  if (SGP_CON_TAIL < 2 || ntail == 0 || 2 * ntail > slots) return;
-  int64_t S = slots / ntail;
-  if (S > SGP_CON_TAIL) S = SGP_CON_TAIL;
-  if (S > mp / BK) S = mp / BK;
-  if (S < 2) return;
-  c.tail_s = (int)S;
-  c.nfull = ntile - ntail;
-  *grid = c.nfull + ntail * S;
-}
-
-// most record slots a contraction pass can use (the split-K tail adds < one round of slots)
-int64_t contract_record_slots(int64_t n_pad, int64_t mp) {
-  return (n_pad / T128) * (mp / T128) + con_slots();
-}
-
 hipError_t launch_contract_args(const KernParams& kp, const double* K, const double* M,
                                 const double* X, int64_t ldx, int64_t n, int64_t n_pad,
                                 const double* U, int64_t ldu, int64_t m, int64_t mp,
-                                const ConArgs& ca_in, double* slab, int64_t* nrec_out,
+                                const ConArgs& ca, double* slab, int64_t* nrec_out,
                                 int64_t* nwg_out, hipStream_t s) {
-  const int64_t ntile = (n_pad / T128) * (mp / T128);
+  const int64_t nwg = (n_pad / T128) * (mp / T128);
   const int nrec = kp.L + 5;
-  ConArgs ca = ca_in;
-  ca.tail_s = 0;
-  ca.nfull = 0;
-  int64_t nwg = ntile;
-  // the split-K tail serves the k-loop passes without knot partials (those write per-tile slabs)
-  if (ca.tin == nullptr && ca.knot_slab == nullptr) con_tail_plan(ntile, mp, ca, &nwg);
   *nrec_out = nrec;
   *nwg_out = nwg;
   if (ca.tin != nullptr) {   // stored product: no k-loop (alpha from alpha_in)

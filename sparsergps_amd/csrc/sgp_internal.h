@@ -200,15 +200,7 @@ struct ConArgs {
   // from alpha_in; d <= 8)
   double* tstore = nullptr;
   const double* tin = nullptr;
-  // split-K tail (set by launch_contract_args, not by callers): the tiles past the last whole
-  // residency round, nfull .. ntile - 1, run as tail_s workgroups each over a slice of the
-  // k-loop; the epilogue is linear in G, so each part contracts its partial G (the rank-1 terms
-  // only in part 0, whose alpha comes from a full row dot product)
-  int tail_s = 0;
-  int64_t nfull = 0;
 };
-// record slots (workgroups) a contraction pass may write: the slab holds nrec x this doubles
-int64_t contract_record_slots(int64_t n_pad, int64_t mp);
 hipError_t launch_contract_args(const KernParams& kp, const double* K, const double* M,
                                 const double* X, int64_t ldx, int64_t n, int64_t n_pad,
                                 const double* U, int64_t ldu, int64_t m, int64_t mp,
