@@ -226,6 +226,11 @@ def main():
                          "write it to OUT_JSON")
     ap.add_argument("--knots", action="store_true",
                     help="also the m*d knot gradient (xu_opt = 'simultaneous', SURVEY 8(a) a16)")
+    ap.add_argument("--devices", default=None, metavar="LIST",
+                    help="one process over the row shards on these devices (comma list, repeats "
+                         "allowed): the in-library multi-device context (sgp_ctx_create_multi, "
+                         "RCCL inside libsgp) -- the path an R caller of the drop-in takes.  The "
+                         "driver's multi-GPU runs keep one process per GPU (torchrun)")
     args = ap.parse_args()
     if args.cpu_full:
         res = cpu_baseline_full()
@@ -243,6 +248,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.devices is not None:
+        if world > 1 or "RANK" in os.environ:
+            ap.error("--devices runs one process over several devices (not under torchrun)")
+        return bench_library_shards(args, [int(v) for v in args.devices.split(",")])
 
     import torch
     import torch.distributed as dist
@@ -419,6 +428,78 @@ def main():
     backend.close()
     if distributed:
         dist.destroy_process_group()
+
+
+def bench_library_shards(args, devices):
+    """The in-library multi-device context: the rows split into len(devices) shards, each
+    evaluation's reductions summed on the devices and over them by RCCL inside libsgp (one host
+    worker thread per distinct device).  With every shard on one GPU (e.g. --devices
+    0,0,0,0,0,0,0,0) this times C4's eight-way composition on a one-GPU box; on a node,
+    --devices 0,1,...,7 is the R drop-in's 8-GPU path."""
+    import torch
+
+    import sparsergps_amd as S
+    from sparsergps_amd.dist import shard_rows
+    P = make_problem(args.config, n=args.n, m=args.m, d=args.d)
+    n, m, d = P["X"].shape[0], P["U"].shape[0], P["X"].shape[1]
+    cov_fun = P["cov_fun"]
+    names = S.param_names(cov_fun, d)
+    theta0 = np.array([P["cov_par"][k] for k in names])
+    ctx = S.SparseGPContext(P["X"], P["y"], P["mu"], m_max=m, devices=devices)
+    nshards, ndev = ctx.shards()
+    U = np.asfortranarray(P["U"])
+    if args.mode == "laplace":
+        ctx.lap_set_f(P["f0"])
+
+    def run(k):
+        th = theta0 * np.exp(1e-3 * np.sin(np.arange(theta0.size) + k))
+        if args.mode == "vi":
+            return ctx.eval_vi(th, cov_fun, U, P["delta"])
+        if args.mode == "fitc":
+            return ctx.eval_fitc(th, cov_fun, U, P["delta"])
+        o, g, _ = ctx.eval_laplace(th, cov_fun, U, P["delta"], P["a"], args.tol_nr, 1000)
+        return o, g
+
+    for k in range(args.warmup):
+        run(k)
+    con_key = {"vi": "contract_knm", "fitc": "rowquad_q", "laplace": "rowquad_q"}[args.mode]
+    ctx.timing_filter(con_key)     # shard 0's launch stream (the timing calls follow shard 0)
+    ctx.enable_timing(True)
+    for dv in sorted(set(devices)):
+        torch.cuda.synchronize(dv)
+    t0 = time.perf_counter()
+    obj = None
+    for k in range(args.steps):
+        obj, _ = run(args.warmup + k)
+    for dv in sorted(set(devices)):
+        torch.cuda.synchronize(dv)
+    elapsed = time.perf_counter() - t0
+    evals = max(ctx.timing_evals(), 1)
+    t_con = dict(ctx.timings()).get(con_key, float("nan")) / evals * 1e-3
+    ctx.enable_timing(False)
+    n0 = shard_rows(n, nshards, 0)[1]
+    flops = 2.0 * n0 * m * m
+    achieved = flops / t_con / 1e12 if t_con > 0 else float("nan")
+    metric = {"vi": "sparse-GP objective+gradient evals/sec at n=1e6, m=1024, d=8",
+              "fitc": "FITC objective+gradient evals/sec (secondary mode)",
+              "laplace": "Poisson sparse-Laplace NR+objective+gradient evals/sec (C5, secondary)"}
+    out = {"metric": metric[args.mode], "value": args.steps / elapsed, "unit": "evals/s",
+           "n_gpus": ndev, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+           "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+           "data": f"synthetic (SURVEY.md 8(d) {args.config} generator, numpy PCG64)",
+           "config": {"workload": f"{args.config} {args.mode}, n={n}, m={m}, d={d}, {cov_fun}",
+                      "n": n, "m": m, "d": d, "kernel": cov_fun,
+                      "parallelism": f"library-rows{nshards} on {ndev} device(s)",
+                      "devices": devices},
+           "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
+                        "kernel": con_key + " of shard 0", "flops_per_launch": flops},
+           "objective": obj,
+           "note": "in-library multi-device context (sgp_ctx_create_multi); shards on one "
+                   "device run one after another on it"}
+    print(json.dumps(out), flush=True)
+    ctx.close()
 
 
 if __name__ == "__main__":
