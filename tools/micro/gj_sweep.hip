@@ -1,0 +1,154 @@
+// Round 5: the 16 scalar sweeps of a 16x16 SPD diagonal block (the serial core of the
+// Gauss-Jordan pivot, k_dense.hip gj_pivot_body) in two register layouts, one wave, timed over
+// many repetitions (the block L2-resident):
+//   cur: lane (lr, lc) holds rows lr + 4q of column lc (MFMA accumulator layout); row k by
+//        ds_bpermute, column k by DPP row_newbcast, the pivot by readlane (k_dense.hip today);
+//   col: every 16-lane row holds the whole block, lane c column c (16 registers); a sweep is one
+//        v_fmac_f64_dpp per element (src0 = lane k's register by row_newbcast), the pivot lane's
+//        column kept unscaled with a pending factor (applied once after the 16 sweeps).
+//   build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form -o gj_sweep gj_sweep.hip
+#include <cmath>
+#include <cstdio>
+#include <random>
+#include <vector>
+
+#include "../../sparsergps_amd/csrc/k_dense.hip"
+
+namespace {
+#include "gj_fmac_bcast.inc"
+
+// the current sweep (gj_pivot_body's wave-kb loop), on a tile in accumulator layout
+__device__ __forceinline__ void sweep_cur(d4& t, double (&dk)[16]) {
+  const int lane = threadIdx.x & 63, lr = lane >> 4, lc = lane & 15;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int kq = k >> 2, kr = k & 3;
+    const double vc = __shfl(t[kq], lc + 16 * kr, 64);
+    const double d = readlane_f64(t[kq], k + 16 * kr);
+    double vr[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) vr[q] = row_bcast_f64(t[q], k);
+    const double r = rcp_nr(d);
+    dk[k] = d;
+    const double vj = (lc == k) ? -1.0 : vc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = lr + 4 * q;
+      const double vi = (i == k) ? -r : vr[q] * r;
+      const double base = (i == k || lc == k) ? 0.0 : t[q];
+      t[q] = fma(-vi, vj, base);
+    }
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void sweep_col_step(double (&R)[16], double (&dk)[16], double& sig,
+                                               int c) {
+  const double d = row_bcast_f64<K>(R[K]);
+  dk[K] = d;
+  const double r = rcp_nr(d);
+  const bool piv = c == K;
+  const double f = piv ? 0.0 : R[K] * r;
+  fmac_bcast<K>(R, -f);
+  R[K] = piv ? -1.0 : f;
+  sig = piv ? r : sig;
+}
+
+__device__ __forceinline__ void sweep_col(double (&R)[16], double (&dk)[16]) {
+  const int c = threadIdx.x & 15;
+  double sig = 1.0;
+  sweep_col_step<0>(R, dk, sig, c);   sweep_col_step<1>(R, dk, sig, c);
+  sweep_col_step<2>(R, dk, sig, c);   sweep_col_step<3>(R, dk, sig, c);
+  sweep_col_step<4>(R, dk, sig, c);   sweep_col_step<5>(R, dk, sig, c);
+  sweep_col_step<6>(R, dk, sig, c);   sweep_col_step<7>(R, dk, sig, c);
+  sweep_col_step<8>(R, dk, sig, c);   sweep_col_step<9>(R, dk, sig, c);
+  sweep_col_step<10>(R, dk, sig, c);  sweep_col_step<11>(R, dk, sig, c);
+  sweep_col_step<12>(R, dk, sig, c);  sweep_col_step<13>(R, dk, sig, c);
+  sweep_col_step<14>(R, dk, sig, c);  sweep_col_step<15>(R, dk, sig, c);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) R[i] *= sig;
+}
+
+// B: 16 x 16 row-major; out: the swept block (-inv(B)); piv: the 16 pivots
+__global__ void __launch_bounds__(64) k_cur(const double* B, double* out, double* piv, int reps) {
+  const int lane = threadIdx.x, lr = lane >> 4, lc = lane & 15;
+  double dk[16];
+  d4 t;
+  for (int r = 0; r < reps; ++r) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] = B[(lr + 4 * q) * 16 + lc];
+    sweep_cur(t, dk);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[(lr + 4 * q) * 16 + lc] = t[q];
+  }
+  if (lane < 16) {
+    double v = dk[0];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) v = (lane == k) ? dk[k] : v;
+    piv[lane] = v;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_col(const double* B, double* out, double* piv, int reps) {
+  const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+  double dk[16], R[16];
+  for (int r = 0; r < reps; ++r) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) R[i] = B[i * 16 + c];
+    sweep_col(R, dk);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      // row group g writes rows 4g .. 4g + 3 (static register indices via a select chain)
+      const double v = g == 0 ? R[q] : g == 1 ? R[4 + q] : g == 2 ? R[8 + q] : R[12 + q];
+      out[(4 * g + q) * 16 + c] = v;
+    }
+  }
+  if (lane < 16) {
+    double v = dk[0];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) v = (lane == k) ? dk[k] : v;
+    piv[lane] = v;
+  }
+}
+}  // namespace
+
+int main() {
+  std::mt19937_64 gen(5);
+  std::normal_distribution<double> N01;
+  std::vector<double> G(16 * 16), B(16 * 16, 0.0), O(16 * 16), pv(16);
+  for (auto& v : G) v = N01(gen);
+  for (int i = 0; i < 16; ++i)
+    for (int j = 0; j < 16; ++j) {
+      double s = 0;
+      for (int k = 0; k < 16; ++k) s += G[i * 16 + k] * G[j * 16 + k];
+      B[i * 16 + j] = s / 16 + (i == j ? 0.5 : 0.0) + (i == j ? 3e3 * (i % 3) : 0.0);
+    }
+  double *dB, *dO, *dP;
+  hipMalloc(&dB, 16 * 16 * 8); hipMalloc(&dO, 16 * 16 * 8); hipMalloc(&dP, 16 * 8);
+  hipMemcpy(dB, B.data(), 16 * 16 * 8, hipMemcpyHostToDevice);
+  hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+  const char* names[2] = {"cur (accumulator layout)", "col (v_fmac_f64_dpp)"};
+  for (int it = 0; it < 3; ++it)
+    for (int v = 0; v < 2; ++v) {
+      const int reps = 20000;
+      hipEventRecord(e0, 0);
+      if (v == 0) hipLaunchKernelGGL(k_cur, dim3(1), dim3(64), 0, 0, dB, dO, dP, reps);
+      else hipLaunchKernelGGL(k_col, dim3(1), dim3(64), 0, 0, dB, dO, dP, reps);
+      hipEventRecord(e1, 0); hipEventSynchronize(e1);
+      float ms; hipEventElapsedTime(&ms, e0, e1);
+      hipMemcpy(O.data(), dO, 16 * 16 * 8, hipMemcpyDeviceToHost);
+      hipMemcpy(pv.data(), dP, 16 * 8, hipMemcpyDeviceToHost);
+      double err = 0, ld = 0;   // || B (-O) - I ||_max
+      for (int i = 0; i < 16; ++i) {
+        ld += log(pv[i]);
+        for (int j = 0; j < 16; ++j) {
+          double s = 0;
+          for (int k = 0; k < 16; ++k) s -= B[i * 16 + k] * O[k * 16 + j];
+          err = fmax(err, fabs(s - (i == j ? 1.0 : 0.0)));
+        }
+      }
+      printf("%-26s %7.3f us per 16 sweeps (%6.1f ns/sweep)  |B inv - I| %.2e  sum log piv %.15f\n",
+             names[v], ms * 1e3 / reps, ms * 1e6 / reps / 16, err, ld);
+    }
+  return 0;
+}
