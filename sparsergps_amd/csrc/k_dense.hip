@@ -97,74 +97,6 @@ __device__ __forceinline__ double row_bcast_f64(double v, int k) {
   }
 }
 
-// ---- the 16 scalar sweeps of a 16 x 16 diagonal block in the column layout (round 5) ----
-// Every 16-lane row of the pivot wave holds the whole block, lane c its column c in 16 registers
-// R[0..15].  Sweep k: d = W_kk (lane k's R[k], DPP row_newbcast), r = 1/d, and for every lane
-// c != k the row entry f = W_kc r; then W_ic -= W_ik f for all i -- ONE v_fmac_f64_dpp per
-// register, its src0 read from lane k of the row by row_newbcast (gfx90a+ DPP64), so a sweep is
-// ~30 instructions with no LDS or scalar round trip (the accumulator-layout sweep needed a
-// ds_bpermute for the row, a readlane for the pivot and ~45 instructions).  The pivot lane's own
-// column must become W_ik / d: it runs the same FMAs with f = 0 (unchanged) and keeps a pending
-// factor sig = r, applied once after the 16 sweeps; its row entry is stored as -1 (= -r / sig).
-// The s_nop covers the VALU-write -> DPP-read hazard the compiler cannot see inside the asm.
-#define SGP_GJ_F(i, K) \
-  "v_fmac_f64_dpp %" #i ", %" #i ", %16 row_newbcast:" #K " row_mask:0xf bank_mask:0xf\n"
-#define SGP_GJ_FMAC16(K)                                                                       \
-  asm volatile("s_nop 1\n" SGP_GJ_F(0, K) SGP_GJ_F(1, K) SGP_GJ_F(2, K) SGP_GJ_F(3, K)          \
-               SGP_GJ_F(4, K) SGP_GJ_F(5, K) SGP_GJ_F(6, K) SGP_GJ_F(7, K) SGP_GJ_F(8, K)        \
-               SGP_GJ_F(9, K) SGP_GJ_F(10, K) SGP_GJ_F(11, K) SGP_GJ_F(12, K) SGP_GJ_F(13, K)   \
-               SGP_GJ_F(14, K) SGP_GJ_F(15, K)                                                 \
-               : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]), "+v"(R[4]), "+v"(R[5]),        \
-                 "+v"(R[6]), "+v"(R[7]), "+v"(R[8]), "+v"(R[9]), "+v"(R[10]), "+v"(R[11]),      \
-                 "+v"(R[12]), "+v"(R[13]), "+v"(R[14]), "+v"(R[15])                             \
-               : "v"(nf))
-
-// R_i += (lane K's R_i) * nf for all i (i = K included: R[K] is overwritten afterwards)
-template <int K>
-__device__ __forceinline__ void gj_fmac_bcast(double (&R)[16], double nf) {
-  switch (K) {
-    case 0: SGP_GJ_FMAC16(0); break;    case 1: SGP_GJ_FMAC16(1); break;
-    case 2: SGP_GJ_FMAC16(2); break;    case 3: SGP_GJ_FMAC16(3); break;
-    case 4: SGP_GJ_FMAC16(4); break;    case 5: SGP_GJ_FMAC16(5); break;
-    case 6: SGP_GJ_FMAC16(6); break;    case 7: SGP_GJ_FMAC16(7); break;
-    case 8: SGP_GJ_FMAC16(8); break;    case 9: SGP_GJ_FMAC16(9); break;
-    case 10: SGP_GJ_FMAC16(10); break;  case 11: SGP_GJ_FMAC16(11); break;
-    case 12: SGP_GJ_FMAC16(12); break;  case 13: SGP_GJ_FMAC16(13); break;
-    case 14: SGP_GJ_FMAC16(14); break;  default: SGP_GJ_FMAC16(15); break;
-  }
-}
-#undef SGP_GJ_FMAC16
-#undef SGP_GJ_F
-
-template <int K>
-__device__ __forceinline__ void gj_sweep_col_step(double (&R)[16], double (&dk)[16], double& sig,
-                                                  int c) {
-  const double d = row_bcast_f64<K>(R[K]);
-  dk[K] = d;
-  const double r = rcp_nr(d);
-  const bool piv = c == K;
-  const double f = piv ? 0.0 : R[K] * r;
-  gj_fmac_bcast<K>(R, -f);
-  R[K] = piv ? -1.0 : f;
-  sig = piv ? r : sig;
-}
-
-// the 16 sweeps; R ends as the swept block (-inv(W_KK)), dk holds the pivots
-__device__ __forceinline__ void gj_sweep_col(double (&R)[16], double (&dk)[16]) {
-  const int c = threadIdx.x & 15;
-  double sig = 1.0;
-  gj_sweep_col_step<0>(R, dk, sig, c);   gj_sweep_col_step<1>(R, dk, sig, c);
-  gj_sweep_col_step<2>(R, dk, sig, c);   gj_sweep_col_step<3>(R, dk, sig, c);
-  gj_sweep_col_step<4>(R, dk, sig, c);   gj_sweep_col_step<5>(R, dk, sig, c);
-  gj_sweep_col_step<6>(R, dk, sig, c);   gj_sweep_col_step<7>(R, dk, sig, c);
-  gj_sweep_col_step<8>(R, dk, sig, c);   gj_sweep_col_step<9>(R, dk, sig, c);
-  gj_sweep_col_step<10>(R, dk, sig, c);  gj_sweep_col_step<11>(R, dk, sig, c);
-  gj_sweep_col_step<12>(R, dk, sig, c);  gj_sweep_col_step<13>(R, dk, sig, c);
-  gj_sweep_col_step<14>(R, dk, sig, c);  gj_sweep_col_step<15>(R, dk, sig, c);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) R[i] *= sig;
-}
-
 __device__ __forceinline__ void gj_pivot_body(const double* B, int64_t ldb, int64_t gofs,
                                               double* __restrict__ P,
                                               double* __restrict__ logd_slot,
@@ -195,28 +127,7 @@ __device__ __forceinline__ void gj_pivot_body(const double* B, int64_t ldb, int6
 #pragma unroll
     for (int q = 0; q < 4; ++q) Es[(16 * wv + lr + 4 * q) * GJP_LD + lc] = acc[kb][q];
     __syncthreads();
-    if (wv == kb && SGP_GJ_SWEEP_COL) {
-      // the column layout: W_KK from the published panel (rows 16 kb .. of E), swept, written
-      // to Qs (row group g: rows 4g .. 4g + 3) and read back in the accumulator layout
-      double R[16], dk[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) R[i] = Es[(16 * kb + i) * GJP_LD + lc];
-      gj_sweep_col(R, dk);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        Qs[(4 * lr + q) * GJP_LD + lc] =
-            lr == 0 ? R[q] : lr == 1 ? R[4 + q] : lr == 2 ? R[8 + q] : R[12 + q];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc[kb][q] = Qs[(lr + 4 * q) * GJP_LD + lc];
-      double dl = dk[0];
-#pragma unroll
-      for (int k = 1; k < 16; ++k) dl = (lane == k) ? dk[k] : dl;
-      const bool bad = lane < 16 && (!(dl > 0.0) || !isfinite(dl));
-      const unsigned long long badm = __ballot(bad);
-      if (lane < 16) piv[16 * kb + lane] = dl;
-      if (lane == 0 && badm)
-        atomicCAS(status, 0, (int)(gofs + 16 * kb + __builtin_ctzll(badm) + 1));
-    } else if (wv == kb) {
+    if (wv == kb) {
       // 16 scalar sweeps of W_KK in registers: lane (lr, lc) holds rows lr + 4q of column lc
       double dk[16];                                                       // the pivots
 #pragma unroll

@@ -28,7 +28,6 @@
 //                       SIMD), 1 (half the rows, 4 waves), 2 (twice the rows, 2 waves)
 //   SGP_GJ_MM_UNROLL    unroll of gj_mm64's 16 k-substeps (16; 4 before round 4)
 //   SGP_S256_IL         1: k_syrk_s256's step with an interleave request
-//   SGP_GJ_SWEEP_COL    0: the Gauss-Jordan pivot's 16x16 sweeps in the accumulator layout
 #pragma once
 
 #if (defined(SGP_CON_TRACE) || defined(SGP_CON_NO_EPILOGUE) || defined(SGP_GJ_TRACE) ||       \
@@ -37,7 +36,7 @@
      defined(SGP_SYRK_BAL) || defined(SGP_SDT_IL) || defined(SGP_S256_IL) ||                  \
      defined(SGP_SDT_W) || defined(SGP_SDT_WW) || defined(SGP_SDT_WT) ||                      \
      defined(SGP_SYRK_W3) || defined(SGP_CON_ROWQ_KU) ||                                      \
-     defined(SGP_LAP_RS_CFG) || defined(SGP_GJ_MM_UNROLL) || defined(SGP_GJ_SWEEP_COL)) &&                                 \
+     defined(SGP_LAP_RS_CFG) || defined(SGP_GJ_MM_UNROLL)) &&                                 \
     !defined(SGP_PROBE_BUILD)
 #error "timing probes and experiment knobs are for variant builds only (SGP_PROBE_BUILD)"
 #endif
@@ -74,9 +73,6 @@
 #endif
 #ifndef SGP_SYRK_W3
 #define SGP_SYRK_W3 1
-#endif
-#ifndef SGP_GJ_SWEEP_COL
-#define SGP_GJ_SWEEP_COL 1
 #endif
 #ifndef SGP_CON_ROWQ_KU
 #define SGP_CON_ROWQ_KU 0
