@@ -263,6 +263,7 @@ struct sgp_ctx {
   hipEvent_t ev_lo = nullptr;             // VI phase 1: builder done (main) / side work done (aux_lo)
   bool vi_k22_ordered = true;             // VI phase 1 ordered main behind K22's build (ev_lo)
   bool pack_red1 = false;                 // VI red1 carries S as packed lower 64-blocks
+  bool borrowed_streams = false;          // own / aux / aux_lo belong to another context
   double* Sfull = nullptr;                // S unpacked from a packed red1 (mp_max^2)
   hipStream_t aux_lo = nullptr;           // ... at normal priority (the Bm chain keeps its CUs)
   double* slab_aux = nullptr;             // partials of the aux stream's small reductions
@@ -449,10 +450,10 @@ void ctx_free(sgp_ctx* c) {
   if (c->ev_m3) hipEventDestroy(c->ev_m3);
   if (c->ev_bm) hipEventDestroy(c->ev_bm);
   if (c->ev_lo) hipEventDestroy(c->ev_lo);
-  if (c->aux) hipStreamDestroy(c->aux);
-  if (c->aux_lo) hipStreamDestroy(c->aux_lo);
+  if (c->aux && !c->borrowed_streams) hipStreamDestroy(c->aux);
+  if (c->aux_lo && !c->borrowed_streams) hipStreamDestroy(c->aux_lo);
   for (hipEvent_t e : c->pool) hipEventDestroy(e);
-  if (c->own) hipStreamDestroy(c->own);
+  if (c->own && !c->borrowed_streams) hipStreamDestroy(c->own);
 }
 
 // n host values -> device vector of n_pad (zero padded), synchronous
@@ -564,6 +565,26 @@ void sgp_internal_set_err(const char* msg) { set_err("%s", msg); }
 void sgp_internal_forget_eval(sgp_ctx* c) {
   c->last_mode = 0;
   c->lap_gpsi_valid = false;
+}
+
+hipStream_t sgp_internal_stream(sgp_ctx* c) { return c->stream; }
+
+// c takes over src's three streams (same device; c's own are idle after creation): the shards
+// of one device then use the streams of the first, not three more hardware-queue clients each
+int sgp_internal_share_streams(sgp_ctx* c, sgp_ctx* src) {
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->own));
+  HIPCHK(hipStreamSynchronize(c->aux));
+  HIPCHK(hipStreamSynchronize(c->aux_lo));
+  (void)hipStreamDestroy(c->own);
+  (void)hipStreamDestroy(c->aux);
+  (void)hipStreamDestroy(c->aux_lo);
+  c->own = src->own;
+  c->stream = src->stream;
+  c->aux = src->aux;
+  c->aux_lo = src->aux_lo;
+  c->borrowed_streams = true;
+  return SGP_OK;
 }
 
 // =========================================================================== public API

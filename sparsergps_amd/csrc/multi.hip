@@ -31,6 +31,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -140,72 +142,93 @@ struct MultiCtx {
   bool knot_on = false;
   std::vector<double> xmin, xmax;   // column ranges of all rows
 
-  // ---- worker pool: one thread per group
+  // ---- workers: the calling thread runs group 0, one thread each the other groups.  Hand-offs
+  // spin (bounded, then yield / sleep on the condition variable): a condition-variable wake-up
+  // costs tens to hundreds of microseconds, paid at the start of every evaluation and at every
+  // barrier (measured: the builder started ~0.4 ms after the previous evaluation's readback
+  // with blocking hand-offs)
+  static constexpr int SPIN = 1 << 16;
   std::vector<std::thread> threads;
   std::mutex mu;
-  std::condition_variable cv_job, cv_done;
+  std::condition_variable cv_job;
   std::function<int(int)> job;
-  uint64_t job_gen = 0;
-  int pending = 0;
-  bool quit = false;
+  std::atomic<uint64_t> job_gen{0};
+  std::atomic<int> pending{0};
+  std::atomic<bool> quit{false};
 
   // ---- barrier with a vote (all ok? any / all done?)
   std::mutex bmu;
-  std::condition_variable bcv;
+  std::atomic<uint64_t> b_gen{0};
   int b_count = 0;
-  uint64_t b_gen = 0;
   bool b_all_ok = true, b_any = false, b_all = true;
   bool r_ok = true, r_any = false, r_all = true;
+
+  static void relax(int& spins) {
+    if (++spins < SPIN) {
+      __builtin_ia32_pause();
+    } else {
+      std::this_thread::yield();
+    }
+  }
+
+  void run_group(int g, const std::function<int(int)>& f) {
+    Group& gr = groups[(size_t)g];
+    gr.err.clear();
+    gr.status = f(g);
+    if (gr.status != SGP_OK && gr.status != ABORTED) gr.err = sgp_last_error();
+  }
 
   void worker(int g) {
     uint64_t seen = 0;
     for (;;) {
-      std::function<int(int)> f;
-      {
-        std::unique_lock<std::mutex> lk(mu);
-        cv_job.wait(lk, [&] { return quit || job_gen != seen; });
-        if (quit) return;
-        seen = job_gen;
-        f = job;
+      int spins = 0;
+      while (job_gen.load(std::memory_order_acquire) == seen && !quit.load()) {
+        if (spins < SPIN) {
+          relax(spins);
+        } else {   // idle for long: sleep until the next job
+          std::unique_lock<std::mutex> lk(mu);
+          cv_job.wait_for(lk, std::chrono::milliseconds(2), [&] {
+            return quit.load() || job_gen.load(std::memory_order_acquire) != seen;
+          });
+        }
       }
-      Group& gr = groups[(size_t)g];
-      gr.err.clear();
-      gr.status = f(g);
-      if (gr.status != SGP_OK && gr.status != ABORTED) gr.err = sgp_last_error();
-      {
-        std::lock_guard<std::mutex> lk(mu);
-        if (--pending == 0) cv_done.notify_all();
-      }
+      if (quit.load()) return;
+      seen = job_gen.load(std::memory_order_acquire);
+      run_group(g, job);
+      pending.fetch_sub(1, std::memory_order_acq_rel);
     }
   }
 
   void start_workers() {
-    for (int g = 0; g < (int)groups.size(); ++g) threads.emplace_back([this, g] { worker(g); });
+    for (int g = 1; g < (int)groups.size(); ++g) threads.emplace_back([this, g] { worker(g); });
   }
 
   void stop_workers() {
     {
       std::lock_guard<std::mutex> lk(mu);
-      quit = true;
+      quit.store(true);
     }
     cv_job.notify_all();
     for (std::thread& t : threads) t.join();
     threads.clear();
   }
 
-  // run f(g) on every group's worker and wait; the first real error is reported
+  // run f(g) for every group (group 0 on this thread) and wait; the first real error is
+  // reported
   int run_all(std::function<int(int)> f) {
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      job = std::move(f);
-      pending = (int)groups.size();
-      ++job_gen;
+    const int G = (int)groups.size();
+    if (G > 1) {
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        job = f;
+        pending.store(G - 1, std::memory_order_release);
+        job_gen.fetch_add(1, std::memory_order_acq_rel);
+      }
+      cv_job.notify_all();
     }
-    cv_job.notify_all();
-    {
-      std::unique_lock<std::mutex> lk(mu);
-      cv_done.wait(lk, [&] { return pending == 0; });
-    }
+    run_group(0, f);
+    int spins = 0;
+    while (pending.load(std::memory_order_acquire) > 0) relax(spins);
     int st = SGP_OK;
     for (const Group& g : groups)
       if (g.status != SGP_OK && g.status != ABORTED) {
@@ -218,27 +241,40 @@ struct MultiCtx {
     return st;
   }
 
-  // every worker arrives with its status (and a done flag); returns false for all when any
-  // worker failed, and sets *any_done / *all_done from the votes
+  // every group arrives with its status (and a done flag); returns false for all when any
+  // group failed, and sets *any_done / *all_done from the votes
   bool arrive(bool ok, bool done = false, bool* any_done = nullptr, bool* all_done = nullptr) {
-    std::unique_lock<std::mutex> lk(bmu);
-    const uint64_t gen = b_gen;
-    b_all_ok = b_all_ok && ok;
-    b_any = b_any || done;
-    b_all = b_all && done;
-    if (++b_count == (int)groups.size()) {
-      r_ok = b_all_ok;
-      r_any = b_any;
-      r_all = b_all;
-      b_all_ok = true;
-      b_any = false;
-      b_all = true;
-      b_count = 0;
-      ++b_gen;
-      bcv.notify_all();
-    } else {
-      bcv.wait(lk, [&] { return b_gen != gen; });
+    const int G = (int)groups.size();
+    if (G == 1) {
+      if (any_done) *any_done = done;
+      if (all_done) *all_done = done;
+      return ok;
     }
+    uint64_t gen;
+    bool last = false;
+    {
+      std::lock_guard<std::mutex> lk(bmu);
+      gen = b_gen.load(std::memory_order_relaxed);
+      b_all_ok = b_all_ok && ok;
+      b_any = b_any || done;
+      b_all = b_all && done;
+      if (++b_count == G) {
+        r_ok = b_all_ok;
+        r_any = b_any;
+        r_all = b_all;
+        b_all_ok = true;
+        b_any = false;
+        b_all = true;
+        b_count = 0;
+        last = true;
+        b_gen.store(gen + 1, std::memory_order_release);
+      }
+    }
+    if (!last) {
+      int spins = 0;
+      while (b_gen.load(std::memory_order_acquire) == gen) relax(spins);
+    }
+    std::lock_guard<std::mutex> lk(bmu);   // r_* of this round: the next round needs every group
     if (any_done) *any_done = r_any;
     if (all_done) *all_done = r_all;
     return r_ok;
@@ -306,16 +342,18 @@ struct MultiCtx {
       (void)hipSetDevice(g.device);
       if (g.stream) (void)hipStreamSynchronize(g.stream);
     }
-    for (Shard& s : shards) {
-      if (s.ctx) sgp_ctx_destroy(s.ctx);
-      s.ctx = nullptr;
+    // (an evaluation's aux-stream work is joined into the launch stream before it returns)
+    // reverse order: a device's first shard owns the streams its other shards borrow
+    for (size_t k = shards.size(); k-- > 0;) {
+      if (shards[k].ctx) sgp_ctx_destroy(shards[k].ctx);
+      shards[k].ctx = nullptr;
     }
     for (Group& g : groups) {
       (void)hipSetDevice(g.device);
       if (g.comm) rccl().comm_destroy(g.comm);
       for (double*& p : g.red)
         if (p) (void)hipFree(p);
-      if (g.stream) (void)hipStreamDestroy(g.stream);
+      g.stream = nullptr;   // the first shard's, destroyed with it
     }
     for (Shard& s : shards)
       if (s.part) {
@@ -375,11 +413,12 @@ int multi_create(MultiCtx** out, const int* devices, int nshards, const double* 
     mc->xmin[(size_t)q] = lo;
     mc->xmax[(size_t)q] = hi;
   }
-  // per device: stream, summed buffers, the shards' partial buffers
+  // per device: summed buffers, the shards' partial buffers (the launch stream is the first
+  // shard's own: no extra hardware-queue client -- with more streams than the process's hardware
+  // queues (GPU_MAX_HW_QUEUES, 4) the latency-bound Gauss-Jordan steps ran 2.4x slower)
   int st = SGP_OK;
   for (Group& g : mc->groups) {
     hipError_t e = hipSetDevice(g.device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking);
     for (int b = 0; b < 2 && e == hipSuccess; ++b)
       e = hipMalloc(reinterpret_cast<void**>(&g.red[b]), sizeof(double) * (size_t)cap);
     for (size_t q = 0; q < g.shards.size() && g.shards.size() > 1 && e == hipSuccess; ++q)
@@ -427,7 +466,9 @@ int multi_create(MultiCtx** out, const int* devices, int nshards, const double* 
       Shard& s = mc->shards[(size_t)g.shards[q]];
       s2 = sgp_ctx_create(&s.ctx, s.device, X + s.row0, s.rows, ldx, d, y + s.row0, mu + s.row0,
                           m_max);
-      if (!s2) s2 = sgp_ctx_set_stream(s.ctx, g.stream);
+      if (!s2 && q == 0) g.stream = sgp_internal_stream(s.ctx);
+      // the device's other shards use the first one's streams (one worker issues them in turn)
+      if (!s2 && q > 0) s2 = sgp_internal_share_streams(s.ctx, mc->shards[(size_t)g.shards[0]].ctx);
       if (!s2) s2 = sgp_ctx_set_packed_reduction(s.ctx, 1);   // all-reduce #1: 53 % of S
     }
     return s2;

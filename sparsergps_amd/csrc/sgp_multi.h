@@ -5,6 +5,7 @@
 // worker thread per distinct device, and an RCCL communicator over those devices.  capi.hip's
 // public functions forward to the multi_* functions below when c->multi is set.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/sgp.h"
@@ -16,6 +17,8 @@ struct MultiCtx;
 // capi.hip hooks used by multi.hip
 void sgp_internal_set_err(const char* msg);
 void sgp_internal_forget_eval(sgp_ctx* c);   // no posterior / grad psi after candidate scoring
+hipStream_t sgp_internal_stream(sgp_ctx* c);  // the context's launch stream
+int sgp_internal_share_streams(sgp_ctx* c, sgp_ctx* src);   // c uses src's three streams
 
 int multi_create(MultiCtx** out, const int* devices, int nshards, const double* X, int64_t n,
                  int64_t ldx, int d, const double* y, const double* mu, int64_t m_max);
