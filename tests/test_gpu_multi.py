@@ -165,10 +165,19 @@ def test_candidates_on_shards(sgp):
         with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=65, devices=dv) as c:
             res[key] = (c.vi_candidates(th, "sqexp", P["U"], cand, P["delta"]),
                         c.fitc_candidates(th, "sqexp", P["U"], cand, P["delta"]))
+            if dv is not None:   # the sharded path is deterministic: bit-identical on repeat
+                again = (c.vi_candidates(th, "sqexp", P["U"], cand, P["delta"]),
+                         c.fitc_candidates(th, "sqexp", P["U"], cand, P["delta"]))
+                np.testing.assert_array_equal(again[0], res[key][0])
+                np.testing.assert_array_equal(again[1], res[key][1])
     # VI: two different algorithms for the same bordered ELBO (Schur update vs a rebuild), ~4e4
-    # in magnitude: they agree to a few 1e-10 relative; FITC: the same algorithm on both sides
+    # in magnitude; FITC: the same algorithm over different row-sum orders.  A candidate next to
+    # a knot makes the bordered K22 ill-conditioned, so the objectives (sums of ~1e5-sized terms)
+    # agree to a few 1e-10 relative -- far inside the 1e-6 north-star bar
+    print(f"\n[candidates] VI {np.max(np.abs(res['multi'][0] / res['one'][0] - 1)):.2e} "
+          f"FITC {np.max(np.abs(res['multi'][1] / res['one'][1] - 1)):.2e}")
     np.testing.assert_allclose(res["multi"][0], res["one"][0], rtol=1e-8)
-    np.testing.assert_allclose(res["multi"][1], res["one"][1], rtol=1e-10)
+    np.testing.assert_allclose(res["multi"][1], res["one"][1], rtol=1e-8)
 
 
 def test_refused_entry_points_and_recovery(sgp):
