@@ -573,9 +573,13 @@ k_syrk_reduce_blk(const double* __restrict__ slab, int splits, int64_t nblk, int
   const int cp = (int)(bid - (int64_t)rp * (rp + 1) / 2);
   // a diagonal 64-block's upper fragments are not written by k_syrk_s256: the lower element of
   // each symmetric pair writes both (a, b) and (b, a), for both SYRK kernels (packed: the
-  // block as it is, its upper fragments zero; k_unpack_lower64 mirrors)
+  // block as it is, its upper fragments zero; k_unpack_lower64 mirrors).  Inside a diagonal
+  // 16 x 16 fragment both elements of a pair are computed; with weights they differ in the last
+  // bit ((w_k K_ka) K_kb against (w_k K_kb) K_ka), so only the lower one (row >= column) may
+  // write the pair -- two writers of one address made FITC and Laplace non-deterministic
   const bool upper = rp == cp && (e / 64) / 16 < (e % 64) / 16;
   if (upper && !packed) return;
+  if (!packed && rp == cp && (e / 64) < (e % 64)) return;
   // the balanced plan keeps the diagonal 128-tiles' blocks in their own slab region
   if (slab_d && rp / 2 == cp / 2) {
     slab = slab_d;
@@ -595,8 +599,7 @@ k_syrk_reduce_blk(const double* __restrict__ slab, int splits, int64_t nblk, int
 }
 
 // Full symmetric S (mp x mp) from its packed lower 64-blocks (k_syrk_reduce_blk, packed): an
-// element below the block diagonal, or in a diagonal block's lower 16x16 fragments, is read
-// as stored, the rest from its mirror.
+// element on or below the diagonal is read as stored, the rest from its mirror.
 __global__ void __launch_bounds__(256)
 k_unpack_lower64(const double* __restrict__ packed, int64_t mp, double* __restrict__ S) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -604,7 +607,9 @@ k_unpack_lower64(const double* __restrict__ packed, int64_t mp, double* __restri
   const int64_t a = idx / mp, b = idx % mp;
   const int64_t ra = a / 64, rb = b / 64;
   const int ia = (int)(a % 64), ib = (int)(b % 64);
-  const bool lower = ra > rb || (ra == rb && ia / 16 >= ib / 16);
+  // the lower element of every pair (row >= column), also inside a diagonal 16 x 16 fragment,
+  // where both are stored: S comes out exactly symmetric, as the unpacked reduction writes it
+  const bool lower = ra > rb || (ra == rb && ia >= ib);
   const int64_t r = lower ? ra : rb, c = lower ? rb : ra;
   const int i = lower ? ia : ib, j = lower ? ib : ia;
   S[idx] = packed[(r * (r + 1) / 2 + c) * 4096 + i * 64 + j];
