@@ -20,6 +20,7 @@
 
 #include "../../include/sgp.h"
 #include "sgp_internal.h"
+#include "sgp_probe.h"
 #include "sgp_multi.h"
 
 namespace {
@@ -219,6 +220,9 @@ struct sgp_ctx {
   double *K22 = nullptr, *K22inv = nullptr, *Bm = nullptr, *Binv = nullptr, *Pm = nullptr;
   double *Xt = nullptr, *T1 = nullptr, *M3 = nullptr;
   double *Xt22 = nullptr, *T22 = nullptr;  // K22-stage temporaries (aux stream)
+  // sync words of the two Gauss-Jordan chains that can run together: [0] main stream (Bm),
+  // [SGP_GJ_SYNC_WORDS] the aux stream's K22 chain (dense_spd_inverse: zero between launches)
+  unsigned* gjs = nullptr;
   double *dinv = nullptr, *dinv22 = nullptr, *logd22 = nullptr, *logdB = nullptr;
   double *uvec = nullptr, *cdiag = nullptr;
   int* status = nullptr;
@@ -395,6 +399,16 @@ void timers_reset(sgp_ctx* c) {
   c->pool_used = 0;
 }
 
+// a Gauss-Jordan chain whose watchdog expired (k_dense.hip: status -1; never expected)
+static bool chain_watchdog(const int* status) {
+  for (int q = 0; q < 3; ++q)
+    if (status[q] < 0) {
+      set_err("internal error: a Gauss-Jordan chain's wait watchdog expired");
+      return true;
+    }
+  return false;
+}
+
 template <typename T>
 int dalloc(T** p, int64_t count) {
   *p = nullptr;
@@ -435,7 +449,7 @@ void ctx_free(sgp_ctx* c) {
                   c->Xt22,   c->T22,    c->dinv22, c->omega, c->pvec, c->rowq, c->red2f,
                   c->y,      c->mu,     c->lv,     c->lm,    c->lslab, c->lred[0], c->lred[1],
                   c->Cprev,  c->knot_slab, c->knot_part, c->knot_kmm, c->tslab, c->tq, c->tp,
-                  c->rr_dev, c->Sfull};
+                  c->rr_dev, c->Sfull, c->gjs};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->khash) hipFree(c->khash);
@@ -783,6 +797,11 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->dinv22, mm / SGP_DB * SGP_DB);
   st = st ? st : dalloc(&c->Xt22, mm);
   st = st ? st : dalloc(&c->T22, mm);
+  st = st ? st : dalloc(&c->gjs, 2 * SGP_GJ_SYNC_WORDS);
+  if (!st && hipMemset(c->gjs, 0, sizeof(unsigned) * 2 * SGP_GJ_SYNC_WORDS) != hipSuccess) {
+    set_err("hipMemset of the Gauss-Jordan sync words failed");
+    st = SGP_EHIP;
+  }
   st = st ? st : dalloc(&c->logd22, mp / SGP_DB);
   st = st ? st : dalloc(&c->logdB, mp / SGP_DB);
   st = st ? st : dalloc(&c->uvec, mp);
@@ -1202,8 +1221,12 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
     // diagonal tiles as cheap as the others); the first HIP call of the evaluation, so the
     // GPU starts on it as soon as the host gets here
     Scope t(c, "build_knm");
-    HIPCHK(launch_build_knm_t(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, mpv, m, mpv, c->K, c->r,
-                              c->tslab, &t_rows, c->stream, false));
+    if (SGP_VI_BUILD_NO_T)
+      HIPCHK(launch_build_knm(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, mpv, m, mpv, c->K,
+                              c->stream, false));
+    else
+      HIPCHK(launch_build_knm_t(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, mpv, m, mpv, c->K,
+                                c->r, c->tslab, &t_rows, c->stream, false));
   }
   // ev_knots after the builder: aux may build K22 from here on (first needed by phase 2), and
   // aux_lo may reduce the builder's t partials.  The SYRK goes right behind the builder (it
@@ -1269,7 +1292,8 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
 static int k22_factor_launches(sgp_ctx* c, hipStream_t s) {
   const int64_t mp = c->mp;
   // K22inv holds a copy of K22 already (k22_build writes both)
-  HIPCHK(dense_spd_inverse(c->K22inv, mp, c->Xt22, c->T22, c->dinv22, c->logd22, c->status, s));
+  HIPCHK(dense_spd_inverse(c->K22inv, mp, c->Xt22, c->dinv22, c->logd22, c->status,
+                           c->gjs + SGP_GJ_SYNC_WORDS, s));
   HIPCHK(launch_sum_and_diag(c->logd22, mp / SGP_DB, c->sc + SC_LD22, c->K22inv, mp, mp,
                              c->cdiag, s));
   return SGP_OK;
@@ -1323,7 +1347,7 @@ static int bm_stage(sgp_ctx* c, const double* S, double s_scale, bool k22_ordere
   if (!k22_ordered)   // Bm needs K22, not its inverse (VI: ordered through phase 1's ev_lo)
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22m, 0));
   HIPCHK(dense_spd_inverse_sum(c->K22, s_scale, S, c->Binv, mp, c->Xt, c->dinv, c->logdB,
-                               c->status + 1, c->stream));
+                               c->status + 1, c->gjs, c->stream));
   HIPCHK(launch_sum_small(c->logdB, mp / SGP_DB, c->sc + SC_LDB, c->stream));
   return SGP_OK;
 }
@@ -1439,6 +1463,7 @@ int sgp_vi_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
     HIPCHK(rb.wait());
   }
   c->phase = 0;
+  if (chain_watchdog(status)) return SGP_EHIP;
   if (status[0] || status[1]) {
     set_err("chol(): the leading minor of order %d of %s is not positive definite",
             status[0] ? status[0] : status[1],
@@ -1677,6 +1702,7 @@ int sgp_fitc_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
     HIPCHK(rb.wait());
   }
   c->phase = 0;
+  if (chain_watchdog(status)) return SGP_EHIP;
   if (status[0] || status[1]) {
     set_err("chol(): the leading minor of order %d of %s is not positive definite",
             status[0] ? status[0] : status[1],
@@ -1882,12 +1908,12 @@ static int lap_consume_obj(sgp_ctx* c, const double* red, int64_t o, bool first,
     Scope t(c, "lap_dense");
     if (first)   // (K22 + S_Z)^-1 is fixed for the whole NR run (Z depends on theta only)
       HIPCHK(dense_spd_inverse_sum(c->K22, 1.0, red, c->Bm, mp, c->Xt, c->dinv, c->logdB,
-                                   c->status + 1, c->stream));
+                                   c->status + 1, c->gjs, c->stream));
     if (!first)   // newtrap_sparseGP's u posterior uses the W of the last update's start
       HIPCHK(hipMemcpyAsync(c->Cprev, c->Binv, sizeof(double) * mm, hipMemcpyDeviceToDevice,
                             c->stream));
     HIPCHK(dense_spd_inverse_sum(c->K22, 1.0, red + o, c->Binv, mp, c->Xt, c->dinv, c->logdB,
-                                 c->status + 2, c->stream));
+                                 c->status + 2, c->gjs, c->stream));
     HIPCHK(launch_sum_small(c->logdB, mp / SGP_DB, c->sc + SC_LDB, c->stream));
     HIPCHK(dense_gemv(c->Bm, mp, red + o + mm, 1.0, lmv(c, LM_X1), c->stream));
     HIPCHK(launch_dot(red + o + mm, lmv(c, LM_X1), mp, c->slab_small, c->sc + SC_TU, c->stream));
@@ -1899,6 +1925,7 @@ static int lap_consume_obj(sgp_ctx* c, const double* red, int64_t o, bool first,
   HIPCHK(hipMemcpyAsync(sc, c->sc, sizeof(sc), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(status, c->status, sizeof(status), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  if (chain_watchdog(status)) return SGP_EHIP;
   if (status[0] || status[1] || status[2]) {
     c->lap_state = LS_NONE;
     set_err("chol(): the leading minor of order %d of %s is not positive definite",
@@ -2263,6 +2290,7 @@ int sgp_eval_full(sgp_ctx* c, int kernel, const double* theta, double delta, uns
     HIPCHK(rb.add(status, c->status, sizeof(status)));
     HIPCHK(rb.wait());
   }
+  if (chain_watchdog(status)) return SGP_EHIP;
   if (status[0]) {
     set_err("Sigma11 is not positive definite (leading minor of order %d)", status[0]);
     return SGP_ENOTPD;
@@ -2367,7 +2395,7 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
   hipStream_t s = sg.s;
   const int64_t mp = round_up(m, SGP_TILE), npp = round_up(np, SGP_TILE), mm = mp * mp;
   DevBuf dU, K22, Kinv, R, Pb, logd, V, T1, T22, wv, Xp, Kp, yv, rowq, q, S, Y;
-  IntBuf status;
+  IntBuf status, gsync;
   st = dalloc(&dU.p, mp * d);
   st = st ? st : dalloc(&K22.p, mm);
   st = st ? st : dalloc(&Kinv.p, mm);
@@ -2384,6 +2412,7 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
   st = st ? st : dalloc(&rowq.p, npp * (mp / SGP_TILE));
   st = st ? st : dalloc(&q.p, npp);
   st = st ? st : dalloc(&status.p, 4);
+  st = st ? st : dalloc(&gsync.p, SGP_GJ_SYNC_WORDS);
   if (!st && full_cov) {
     st = dalloc(&S.p, npp * npp);
     st = st ? st : dalloc(&Y.p, npp * mp);
@@ -2405,6 +2434,7 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
     HIPCHK(hipMemcpy(wv.p + mp, hd.data(), sizeof(double) * mp, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(V.p, hV.data(), sizeof(double) * mm, hipMemcpyHostToDevice));
     HIPCHK(hipMemset(status.p, 0, sizeof(int) * 4));
+    HIPCHK(hipMemset(gsync.p, 0, sizeof(int) * SGP_GJ_SYNC_WORDS));
   }
   // Sigma22: the gaussian family subtracts tau^2 I again (vi_functions.R:1246-1260,
   // laplace_approx_prediction.R:25-43) -> diagonal sigma^2 + delta; otherwise Kuu+(tau^2+delta)I
@@ -2412,7 +2442,8 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
   const double diag_sub = (gaussian && !full) ? kp.tau2 : 0.0;
   HIPCHK(launch_build_kmm(kp, dU.p, mp, m, mp, diag_sub, K22.p, s));
   HIPCHK(hipMemcpyAsync(Kinv.p, K22.p, sizeof(double) * mm, hipMemcpyDeviceToDevice, s));
-  HIPCHK(dense_spd_inverse(Kinv.p, mp, R.p, nullptr, Pb.p, logd.p, status.p, s));
+  HIPCHK(dense_spd_inverse(Kinv.p, mp, R.p, Pb.p, logd.p, status.p,
+                           reinterpret_cast<unsigned*>(gsync.p), s));
   HIPCHK(dense_gemv(Kinv.p, mp, wv.p + mp, 1.0, wv.p, s));          // Sigma22^-1 (u_mean - muu)
   HIPCHK(launch_gemm64(false, false, false, mp, mp, mp, 1.0, Kinv.p, mp, V.p, mp, 0.0, T1.p, mp,
                        s));
@@ -2543,6 +2574,7 @@ int sgp_vi_candidates(sgp_ctx* c, int kernel, const double* theta, const double*
   HIPCHK(hipMemcpyAsync(status, c->status, sizeof(status), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   c->phase = 0;
+  if (chain_watchdog(status)) return SGP_EHIP;
   if (status[0] || status[1]) {
     set_err("chol(): the leading minor of order %d of %s is not positive definite",
             status[0] ? status[0] : status[1],

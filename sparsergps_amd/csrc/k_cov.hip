@@ -220,15 +220,25 @@ __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* 
 // knots as one 16-byte store (lanes 0-15: 256 contiguous bytes of one row).  Persistent over
 // row blocks rb0 + blockIdx.y + k gridDim.y; with t, the workgroup's t = K^T r partial over all
 // its row blocks goes to slot slot0 + blockIdx.y of tslab (fixed order: deterministic).
+// t's running sums live in LDS, not registers: lane (w, lq, l') owns the two doubles of its
+// columns in tacc_s[w][lq], a private read-modify-write per tile pair and row block (no other
+// lane touches them, so no atomics), and r reaches the lanes as one value per lane (row ia)
+// broadcast by shuffles.  In registers (8 sums, 4 + 4 r values) the with-t builder needed 162
+// VGPRs, i.e. 3 workgroups per CU against the t-free builder's 4 (VI's build 1.67 ms against
+// FITC's 1.50 ms for the same K12); the sums and their reduction order are unchanged, so t is
+// bit-identical to the register form.
 template <bool WITH_T, int NC>
-__global__ void __launch_bounds__(256, NC > 4 ? (WITH_T ? 2 : 3) : (WITH_T ? 3 : 4))
+__global__ void __launch_bounds__(256, NC > 4 ? (WITH_T ? 2 : 3) : 4)
 k_build_knm_mfma(KernParams kp, const double* __restrict__ X, int64_t ldx, int64_t n,
                  const double* __restrict__ U, int64_t ldu, int64_t m, int64_t mp,
                  double* __restrict__ K, const double* __restrict__ rvec,
                  double* __restrict__ tslab, int64_t slot0, int64_t rb0, int64_t rb1) {
-  __shared__ double tsh[WITH_T ? 4 : 1][128];
+  typedef double nt2 __attribute__((ext_vector_type(2)));
+  __shared__ nt2 tacc_s[WITH_T ? 16 : 1][64];   // [wave][lq][tile pair p][lane & 15]
   __shared__ double etab[32];
   if (threadIdx.x < 32) etab[threadIdx.x] = kp.et[threadIdx.x];
+  if (WITH_T)
+    for (int e = threadIdx.x; e < 16 * 64; e += 256) tacc_s[e >> 6][e & 63] = nt2{0.0, 0.0};
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ln = lane & 15, lq = lane >> 4;
@@ -242,10 +252,11 @@ k_build_knm_mfma(KernParams kp, const double* __restrict__ X, int64_t ldx, int64
     rl[k] = fc[k] ? kp.rl[4 * k + lq] : 0.0;
   }
   const int64_t j0 = (int64_t)blockIdx.x * 128;
-  // knot fragments: in registers for d <= 8; for wider d (4 NC + 4 per lane and tile) they
-  // would not fit beside the row state, so they sit in LDS as [chunk][tile][lane] (each read
-  // one conflict-free ds_read_b64), written by wave w for tiles 2w, 2w + 1
-  constexpr bool BL = NC > 2;
+  // knot fragments: in registers for d <= 8 without t; for wider d (4 NC + 4 per lane and
+  // tile), or beside t's row values, they would not fit within 128 VGPRs (4 workgroups per
+  // CU), so they sit in LDS as [chunk][tile][lane] (each read one conflict-free ds_read_b64),
+  // written by wave w for tiles 2w, 2w + 1
+  constexpr bool BL = NC > 2 || WITH_T;
   __shared__ double sbf[BL ? (NC + 1) * 8 * 64 : 1];
   double bc[BL ? 1 : NC][8], b2[BL ? 1 : 8];
 #pragma unroll
@@ -275,22 +286,16 @@ k_build_knm_mfma(KernParams kp, const double* __restrict__ X, int64_t ldx, int64
     else return k < NC ? bc[k][tt] : b2[tt];
   };
   const double ehi = kp.lsig2;
-  double tacc[8];
-#pragma unroll
-  for (int tt = 0; tt < 8; ++tt) tacc[tt] = 0.0;
-  typedef double nt2 __attribute__((ext_vector_type(2)));
+  nt2* const tl = &tacc_s[4 * w + lq][0];       // this lane's t sums: tl[16 p + ln]
   // The next row block's coordinates and r are loaded before this block's stores: vmcnt
   // counts loads and stores in issue order, so loads issued after the stores would make every
   // block wait for the previous block's 16 stores to drain.
-  double xn[NC], rn[4] = {0.0, 0.0, 0.0, 0.0};
+  double xn[NC], rn = 0.0;
   auto load_rows = [&](int64_t rb) {
-    const int64_t ib = rb * 64 + 16 * w, ia = ib + ln;   // X is zero-padded to n_pad rows
+    const int64_t ia = rb * 64 + 16 * w + ln;   // X (and r) are zero-padded to n_pad rows
 #pragma unroll
     for (int k = 0; k < NC; ++k) xn[k] = fc[k] ? X[ia + (4 * k + lq) * ldx] : 0.0;
-    if (WITH_T) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) rn[r] = rvec[ib + lq + 4 * r];
-    }
+    if (WITH_T) rn = rvec[ia];
   };
 #pragma unroll
   for (int k = 0; k < NC; ++k) xn[k] = 0.0;
@@ -304,10 +309,11 @@ k_build_knm_mfma(KernParams kp, const double* __restrict__ X, int64_t ldx, int64
       ac[k] = fc[k] ? (xn[k] - ct[k]) * rl[k] : 0.0;
       x2 = fma(ac[k], ac[k], x2);
     }
-    double rr[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) rr[r] = rn[r];
+    const double rcur = rn;
     if (rb + gridDim.y < rb1) load_rows(rb + gridDim.y);
+    double rr[4];   // r of this lane's output rows lq + 4 r (held by lanes lq + 4 r)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rr[r] = WITH_T ? __shfl(rcur, lq + 4 * r, 64) : 0.0;
     x2 += __shfl_xor(x2, 16, 64);
     x2 += __shfl_xor(x2, 32, 64);
     // exponent = x~.u~ - |x~|^2 / 2 - |u~|^2 / 2 + log(sig2); padding rows as padding knots
@@ -324,6 +330,7 @@ k_build_knm_mfma(KernParams kp, const double* __restrict__ X, int64_t ldx, int64
       }
       e0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, bfr(NC, 2 * p), e0, 0, 0, 0);
       e1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, bfr(NC, 2 * p + 1), e1, 0, 0, 0);
+      nt2 ta = WITH_T ? tl[16 * p + ln] : nt2{0.0, 0.0};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         // K = exp(exponent) <= sig2: clamp the rounding above log(sig2), and below at -746
@@ -334,10 +341,11 @@ k_build_knm_mfma(KernParams kp, const double* __restrict__ X, int64_t ldx, int64
         __builtin_nontemporal_store(nt2{v0, v1},
                                     reinterpret_cast<nt2*>(&K[i * mp + j0 + 32 * p + 2 * ln]));
         if (WITH_T) {
-          tacc[2 * p] = fma(v0, rr[r], tacc[2 * p]);
-          tacc[2 * p + 1] = fma(v1, rr[r], tacc[2 * p + 1]);
+          ta.x = fma(v0, rr[r], ta.x);
+          ta.y = fma(v1, rr[r], ta.y);
         }
       }
+      if (WITH_T) tl[16 * p + ln] = ta;
       // keep each tile pair's four stores where they are: left to itself the scheduler sinks
       // all 16 to the end of the block, so a wave alternates a store burst with a long
       // store-free VALU stretch
@@ -345,18 +353,17 @@ k_build_knm_mfma(KernParams kp, const double* __restrict__ X, int64_t ldx, int64
     }
   }
   if (WITH_T) {
-#pragma unroll
-    for (int tt = 0; tt < 8; ++tt) {
-      double v = tacc[tt];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      if (lq == 0) tsh[w][32 * (tt >> 1) + 2 * ln + (tt & 1)] = v;
-    }
+    // column cc = 32 p + 2 l' + h: per wave (lq 0 + lq 1) + (lq 2 + lq 3), then the waves in order
     __syncthreads();
     if (threadIdx.x < 128) {
-      const int cc = threadIdx.x;
-      tslab[(slot0 + blockIdx.y) * mp + j0 + cc] =
-          ((tsh[0][cc] + tsh[1][cc]) + tsh[2][cc]) + tsh[3][cc];
+      const int cc = threadIdx.x, sl = 16 * (cc >> 5) + ((cc >> 1) & 15), h = cc & 1;
+      double v[4];
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) {
+        const double* q0 = reinterpret_cast<const double*>(&tacc_s[4 * ww][sl]) + h;
+        v[ww] = (q0[0] + q0[128]) + (q0[256] + q0[384]);
+      }
+      tslab[(slot0 + blockIdx.y) * mp + j0 + cc] = ((v[0] + v[1]) + v[2]) + v[3];
     }
   }
 }

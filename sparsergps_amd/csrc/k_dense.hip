@@ -97,6 +97,7 @@ __device__ __forceinline__ double row_bcast_f64(double v, int k) {
   }
 }
 
+template <bool SC1 = false>   // SC1: P stored write-through (k_gj_persist's hand-off)
 __device__ __forceinline__ void gj_pivot_body(const double* B, int64_t ldb, int64_t gofs,
                                               double* __restrict__ P,
                                               double* __restrict__ logd_slot,
@@ -207,7 +208,11 @@ __device__ __forceinline__ void gj_pivot_body(const double* B, int64_t ldb, int6
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) P[(16 * wv + lr + 4 * q) * 64 + 16 * ct + lc] = -acc[ct][q];
+    for (int q = 0; q < 4; ++q) {
+      double* d = &P[(16 * wv + lr + 4 * q) * 64 + 16 * ct + lc];
+      if constexpr (SC1) __hip_atomic_store(d, -acc[ct][q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else *d = -acc[ct][q];
+    }
   __syncthreads();
   double lg = (tid < 64) ? log(piv[tid]) : 0.0;
 #pragma unroll
@@ -419,6 +424,272 @@ __global__ void __launch_bounds__(256) k_gj_step(const double* __restrict__ Ao,
 #undef GJ_STAMP
 }
 
+// ---------------------------------------------------------------- persistent Gauss-Jordan
+// The whole chain of an SPD inverse in one launch (nb <= GJ_NB_MAX): G workgroups claim tasks
+// from a ticket counter in dependency order and run them in place on the matrix, so a step's
+// tiles start as soon as their own inputs exist instead of at a launch boundary, and the next
+// pivot's workgroup (task 1 of each step) is never queued behind the step's other tiles.
+// Tasks, in ticket order:  0: pivot P_0 of tile (0, 0);  then per step k (nb^2 tasks):
+//   interior (i, j), i, j != k:  A_ij <- A_ij - (A_ik P_k) A_kj; the first one is (k+1, k+1),
+//                                which then factors its fresh tile into P_{k+1} (look-ahead);
+//                                in shell order max(a, b), a = i - k - 1, b = j - k - 1 (mod nb),
+//                                so the tiles step k+1's look-ahead needs come first
+//   column (i, k):  A_ik <- -A_ik P_k       row (k, j):  A_kj <- P_k A_kj       (k, k): P_k
+// A task waits only for tasks with smaller tickets, and a ticket is only claimed by a running
+// workgroup, so the smallest unfinished ticket can always proceed: no co-residency is assumed
+// (the K22 chain on `aux` may hold CUs at the same time).  Flags (device-scope release /
+// acquire): ver[i][j] = steps applied to tile (i, j); loaded[i][j] = k + 1 once interior task
+// (k, i, j) holds A_ik and A_kj (the in-place column / row tasks overwrite them only then);
+// piv[k] = P_k is in memory.  The last workgroup to leave zeroes the sync words for the next
+// launch (allocated zeroed).  Arithmetic per tile is k_gj_step's: results are bit-identical.
+constexpr int GJ_NB_MAX = 64;
+constexpr int GJ_SYNC_PIV = 64, GJ_SYNC_VER = GJ_SYNC_PIV + GJ_NB_MAX;
+
+// Hand-offs between workgroups (MI355X_MICROARCH.md, inter-workgroup visibility, first row of
+// the sc1 table): every byte handed over is stored write-through (sc1) and loaded sc1 (L1
+// bypassed), each storing wave drains its stores (s_waitcnt vmcnt(0)) before the workgroup
+// barrier behind which one lane stores the flag (sc1); a consumer polls with sc1 loads in one
+// wave and the others load after the barrier it then joins.  No cache-wide fences: an acquire
+// fence per task, or polling with acquire loads, made a step at m = 1024 five times slower.
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned ldu_sc1(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stu_sc1(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Threads tid < cnt (wave 0) wait for their flag (ptr(tid)) to reach v, then the workgroup
+// proceeds.  Watchdog: a wait that outlasts ~2^24 polls (seconds; a real wait is microseconds)
+// marks the chain aborted (sync[2], status -1, reported by the host as an internal error) and
+// every later wait returns at once, so the grid always drains.
+constexpr unsigned GJ_SPIN_MAX = 1u << 24;
+template <typename F>
+__device__ __forceinline__ void gj_wait(int cnt, F ptr, unsigned v, unsigned* sync, int* status) {
+  if ((int)threadIdx.x < cnt) {
+    const unsigned* f = ptr((int)threadIdx.x);
+    unsigned it = 0;
+    while (ldu_sc1(f) < v) {
+      if ((++it & 255u) == 0) {
+        if (it >= GJ_SPIN_MAX) {
+          stu_sc1(sync + 2, 1u);
+          atomicCAS(status, 0, -1);
+          break;
+        }
+        if (ldu_sc1(sync + 2)) break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+}
+// the workgroup's (sc1) stores drained, then flag = v
+__device__ __forceinline__ void gj_publish(unsigned* f, unsigned v) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) stu_sc1(f, v);
+}
+__device__ __forceinline__ void gj_ld_sc1(double (&v)[16], const double* G, int64_t ldg) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = threadIdx.x + 256 * q;
+    v[q] = ld_sc1(&G[(int64_t)(e >> 6) * ldg + (e & 63)]);
+  }
+}
+
+template <bool SC1>
+__device__ __forceinline__ void gj_store_acc(double* T, int64_t ld, const d4 (&acc)[2][2],
+                                             double sgn) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
+#pragma unroll
+  for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
+        const int c = wc * 32 + fn * 16 + (lane & 15);
+        if constexpr (SC1) st_sc1(&T[r * ld + c], sgn * acc[fm][fn][q]);
+        else T[r * ld + c] = sgn * acc[fm][fn][q];
+      }
+}
+
+__global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const double* src0b,
+                                                    double beta, double* buf, int64_t lda,
+                                                    int nb, double* __restrict__ P,
+                                                    double* __restrict__ logd,
+                                                    int* __restrict__ status,
+                                                    unsigned* __restrict__ sync) {
+  __shared__ double lds[3 * 64 * GJ_LS];
+  __shared__ int tk;
+  double* S0 = lds;
+  double* S1 = lds + 64 * GJ_LS;
+  double* S2 = lds + 2 * 64 * GJ_LS;
+  unsigned* piv = sync + GJ_SYNC_PIV;
+  unsigned* ver = sync + GJ_SYNC_VER;
+  unsigned* loaded = ver + nb * nb;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int nn = nb * nb, n1 = nb - 1;
+  const int ntask = 1 + nb * nn;
+  auto tile = [&](const double* A, int i, int j) { return A + (int64_t)i * 64 * lda + (int64_t)j * 64; };
+  auto wtile = [&](int i, int j) { return buf + (int64_t)i * 64 * lda + (int64_t)j * 64; };
+  // step k's operand (i, j): step 0 reads src0 (+ beta src0b), later steps the matrix itself
+  // every load of the matrix and P is sc1 (src0 too: in place it is the matrix)
+  auto ld_tile = [&](double (&v)[16], int k, int i, int j) {
+    gj_ld_sc1(v, tile(k == 0 ? src0 : buf, i, j), lda);
+    if (k == 0 && src0b) {
+      const double* B = tile(src0b, i, j);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int e = threadIdx.x + 256 * q;
+        v[q] = fma(beta, B[(int64_t)(e >> 6) * lda + (e & 63)], v[q]);
+      }
+    }
+  };
+  auto ld_pk = [&](int k) {   // P_k -> S1
+    gj_wait(1, [&](int) { return piv + k; }, 1u, sync, status);
+    double v[16];
+    gj_ld_sc1(v, P + (int64_t)k * 4096, 64);
+    gj_st(S1, v);
+  };
+  for (;;) {
+    if (threadIdx.x == 0) tk = (int)__hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int t = tk;
+    __syncthreads();
+    if (t >= ntask) break;
+    if (t == 0) {   // P_0
+      double v[16];
+      ld_tile(v, 0, 0, 0);
+      gj_st(S0, v);
+      __syncthreads();
+      gj_pivot_body<true>(S0, GJ_LS, 0, P, logd, status, S1);
+      gj_publish(piv, 1u);
+      continue;
+    }
+    const int s = t - 1, k = s / nn;
+    int r = s - k * nn;
+    d4 acc[2][2];
+    if (r < n1 * n1) {
+      // interior tile in shell order
+      int sh = (int)sqrtf((float)r);
+      while (sh * sh > r) --sh;
+      while ((sh + 1) * (sh + 1) <= r) ++sh;
+      const int o = r - sh * sh;
+      const int a = o < sh ? o : sh, b = o < sh ? sh : (o < 2 * sh ? o - sh : sh);
+      const int i = (k + 1 + a) % nb, j = (k + 1 + b) % nb;
+      if (k > 0) {
+        const int fi[3] = {i * nb + j, i * nb + k, k * nb + j};
+        gj_wait(3, [&](int q) { return ver + fi[q]; }, (unsigned)k, sync, status);
+      }
+      double v0[16], v2[16], aij[2][2][4];
+      ld_tile(v0, k, i, k);
+      ld_tile(v2, k, k, j);
+      {
+        const double* Aij = tile(k == 0 ? src0 : buf, i, j);
+        const double* Bij = (k == 0 && src0b) ? tile(src0b, i, j) : nullptr;
+#pragma unroll
+        for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int rr = wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
+              const int c = wc * 32 + fn * 16 + (lane & 15);
+              aij[fm][fn][q] = ld_sc1(&Aij[rr * lda + c]);
+              if (Bij) aij[fm][fn][q] = fma(beta, Bij[rr * lda + c], aij[fm][fn][q]);
+            }
+      }
+      gj_st(S0, v0);
+      gj_st(S2, v2);
+      __syncthreads();   // A_ik and A_kj are in LDS: the column / row tasks may overwrite them
+      if (threadIdx.x == 0) stu_sc1(loaded + i * nb + j, (unsigned)(k + 1));
+      ld_pk(k);
+      __syncthreads();
+      gj_mm64(S0, S1, acc);                      // A_ik P_k
+      __syncthreads();
+      gj_store_acc<false>(S0, GJ_LS, acc, 1.0);
+      __syncthreads();
+      gj_mm64(S0, S2, acc);                      // (A_ik P_k) A_kj
+      const bool look_ahead = (i == k + 1) && (j == k + 1);
+      if (look_ahead) __syncthreads();           // S0 takes the fresh tile
+      double* Tij = wtile(i, j);
+#pragma unroll
+      for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int rr = wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
+            const int c = wc * 32 + fn * 16 + (lane & 15);
+            const double v = aij[fm][fn][q] - acc[fm][fn][q];
+            st_sc1(&Tij[rr * lda + c], v);
+            if (look_ahead) S0[rr * GJ_LS + c] = v;
+          }
+      gj_publish(ver + i * nb + j, (unsigned)(k + 1));
+      if (look_ahead) {
+        __syncthreads();
+        gj_pivot_body<true>(S0, GJ_LS, (int64_t)(k + 1) * 64, P + (int64_t)(k + 1) * 4096,
+                      logd + k + 1, status, S1);
+        gj_publish(piv + k + 1, 1u);
+      }
+      continue;
+    }
+    r -= n1 * n1;
+    if (r < 2 * n1) {
+      // column task (i, k): -A_ik P_k, or row task (k, j): P_k A_kj
+      const bool col = r < n1;
+      const int x = (k + 1 + (col ? r : r - n1)) % nb;
+      const int i = col ? x : k, j = col ? k : x;
+      if (k > 0) gj_wait(1, [&](int) { return ver + i * nb + j; }, (unsigned)k, sync, status);
+      double v[16];
+      ld_tile(v, k, i, j);
+      gj_st(col ? S0 : S2, v);
+      ld_pk(k);
+      __syncthreads();
+      if (col) gj_mm64(S0, S1, acc);
+      else gj_mm64(S1, S2, acc);
+      // every interior task of row i (column j) of this step holds its copy of this tile
+      if (col)
+        gj_wait(nb, [&](int q) { return loaded + i * nb + (q == k ? (k + 1) % nb : q); },
+                (unsigned)(k + 1), sync, status);
+      else
+        gj_wait(nb, [&](int q) { return loaded + (q == k ? (k + 1) % nb : q) * nb + j; },
+                (unsigned)(k + 1), sync, status);
+      gj_store_acc<true>(wtile(i, j), lda, acc, col ? -1.0 : 1.0);
+      gj_publish(ver + i * nb + j, (unsigned)(k + 1));
+      continue;
+    }
+    // (k, k) <- P_k
+    gj_wait(1, [&](int) { return piv + k; }, 1u, sync, status);
+    {
+      double* Tkk = wtile(k, k);
+      const double* Pk = P + (int64_t)k * 4096;
+      double v[16];
+      gj_ld_sc1(v, Pk, 64);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int e = threadIdx.x + 256 * q;
+        st_sc1(&Tkk[(int64_t)(e >> 6) * lda + (e & 63)], v[q]);
+      }
+    }
+    gj_publish(ver + k * nb + k, (unsigned)(k + 1));
+  }
+  // the last workgroup out resets the sync words (no other workgroup touches them any more)
+  if (threadIdx.x == 0) tk = (int)__hip_atomic_fetch_add(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (tk == (int)gridDim.x - 1) {
+    for (int e = threadIdx.x; e < 2 * nn; e += 256) ver[e] = 0u;
+    for (int e = threadIdx.x; e < nb; e += 256) piv[e] = 0u;
+    if (threadIdx.x < 3) sync[threadIdx.x] = 0u;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_axpby(double a, const double* __restrict__ A, double b,
                                                const double* __restrict__ B,
                                                double* __restrict__ C, int64_t count) {
@@ -628,11 +899,29 @@ static size_t gj_step_pad() {
   return (size_t)pad;
 }
 
-hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* Cb, double* P,
-                             double* logd, int* status, hipStream_t s) {
-  // R: mp x mp ping-pong buffer; P: nb 64x64 pivot inverses (mp * 64 doubles); Cb unused.
-  (void)Cb;
+// Workgroups of one persistent chain: at m = 1024 a step's 255 other tiles (~4 us each) must
+// finish within the look-ahead task's ~14 us; two chains (K22's, Bm's) may run together.
+static int gj_workgroups(int nb) {
+  const int cap = SGP_GJ_GMAX;
+  return nb * nb < cap ? nb * nb : cap;
+}
+
+static hipError_t gj_persist(const double* src0, const double* src0b, double beta, double* buf,
+                             int64_t mp, double* P, double* logd, int* status, unsigned* sync,
+                             hipStream_t s) {
   const int nb = (int)(mp / SGP_DB);
+  hipLaunchKernelGGL(k_gj_persist, dim3(gj_workgroups(nb)), dim3(256), 0, s, src0, src0b, beta,
+                     buf, mp, nb, P, logd, status, sync);
+  return hipGetLastError();
+}
+
+hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* P, double* logd,
+                             int* status, unsigned* sync, hipStream_t s) {
+  // in place; R: mp x mp ping-pong buffer of the launch-per-step chain (nb > GJ_NB_MAX);
+  // P: nb 64x64 pivot inverses (mp * 64 doubles)
+  const int nb = (int)(mp / SGP_DB);
+  if (nb <= GJ_NB_MAX && !SGP_GJ_STEPS)
+    return gj_persist(A, nullptr, 0.0, A, mp, P, logd, status, sync, s);
   hipLaunchKernelGGL(k_gj_pivot, dim3(1), dim3(256), 0, s, A, mp, 0, P, logd, status,
                      (const double*)nullptr, 0.0);
   double* src = A;
@@ -653,11 +942,13 @@ hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* Cb, doubl
 
 hipError_t dense_spd_inverse_sum(const double* A0, double beta, const double* B0, double* out,
                                  int64_t mp, double* R, double* P, double* logd, int* status,
-                                 hipStream_t s) {
-  // out = inv(A0 + beta B0): step 0 forms the matrix as it reads it (no axpby launch, ~6 us of
-  // the C2 critical path); step k writes buf[(nb - 1 - k) % 2] (buf = {out, R}), so the last
+                                 unsigned* sync, hipStream_t s) {
+  // out = inv(A0 + beta B0), the sum formed as step 0 reads it (no axpby launch).  Launch per
+  // step (nb > GJ_NB_MAX): step k writes buf[(nb - 1 - k) % 2] (buf = {out, R}), so the last
   // step always lands in out and no copy follows
   const int nb = (int)(mp / SGP_DB);
+  if (nb <= GJ_NB_MAX && !SGP_GJ_STEPS)
+    return gj_persist(A0, B0, beta, out, mp, P, logd, status, sync, s);
   double* buf[2] = {out, R};
   hipLaunchKernelGGL(k_gj_pivot, dim3(1), dim3(256), 0, s, A0, mp, 0, P, logd, status, B0, beta);
   for (int k = 0; k < nb; ++k) {

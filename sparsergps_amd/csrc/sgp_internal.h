@@ -7,6 +7,7 @@
 #define SGP_MAXD 32          // largest input dimension d supported by the fused kernels
 #define SGP_TILE 128         // n x m tile edge of the MFMA kernels (rows and knots padded to it)
 #define SGP_DB 64            // block edge of the m x m dense routines
+#define SGP_GJ_SYNC_WORDS (128 + 2 * 64 * 64)   // k_dense.hip: ticket, exits, flags (nb <= 64)
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
@@ -231,13 +232,17 @@ hipError_t launch_gemm64(bool transA, bool transB, bool lower_only, int64_t M, i
 // In-place inverse of an SPD matrix A (mp x mp, full storage) by blocked Gauss-Jordan with
 // 64-wide pivots; logd[k] = sum log L_ii of the k-th pivot block's Cholesky factor, so
 // log det A = 2 * sum_k logd[k].  Work: R (64 x mp), Cb (mp x 64), P (64 x 64).
-hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* Cb, double* P,
-                             double* logd, int* status, hipStream_t s);
-// out = inv(A0 + beta B0), the sum formed by the chain's first pivot and step as they read it
-// (out, R distinct from A0 and B0)
+// In-place SPD inverse (blocked Gauss-Jordan) of the mp x mp matrix A.  P: mp x 64 pivot
+// inverses; logd: mp / 64 block log-determinant halves; sync: SGP_GJ_SYNC_WORDS words, zero
+// when the chain is launched (and zero again when it has finished), one area per chain that may
+// run at the same time; R: mp x mp scratch (only for mp > 64 * 64)
+hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* P, double* logd,
+                             int* status, unsigned* sync, hipStream_t s);
+// out = inv(A0 + beta B0), the sum formed by the chain as it reads it (out, R distinct from A0
+// and B0)
 hipError_t dense_spd_inverse_sum(const double* A0, double beta, const double* B0, double* out,
                                  int64_t mp, double* R, double* P, double* logd, int* status,
-                                 hipStream_t s);
+                                 unsigned* sync, hipStream_t s);
 // C = a*A + b*B elementwise over mp x mp
 hipError_t dense_axpby(double a, const double* A, double b, const double* B, double* C,
                        int64_t count, hipStream_t s);

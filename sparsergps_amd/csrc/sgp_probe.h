@@ -28,6 +28,9 @@
 //                       SIMD), 1 (half the rows, 4 waves), 2 (twice the rows, 2 waves)
 //   SGP_GJ_MM_UNROLL    unroll of gj_mm64's 16 k-substeps (16; 4 before round 4)
 //   SGP_S256_IL         1: k_syrk_s256's step with an interleave request
+//   SGP_VI_BUILD_NO_T   1: VI's builder without t (wrong results: builder timing only)
+//   SGP_GJ_STEPS        1: the m x m inverses as one launch per pivot step (before round 5)
+//   SGP_GJ_GMAX         workgroups of a persistent Gauss-Jordan chain (at most)
 #pragma once
 
 #if (defined(SGP_CON_TRACE) || defined(SGP_CON_NO_EPILOGUE) || defined(SGP_GJ_TRACE) ||       \
@@ -36,7 +39,8 @@
      defined(SGP_SYRK_BAL) || defined(SGP_SDT_IL) || defined(SGP_S256_IL) ||                  \
      defined(SGP_SDT_W) || defined(SGP_SDT_WW) || defined(SGP_SDT_WT) ||                      \
      defined(SGP_SYRK_W3) || defined(SGP_CON_ROWQ_KU) ||                                      \
-     defined(SGP_LAP_RS_CFG) || defined(SGP_GJ_MM_UNROLL)) &&                                 \
+     defined(SGP_LAP_RS_CFG) || defined(SGP_GJ_MM_UNROLL) || defined(SGP_VI_BUILD_NO_T) ||        \
+     defined(SGP_GJ_STEPS) || defined(SGP_GJ_GMAX)) &&                                 \
     !defined(SGP_PROBE_BUILD)
 #error "timing probes and experiment knobs are for variant builds only (SGP_PROBE_BUILD)"
 #endif
@@ -85,6 +89,15 @@
 #endif
 #ifndef SGP_S256_IL
 #define SGP_S256_IL 0
+#endif
+#ifndef SGP_GJ_STEPS
+#define SGP_GJ_STEPS 0
+#endif
+#ifndef SGP_GJ_GMAX
+#define SGP_GJ_GMAX 128
+#endif
+#ifndef SGP_VI_BUILD_NO_T
+#define SGP_VI_BUILD_NO_T 0
 #endif
 
 // k_contract: stamp k from thread 0 of the workgroup
