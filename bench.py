@@ -297,6 +297,16 @@ def main():
                 nr_iters.append(it)
                 return o, g
         runner = _Runner()
+    elif not distributed and not args.knots:
+        # one process, one GPU: the evaluation through the one-call entry the R path uses
+        # (sgp_eval_vi / sgp_eval_fitc: the same phases and kernels, one ctypes call instead of
+        # three plus the Python driver between them)
+        fused = ctx.eval_vi if args.mode == "vi" else ctx.eval_fitc
+
+        class _FusedRunner:
+            def eval(self, theta, U, delta):
+                return fused(theta, cov_fun, U, delta)
+        runner = _FusedRunner()
     else:
         vi = RowShardedVI(backend, n, None, force_collectives=distributed)
         if args.knots:
