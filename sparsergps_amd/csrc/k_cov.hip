@@ -10,6 +10,7 @@
 #include <stdlib.h>
 
 #include "sgp_internal.h"
+#include "sgp_probe.h"
 
 namespace {
 
@@ -671,7 +672,7 @@ static hipError_t build_knm_impl(const KernParams& kp, const double* X, int64_t 
 // step beside the builder (+ build and first pivot) at ~2.8 GB/ms for the shared-occupancy
 // builder (measured, m = 1024).
 static int64_t chain_shared_rb(int64_t mp) {
-  const double chain_us = 60.0 * (double)(mp / 64) + 250.0;
+  const double chain_us = SGP_CHAIN_US_STEP * (double)(mp / 64) + SGP_CHAIN_US_FIX;
   return (int64_t)(chain_us * 2.8e6 / (64.0 * (double)mp * 8.0)) + 1;   // 2.8 GB/ms = 2.8e6 B/us
 }
 

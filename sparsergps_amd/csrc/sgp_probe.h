@@ -31,6 +31,8 @@
 //   SGP_VI_BUILD_NO_T   1: VI's builder without t (wrong results: builder timing only)
 //   SGP_GJ_STEPS        1: the m x m inverses as one launch per pivot step (before round 5)
 //   SGP_GJ_GMAX         workgroups of a persistent Gauss-Jordan chain (at most)
+//   SGP_CHAIN_US_STEP   chain_shared_rb's model of a K22 chain beside the builder: us per
+//   SGP_CHAIN_US_FIX    64-wide step, and fixed us
 #pragma once
 
 #if (defined(SGP_CON_TRACE) || defined(SGP_CON_NO_EPILOGUE) || defined(SGP_GJ_TRACE) ||       \
@@ -40,7 +42,8 @@
      defined(SGP_SDT_W) || defined(SGP_SDT_WW) || defined(SGP_SDT_WT) ||                      \
      defined(SGP_SYRK_W3) || defined(SGP_CON_ROWQ_KU) ||                                      \
      defined(SGP_LAP_RS_CFG) || defined(SGP_GJ_MM_UNROLL) || defined(SGP_VI_BUILD_NO_T) ||        \
-     defined(SGP_GJ_STEPS) || defined(SGP_GJ_GMAX)) &&                                 \
+     defined(SGP_GJ_STEPS) || defined(SGP_GJ_GMAX) || defined(SGP_CHAIN_US_STEP) ||         \
+     defined(SGP_CHAIN_US_FIX)) &&                                 \
     !defined(SGP_PROBE_BUILD)
 #error "timing probes and experiment knobs are for variant builds only (SGP_PROBE_BUILD)"
 #endif
@@ -95,6 +98,12 @@
 #endif
 #ifndef SGP_GJ_GMAX
 #define SGP_GJ_GMAX 128
+#endif
+#ifndef SGP_CHAIN_US_STEP
+#define SGP_CHAIN_US_STEP 60.0
+#endif
+#ifndef SGP_CHAIN_US_FIX
+#define SGP_CHAIN_US_FIX 250.0
 #endif
 #ifndef SGP_VI_BUILD_NO_T
 #define SGP_VI_BUILD_NO_T 0
