@@ -1764,7 +1764,11 @@ int64_t syrk_slab_doubles_mp(int64_t n_pad, int64_t mp) {
   const int64_t nblk = (int64_t)(2 * q.nb) * (2 * q.nb + 1) / 2;
   int64_t need = (int64_t)q.splits * nblk * 4096 + (int64_t)q.splits * q.nb * T128 + q.splits +
                  n_pad;   // + the sqrt(w) rows of WMODE 2
-  // every balanced plan launch_syrk_aug may pick (its split counts depend on the weights / t)
+  // every balanced plan launch_syrk_aug may pick (its split counts depend on the weights / t).
+  // Its diagonal-tile splits are laid out like the others, over all nblk lower 64-blocks,
+  // although syrk_dtile writes only the 3 nb inside the diagonal 128-tiles: ~3.5 MB per diagonal
+  // split at m = 1024, of the order of 100 MB per context at C3 -- kept for the uniform block
+  // index of the reductions (288 GB of HBM per GPU; a compact layout would save it)
   for (int v = 0; v < 3; ++v) {   // unweighted / sqrt(w); signed weights; weights and t
     const SyrkBal bal = syrk_plan_bal(n_pad, mp, syrk_dtile_cost(v > 0, v > 1), v > 0);
     if (bal.on)

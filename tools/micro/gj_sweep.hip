@@ -6,6 +6,7 @@
 //   col: every 16-lane row holds the whole block, lane c column c (16 registers); a sweep is one
 //        v_fmac_f64_dpp per element (src0 = lane k's register by row_newbcast), the pivot lane's
 //        column kept unscaled with a pending factor (applied once after the 16 sweeps).
+//   pipe: cur pipelined one sweep ahead (the product since round 5);
 //   build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form -o gj_sweep gj_sweep.hip
 #include <cmath>
 #include <cstdio>
@@ -37,6 +38,42 @@ __device__ __forceinline__ void sweep_cur(d4& t, double (&dk)[16]) {
       const double vi = (i == k) ? -r : vr[q] * r;
       const double base = (i == k || lc == k) ? 0.0 : t[q];
       t[q] = fma(-vi, vj, base);
+    }
+  }
+}
+
+// round 5, second form (k_dense.hip today): pipelined one sweep ahead -- the next pivot and
+// row k+1 from their pre-sweep values with sweep k's own arithmetic
+__device__ __forceinline__ void sweep_pipe(d4& t, double (&dk)[16]) {
+  const int lane = threadIdx.x & 63, lr = lane >> 4, lc = lane & 15;
+  double vc = __shfl(t[0], lc, 64);
+  double d = readlane_f64(t[0], 0);
+  double r = rcp_nr(d);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int kq = k >> 2, kr = k & 3;
+    const int k1 = k + 1 < 16 ? k + 1 : 15, k1q = k1 >> 2, k1r = k1 & 3;
+    dk[k] = d;
+    const double wnext = __shfl(t[k1q], lc + 16 * k1r, 64);
+    const double a = readlane_f64(t[k1q], k + 16 * k1r);
+    const double b = readlane_f64(t[kq], k1 + 16 * kr);
+    const double cdg = readlane_f64(t[k1q], k1 + 16 * k1r);
+    double vr[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) vr[q] = row_bcast_f64(t[q], k);
+    const double vj = (lc == k) ? -1.0 : vc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = lr + 4 * q;
+      const double vi = (i == k) ? -r : vr[q] * r;
+      const double base = (i == k || lc == k) ? 0.0 : t[q];
+      t[q] = fma(-vi, vj, base);
+    }
+    if (k + 1 < 16) {
+      const double ar = a * r;
+      d = fma(-ar, b, cdg);
+      vc = (lc == k) ? ar : fma(-ar, vc, wnext);
+      r = rcp_nr(d);
     }
   }
 }
@@ -89,6 +126,25 @@ __global__ void __launch_bounds__(64) k_cur(const double* B, double* out, double
   }
 }
 
+__global__ void __launch_bounds__(64) k_pipe(const double* B, double* out, double* piv, int reps) {
+  const int lane = threadIdx.x, lr = lane >> 4, lc = lane & 15;
+  double dk[16];
+  d4 t;
+  for (int r = 0; r < reps; ++r) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] = B[(lr + 4 * q) * 16 + lc];
+    sweep_pipe(t, dk);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[(lr + 4 * q) * 16 + lc] = t[q];
+  }
+  if (lane < 16) {
+    double v = dk[0];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) v = (lane == k) ? dk[k] : v;
+    piv[lane] = v;
+  }
+}
+
 __global__ void __launch_bounds__(64) k_col(const double* B, double* out, double* piv, int reps) {
   const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
   double dk[16], R[16];
@@ -127,13 +183,15 @@ int main() {
   hipMalloc(&dB, 16 * 16 * 8); hipMalloc(&dO, 16 * 16 * 8); hipMalloc(&dP, 16 * 8);
   hipMemcpy(dB, B.data(), 16 * 16 * 8, hipMemcpyHostToDevice);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
-  const char* names[2] = {"cur (accumulator layout)", "col (v_fmac_f64_dpp)"};
+  const char* names[3] = {"cur (accumulator layout)", "col (v_fmac_f64_dpp)", "pipe (one sweep ahead)"};
+  std::vector<double> O0(16 * 16), P0(16);
   for (int it = 0; it < 3; ++it)
-    for (int v = 0; v < 2; ++v) {
+    for (int v = 0; v < 3; ++v) {
       const int reps = 20000;
       hipEventRecord(e0, 0);
       if (v == 0) hipLaunchKernelGGL(k_cur, dim3(1), dim3(64), 0, 0, dB, dO, dP, reps);
-      else hipLaunchKernelGGL(k_col, dim3(1), dim3(64), 0, 0, dB, dO, dP, reps);
+      else if (v == 1) hipLaunchKernelGGL(k_col, dim3(1), dim3(64), 0, 0, dB, dO, dP, reps);
+      else hipLaunchKernelGGL(k_pipe, dim3(1), dim3(64), 0, 0, dB, dO, dP, reps);
       hipEventRecord(e1, 0); hipEventSynchronize(e1);
       float ms; hipEventElapsedTime(&ms, e0, e1);
       hipMemcpy(O.data(), dO, 16 * 16 * 8, hipMemcpyDeviceToHost);
@@ -147,8 +205,11 @@ int main() {
           err = fmax(err, fabs(s - (i == j ? 1.0 : 0.0)));
         }
       }
-      printf("%-26s %7.3f us per 16 sweeps (%6.1f ns/sweep)  |B inv - I| %.2e  sum log piv %.15f\n",
-             names[v], ms * 1e3 / reps, ms * 1e6 / reps / 16, err, ld);
+      if (v == 0) { O0 = O; P0 = pv; }
+      const bool same = v == 1 || (O == O0 && pv == P0);
+      printf("%-26s %7.3f us per 16 sweeps (%6.1f ns/sweep)  |B inv - I| %.2e  sum log piv %.15f%s\n",
+             names[v], ms * 1e3 / reps, ms * 1e6 / reps / 16, err, ld,
+             v == 2 ? (same ? "  bit-identical to cur" : "  DIFFERS from cur") : "");
     }
   return 0;
 }
