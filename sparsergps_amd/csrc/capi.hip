@@ -1372,12 +1372,17 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
     S = c->Sfull;
   }
   // K22's inverse (queued on aux at the end of phase 1) runs concurrently with Bm's on the
-  // main stream: two latency-bound chains of 256-workgroup steps fit one residency round
+  // main stream.  The Bm chain is enqueued before the side work below: the host's issue of
+  // the aux_lo launches first left the GPU idle ~20 us between phase 1's last kernel and the
+  // chain at C2 (kernel trace)
+  HIPCHK(hipEventRecord(c->ev_s, c->stream));   // S (red1, summed) is ready
+  // K22's build ordered by phase 1's ev_lo (or waited for here when phase 1 had no side work)
+  int st = bm_stage(c, S, 1.0 / z, c->vi_k22_ordered);
+  if (st) return st;
   {
     // tr(K22inv S) and M3 = K22inv S K22inv need S and K22inv only: on aux_lo beside the Bm
     // inversion (T22 and K22inv are final once the K22 chain on `aux` has finished).  Beside
     // the K12 contraction instead, the GEMMs' workgroups starved and slowed it more.
-    HIPCHK(hipEventRecord(c->ev_s, c->stream));
     HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_s, 0));
     HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_k22, 0));
     Scope ta(c, "m3_aux", c->aux_lo);
@@ -1391,9 +1396,6 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
       HIPCHK(hipEventRecord(c->ev_m3, c->aux_lo));
     }
   }
-  // K22's build ordered by phase 1's ev_lo (or waited for here when phase 1 had no side work)
-  int st = bm_stage(c, S, 1.0 / z, c->vi_k22_ordered);
-  if (st) return st;
   {
     Scope tm(c, "mm_vectors");
     if (flags & SGP_FLAG_OBJ_ONLY) {   // elbo_fun alone: no adjoint work

@@ -493,11 +493,31 @@ __device__ __forceinline__ void gj_publish(unsigned* f, unsigned v) {
   __syncthreads();
   if (threadIdx.x == 0) stu_sc1(f, v);
 }
-__device__ __forceinline__ void gj_ld_sc1(double (&v)[16], const double* G, int64_t ldg) {
+// A 64x64 tile (row stride ldg) by 16-byte sc1 buffer loads (the 8-byte form runs at ~0.6 of
+// the rate, MI355X_MICROARCH.md): thread t holds columns c = 2 (t & 31), c + 1 of rows
+// (t >> 5) + 8 q in v[2 q], v[2 q + 1]; gj_st16 stores that layout to an LDS tile
+typedef unsigned int gj_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gj_rsrc(const double* G) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(G), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+__device__ __forceinline__ int gj_off16(int q, int64_t ldg) {   // byte offset of thread's pair q
+  return (int)((((int64_t)(threadIdx.x >> 5) + 8 * q) * ldg + 2 * (threadIdx.x & 31)) * 8);
+}
+__device__ __forceinline__ void gj_ld16_sc1(double (&v)[16], const double* G, int64_t ldg) {
+  const __amdgpu_buffer_rsrc_t rs = gj_rsrc(G);
+  gj_u4 w[8];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int e = threadIdx.x + 256 * q;
-    v[q] = ld_sc1(&G[(int64_t)(e >> 6) * ldg + (e & 63)]);
+  for (int q = 0; q < 8; ++q) w[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, gj_off16(q, ldg), 0, 16);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) __builtin_memcpy(&v[2 * q], &w[q], 16);
+}
+__device__ __forceinline__ void gj_st16(double* S, const double (&v)[16]) {
+  const int c = 2 * (threadIdx.x & 31), r0 = threadIdx.x >> 5;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    S[(r0 + 8 * q) * GJ_LS + c] = v[2 * q];
+    S[(r0 + 8 * q) * GJ_LS + c + 1] = v[2 * q + 1];
   }
 }
 
@@ -540,22 +560,25 @@ __global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const do
   auto wtile = [&](int i, int j) { return buf + (int64_t)i * 64 * lda + (int64_t)j * 64; };
   // step k's operand (i, j): step 0 reads src0 (+ beta src0b), later steps the matrix itself
   // every load of the matrix and P is sc1 (src0 too: in place it is the matrix)
+  // (gj_ld16_sc1 layout; stored with gj_st16)
   auto ld_tile = [&](double (&v)[16], int k, int i, int j) {
-    gj_ld_sc1(v, tile(k == 0 ? src0 : buf, i, j), lda);
+    gj_ld16_sc1(v, tile(k == 0 ? src0 : buf, i, j), lda);
     if (k == 0 && src0b) {
       const double* B = tile(src0b, i, j);
+      const int c = 2 * (threadIdx.x & 31), r0 = threadIdx.x >> 5;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int e = threadIdx.x + 256 * q;
-        v[q] = fma(beta, B[(int64_t)(e >> 6) * lda + (e & 63)], v[q]);
-      }
+      for (int q = 0; q < 16; ++q)
+        v[q] = fma(beta, B[(int64_t)(r0 + 8 * (q >> 1)) * lda + c + (q & 1)], v[q]);
     }
   };
+  int pk_have = -1;   // the step whose P is in S1 (a workgroup often runs several of a step)
   auto ld_pk = [&](int k) {   // P_k -> S1
+    if (pk_have == k) return;
     gj_wait(1, [&](int) { return piv + k; }, 1u, sync, status);
     double v[16];
-    gj_ld_sc1(v, P + (int64_t)k * 4096, 64);
-    gj_st(S1, v);
+    gj_ld16_sc1(v, P + (int64_t)k * 4096, 64);
+    gj_st16(S1, v);
+    pk_have = k;
   };
   for (;;) {
     if (threadIdx.x == 0) tk = (int)__hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -566,10 +589,11 @@ __global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const do
     if (t == 0) {   // P_0
       double v[16];
       ld_tile(v, 0, 0, 0);
-      gj_st(S0, v);
+      gj_st16(S0, v);
       __syncthreads();
       gj_pivot_body<true>(S0, GJ_LS, 0, P, logd, status, S1);
       gj_publish(piv, 1u);
+      pk_have = -1;
       continue;
     }
     const int s = t - 1, k = s / nn;
@@ -605,8 +629,8 @@ __global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const do
               if (Bij) aij[fm][fn][q] = fma(beta, Bij[rr * lda + c], aij[fm][fn][q]);
             }
       }
-      gj_st(S0, v0);
-      gj_st(S2, v2);
+      gj_st16(S0, v0);
+      gj_st16(S2, v2);
       __syncthreads();   // A_ik and A_kj are in LDS: the column / row tasks may overwrite them
       if (threadIdx.x == 0) stu_sc1(loaded + i * nb + j, (unsigned)(k + 1));
       ld_pk(k);
@@ -637,6 +661,7 @@ __global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const do
         gj_pivot_body<true>(S0, GJ_LS, (int64_t)(k + 1) * 64, P + (int64_t)(k + 1) * 4096,
                       logd + k + 1, status, S1);
         gj_publish(piv + k + 1, 1u);
+        pk_have = -1;   // S1 was the pivot's scratch
       }
       continue;
     }
@@ -649,7 +674,7 @@ __global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const do
       if (k > 0) gj_wait(1, [&](int) { return ver + i * nb + j; }, (unsigned)k, sync, status);
       double v[16];
       ld_tile(v, k, i, j);
-      gj_st(col ? S0 : S2, v);
+      gj_st16(col ? S0 : S2, v);
       ld_pk(k);
       __syncthreads();
       if (col) gj_mm64(S0, S1, acc);
@@ -668,15 +693,12 @@ __global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const do
     // (k, k) <- P_k
     gj_wait(1, [&](int) { return piv + k; }, 1u, sync, status);
     {
-      double* Tkk = wtile(k, k);
-      const double* Pk = P + (int64_t)k * 4096;
-      double v[16];
-      gj_ld_sc1(v, Pk, 64);
+      const __amdgpu_buffer_rsrc_t rp = gj_rsrc(P + (int64_t)k * 4096), rt = gj_rsrc(wtile(k, k));
+      gj_u4 w[8];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int e = threadIdx.x + 256 * q;
-        st_sc1(&Tkk[(int64_t)(e >> 6) * lda + (e & 63)], v[q]);
-      }
+      for (int q = 0; q < 8; ++q) w[q] = __builtin_amdgcn_raw_buffer_load_b128(rp, gj_off16(q, 64), 0, 16);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) __builtin_amdgcn_raw_buffer_store_b128(w[q], rt, gj_off16(q, lda), 0, 16);
     }
     gj_publish(ver + k * nb + k, (unsigned)(k + 1));
   }

@@ -552,8 +552,15 @@ k_syrk_reduce_grp(double* __restrict__ slab, int splits, int64_t nblk) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   const int s0 = blockIdx.z * SYRK_RGRP;
   const int s1 = s0 + SYRK_RGRP < splits ? s0 + SYRK_RGRP : splits;
+  // all the group's loads in flight before the (ordered) sum: the loop form waited on each
+  double a[SYRK_RGRP];
+#pragma unroll
+  for (int q = 0; q < SYRK_RGRP; ++q)
+    a[q] = s0 + q < s1 ? slab[((int64_t)(s0 + q) * nblk + bid) * 4096 + e] : 0.0;
   double v = 0.0;
-  for (int sp = s0; sp < s1; ++sp) v += slab[((int64_t)sp * nblk + bid) * 4096 + e];
+#pragma unroll
+  for (int q = 0; q < SYRK_RGRP; ++q)
+    if (s0 + q < s1) v += a[q];
   slab[((int64_t)s0 * nblk + bid) * 4096 + e] = v;
 }
 
@@ -588,7 +595,17 @@ k_syrk_reduce_blk(const double* __restrict__ slab, int splits, int64_t nblk, int
   }
   double v = 0.0;
   if (!upper)
-    for (int sp = 0; sp < splits; sp += stride) v += slab[((int64_t)sp * nblk + bid) * 4096 + e];
+    for (int sp0 = 0; sp0 < splits; sp0 += 16 * stride) {   // 16 loads in flight, summed in order
+      double a[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int sp = sp0 + q * stride;
+        a[q] = sp < splits ? slab[((int64_t)sp * nblk + bid) * 4096 + e] : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (sp0 + q * stride < splits) v += a[q];
+    }
   if (packed) {
     red[bid * 4096 + e] = v;
     return;
