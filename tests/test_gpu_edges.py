@@ -302,3 +302,22 @@ def test_data_far_from_origin_or_widely_spread(sgp, mode, layout):
         o = O.fitc_obj_eval(cp, "sqexp", U, X, y, mu, 1e-6)
         gr = O.dlogp_dcov_par(cp, "sqexp", U, X, y, mu, 1e-6)["gradient"]
     _close(obj, grad, o, gr, cp)
+
+
+@pytest.mark.parametrize("mode", ["vi", "fitc"])
+def test_knots_past_the_persistent_chain(sgp, mode):
+    """m = 4160 (m_p = 4224, nb = 66 > 64): the m x m inverses fall back from the persistent
+    Gauss-Jordan kernel to one launch per pivot step, and the SYRKs from the balanced plan to the
+    packed one (m > 3968).  Objective and gradient against the adjoint model (R's det()
+    underflows here, quirk Q4; the literal oracle's n x m algebra is too slow at this m)."""
+    from oracle import adjoint_ref as A
+    P = O.make_gaussian_problem("C3", n=300, m=4160)
+    cp = P["cov_par"]
+    theta = np.array(list(cp.values()))
+    if mode == "vi":
+        obj, grad = sgp.vi_eval(cp, "ard", P["U"], P["X"], P["y"], P["mu"], P["delta"])
+        o, g = A.eval_vi("ard", theta, P["X"], P["y"], P["mu"], P["U"], P["delta"])
+    else:
+        obj, grad = sgp.fitc_eval(cp, "ard", P["U"], P["X"], P["y"], P["mu"], P["delta"])
+        o, g = A.eval_fitc("ard", theta, P["X"], P["y"], P["mu"], P["U"], P["delta"])
+    _close(obj, grad, o, dict(zip(cp, np.asarray(g))), cp)
