@@ -544,18 +544,18 @@ __global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const do
                                                     double* __restrict__ logd,
                                                     int* __restrict__ status,
                                                     unsigned* __restrict__ sync) {
-  __shared__ double lds[3 * 64 * GJ_LS];
+  __shared__ double lds[4 * 64 * GJ_LS];
   __shared__ int tk;
   double* S0 = lds;
   double* S1 = lds + 64 * GJ_LS;
   double* S2 = lds + 2 * 64 * GJ_LS;
+  double* S3 = lds + 3 * 64 * GJ_LS;
   unsigned* piv = sync + GJ_SYNC_PIV;
   unsigned* ver = sync + GJ_SYNC_VER;
   unsigned* loaded = ver + nb * nb;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   const int nn = nb * nb, n1 = nb - 1;
-  const int ntask = 1 + nb * nn;
   auto tile = [&](const double* A, int i, int j) { return A + (int64_t)i * 64 * lda + (int64_t)j * 64; };
   auto wtile = [&](int i, int j) { return buf + (int64_t)i * 64 * lda + (int64_t)j * 64; };
   // step k's operand (i, j): step 0 reads src0 (+ beta src0b), later steps the matrix itself
@@ -580,6 +580,46 @@ __global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const do
     gj_st16(S1, v);
     pk_have = k;
   };
+  // A_ij (step k's operand) in the accumulator layout of gj_mm64
+  auto ld_acc = [&](double (&aij)[2][2][4], int k, int i, int j) {
+    const double* Aij = tile(k == 0 ? src0 : buf, i, j);
+    const double* Bij = (k == 0 && src0b) ? tile(src0b, i, j) : nullptr;
+#pragma unroll
+    for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rr = wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
+          const int c = wc * 32 + fn * 16 + (lane & 15);
+          aij[fm][fn][q] = ld_sc1(&Aij[rr * lda + c]);
+          if (Bij) aij[fm][fn][q] = fma(beta, Bij[rr * lda + c], aij[fm][fn][q]);
+        }
+  };
+  // out tile (i, j) = aij - acc (and into LDS X when it is the look-ahead's fresh tile)
+  auto st_out = [&](int i, int j, const double (&aij)[2][2][4], const d4 (&acc)[2][2], double* X) {
+    double* Tij = wtile(i, j);
+#pragma unroll
+    for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rr = wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
+          const int c = wc * 32 + fn * 16 + (lane & 15);
+          const double v = aij[fm][fn][q] - acc[fm][fn][q];
+          st_sc1(&Tij[rr * lda + c], v);
+          if (X) X[rr * GJ_LS + c] = v;
+        }
+  };
+  // units of a step: the look-ahead tile (k+1, k+1) alone (not in the last step), the other
+  // interior tiles of each row i = k+1+a paired along the row (one A_ik P_k product serves two
+  // tiles: three 64^3 products and six tile loads for two tiles instead of four and eight),
+  // then the column / row tasks and (k, k)
+  const int half = (n1 + 1) / 2;                                   // units of a full row
+  const int u_reg = 1 + n1 / 2 + (n1 - 1) * half + 2 * n1 + 1;    // per step before the last
+  const int u_last = n1 * half + 2 * n1 + 1;
+  const int ntask = 1 + n1 * u_reg + u_last;
   for (;;) {
     if (threadIdx.x == 0) tk = (int)__hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
@@ -596,66 +636,82 @@ __global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const do
       pk_have = -1;
       continue;
     }
-    const int s = t - 1, k = s / nn;
-    int r = s - k * nn;
+    int k, r;
+    {
+      const int s = t - 1;
+      k = s / u_reg;
+      if (k >= n1) k = n1;
+      r = s - k * u_reg;
+    }
+    const bool last = k == n1;
     d4 acc[2][2];
-    if (r < n1 * n1) {
-      // interior tile in shell order
-      int sh = (int)sqrtf((float)r);
-      while (sh * sh > r) --sh;
-      while ((sh + 1) * (sh + 1) <= r) ++sh;
-      const int o = r - sh * sh;
-      const int a = o < sh ? o : sh, b = o < sh ? sh : (o < 2 * sh ? o - sh : sh);
-      const int i = (k + 1 + a) % nb, j = (k + 1 + b) % nb;
+    int ia = -1, b0 = 0, b1 = -1;    // interior unit: row offset a, column offsets b0 (, b1)
+    if (!last && r == 0) {
+      ia = 0;                        // the look-ahead tile
+    } else {
+      int q = last ? r : r - 1;
+      for (int a = 0; a < n1; ++a) {
+        const int skip = (a == 0 && !last) ? 1 : 0;
+        const int cnt = n1 - skip, u = (cnt + 1) / 2;
+        if (q < u) {
+          ia = a;
+          b0 = skip + 2 * q;
+          b1 = b0 + 1 < n1 ? b0 + 1 : -1;
+          break;
+        }
+        q -= u;
+      }
+      if (ia < 0) r = q + 0;         // past the interior units: q counts the column / row tasks
+    }
+    if (ia >= 0) {
+      const int i = (k + 1 + ia) % nb, j0 = (k + 1 + b0) % nb;
+      const bool two = b1 >= 0;
+      const int j1 = two ? (k + 1 + b1) % nb : j0;
+      const bool look_ahead = !last && ia == 0 && b0 == 0;
       if (k > 0) {
-        const int fi[3] = {i * nb + j, i * nb + k, k * nb + j};
-        gj_wait(3, [&](int q) { return ver + fi[q]; }, (unsigned)k, sync, status);
+        const int f0 = i * nb + j0, f1 = i * nb + k, f2 = k * nb + j0, f3 = i * nb + j1,
+                  f4 = k * nb + j1;
+        gj_wait(two ? 5 : 3,
+                [&](int q) {
+                  return ver + (q == 0 ? f0 : q == 1 ? f1 : q == 2 ? f2 : q == 3 ? f3 : f4);
+                },
+                (unsigned)k, sync, status);
       }
-      double v0[16], v2[16], aij[2][2][4];
+      double v0[16], v2[16], aij0[2][2][4], aij1[2][2][4];
       ld_tile(v0, k, i, k);
-      ld_tile(v2, k, k, j);
-      {
-        const double* Aij = tile(k == 0 ? src0 : buf, i, j);
-        const double* Bij = (k == 0 && src0b) ? tile(src0b, i, j) : nullptr;
-#pragma unroll
-        for (int fm = 0; fm < 2; ++fm)
-#pragma unroll
-          for (int fn = 0; fn < 2; ++fn)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const int rr = wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
-              const int c = wc * 32 + fn * 16 + (lane & 15);
-              aij[fm][fn][q] = ld_sc1(&Aij[rr * lda + c]);
-              if (Bij) aij[fm][fn][q] = fma(beta, Bij[rr * lda + c], aij[fm][fn][q]);
-            }
-      }
+      ld_tile(v2, k, k, j0);
+      ld_acc(aij0, k, i, j0);
       gj_st16(S0, v0);
       gj_st16(S2, v2);
+      if (two) {
+        ld_tile(v2, k, k, j1);
+        ld_acc(aij1, k, i, j1);
+        gj_st16(S3, v2);
+      }
       __syncthreads();   // A_ik and A_kj are in LDS: the column / row tasks may overwrite them
-      if (threadIdx.x == 0) stu_sc1(loaded + i * nb + j, (unsigned)(k + 1));
+      if (threadIdx.x == 0) {
+        stu_sc1(loaded + i * nb + j0, (unsigned)(k + 1));
+        if (two) stu_sc1(loaded + i * nb + j1, (unsigned)(k + 1));
+      }
       ld_pk(k);
       __syncthreads();
       gj_mm64(S0, S1, acc);                      // A_ik P_k
       __syncthreads();
       gj_store_acc<false>(S0, GJ_LS, acc, 1.0);
       __syncthreads();
-      gj_mm64(S0, S2, acc);                      // (A_ik P_k) A_kj
-      const bool look_ahead = (i == k + 1) && (j == k + 1);
+      gj_mm64(S0, S2, acc);                      // (A_ik P_k) A_kj0
       if (look_ahead) __syncthreads();           // S0 takes the fresh tile
-      double* Tij = wtile(i, j);
-#pragma unroll
-      for (int fm = 0; fm < 2; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < 2; ++fn)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int rr = wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
-            const int c = wc * 32 + fn * 16 + (lane & 15);
-            const double v = aij[fm][fn][q] - acc[fm][fn][q];
-            st_sc1(&Tij[rr * lda + c], v);
-            if (look_ahead) S0[rr * GJ_LS + c] = v;
-          }
-      gj_publish(ver + i * nb + j, (unsigned)(k + 1));
+      st_out(i, j0, aij0, acc, look_ahead ? S0 : nullptr);
+      if (two) {
+        gj_mm64(S0, S3, acc);                    // (A_ik P_k) A_kj1
+        st_out(i, j1, aij1, acc, nullptr);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        stu_sc1(ver + i * nb + j0, (unsigned)(k + 1));
+        if (two) stu_sc1(ver + i * nb + j1, (unsigned)(k + 1));
+      }
       if (look_ahead) {
         __syncthreads();
         gj_pivot_body<true>(S0, GJ_LS, (int64_t)(k + 1) * 64, P + (int64_t)(k + 1) * 4096,
@@ -665,7 +721,6 @@ __global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const do
       }
       continue;
     }
-    r -= n1 * n1;
     if (r < 2 * n1) {
       // column task (i, k): -A_ik P_k, or row task (k, j): P_k A_kj
       const bool col = r < n1;

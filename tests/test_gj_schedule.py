@@ -1,8 +1,8 @@
 """CPU model of k_gj_persist's task schedule (sparsergps_amd/csrc/k_dense.hip).
 
 The persistent Gauss-Jordan kernel runs the whole m x m SPD inverse in one launch: workgroups
-claim tickets in order and each task waits on flags (tile versions, "operands loaded", pivot
-ready) before it reads or overwrites tiles in place.  This model restates the ticket decoding
+claim tickets in order (interior tiles of a row paired per task) and each task waits on flags
+(tile versions, "operands loaded", pivot ready) before it reads or overwrites tiles in place.  This model restates the ticket decoding
 and the flag protocol task by task, runs G simulated workgroups under random interleavings
 (each wait / load / store is a separate scheduling point), and checks that
 
@@ -18,28 +18,43 @@ import pytest
 
 
 def decode(t, nb):
-    """k_gj_persist's ticket -> (kind, k, i, j); kinds: pivot0, interior, col, row, diag."""
+    """k_gj_persist's ticket -> (kind, k, i, js); kinds: pivot0, unit (interior tiles (i, j) for
+    j in js: the look-ahead (k+1, k+1) alone, the others paired along their row), col, row,
+    diag (js = (j,))."""
     if t == 0:
-        return ("pivot0", 0, 0, 0)
-    nn, n1 = nb * nb, nb - 1
+        return ("pivot0", 0, 0, (0,))
+    n1 = nb - 1
+    half = (n1 + 1) // 2
+    u_reg = 1 + n1 // 2 + (n1 - 1) * half + 2 * n1 + 1
     s = t - 1
-    k, r = divmod(s, nn)
-    if r < n1 * n1:
-        sh = int(np.sqrt(r))
-        while sh * sh > r:
-            sh -= 1
-        while (sh + 1) * (sh + 1) <= r:
-            sh += 1
-        o = r - sh * sh
-        a = o if o < sh else sh
-        b = sh if o < sh else (o - sh if o < 2 * sh else sh)
-        return ("interior", k, (k + 1 + a) % nb, (k + 1 + b) % nb)
-    r -= n1 * n1
+    k = min(s // u_reg, n1)
+    r = s - k * u_reg
+    last = k == n1
+    if not last and r == 0:
+        return ("unit", k, (k + 1) % nb, ((k + 1) % nb,))
+    q = r if last else r - 1
+    for a in range(n1):
+        skip = 1 if (a == 0 and not last) else 0
+        cnt = n1 - skip
+        u = (cnt + 1) // 2
+        if q < u:
+            b0 = skip + 2 * q
+            bs = (b0, b0 + 1) if b0 + 1 < n1 else (b0,)
+            return ("unit", k, (k + 1 + a) % nb, tuple((k + 1 + b) % nb for b in bs))
+        q -= u
+    r = q
     if r < 2 * n1:
         col = r < n1
         x = (k + 1 + (r if col else r - n1)) % nb
-        return ("col", k, x, k) if col else ("row", k, k, x)
-    return ("diag", k, k, k)
+        return ("col", k, x, (k,)) if col else ("row", k, k, (x,))
+    return ("diag", k, k, (k,))
+
+
+def ntasks(nb):
+    n1 = nb - 1
+    half = (n1 + 1) // 2
+    u_reg = 1 + n1 // 2 + (n1 - 1) * half + 2 * n1 + 1
+    return 1 + n1 * u_reg + n1 * half + 2 * n1 + 1
 
 
 class Chain:
@@ -76,28 +91,35 @@ class Chain:
 
     def task(self, t):
         """Generator: yields wait predicates; everything between two yields is atomic."""
-        kind, k, i, j = decode(t, self.nb)
+        kind, k, i, js = decode(t, self.nb)
         nb = self.nb
         if kind == "pivot0":
             self.pivot(0, self.tile(0, 0, 0))
             self.piv[0] = 1
             return
-        if kind == "interior":
+        if kind == "unit":
             if k > 0:
-                yield lambda: min(self.ver[i, j], self.ver[i, k], self.ver[k, j]) >= k
-            aik, akj, aij = self.tile(k, i, k), self.tile(k, k, j), self.tile(k, i, j)
+                yield lambda: min([self.ver[i, k]] + [min(self.ver[i, j], self.ver[k, j])
+                                                      for j in js]) >= k
+            aik = self.tile(k, i, k)
+            ops = [(j, self.tile(k, k, j), self.tile(k, i, j)) for j in js]
             yield None   # the loads land; then "loaded"
-            self.loaded[i, j] = k + 1
+            for j in js:
+                self.loaded[i, j] = k + 1
             yield lambda: self.piv[k] >= 1
-            v = aij - (aik @ self.P[k]) @ akj
+            c = aik @ self.P[k]
+            outs = [(j, aij - c @ akj) for j, akj, aij in ops]
             yield None
-            self.put(i, j, v)
-            self.ver[i, j] = k + 1
-            if i == k + 1 and j == k + 1:
-                self.pivot(k + 1, v)
+            for j, v in outs:
+                self.put(i, j, v)
+            for j, _ in outs:
+                self.ver[i, j] = k + 1
+            if i == k + 1 and js == (k + 1,):
+                self.pivot(k + 1, outs[0][1])
                 yield None
                 self.piv[k + 1] = 1
             return
+        j = js[0]
         if kind in ("col", "row"):
             if k > 0:
                 yield lambda: self.ver[i, j] >= k
@@ -119,7 +141,7 @@ class Chain:
 
 
 def run(chain, G, rng):
-    ntask = 1 + chain.nb ** 3
+    ntask = ntasks(chain.nb)
     ticket = 0
     workers = [None] * G          # (generator, pending predicate)
     done = [False] * G
@@ -172,15 +194,21 @@ def test_schedule_sum_form(nb, G):
 
 
 def test_decode_covers_every_tile_once_per_step():
-    for nb in range(1, 9):
+    for nb in range(1, 10):
         seen = {}
-        for t in range(1, 1 + nb ** 3):
-            kind, k, i, j = decode(t, nb)
-            assert (k, i, j) not in seen
-            seen[(k, i, j)] = kind
-            assert kind == ("diag" if i == k and j == k else
-                            "col" if j == k else "row" if i == k else "interior")
+        for t in range(1, ntasks(nb)):
+            kind, k, i, js = decode(t, nb)
+            for j in js:
+                assert (k, i, j) not in seen
+                seen[(k, i, j)] = kind
+                assert kind == ("diag" if i == k and j == k else "col" if j == k else
+                                "row" if i == k else "unit")
+            if kind == "unit" and len(js) == 2:
+                assert js[1] == (js[0] + 1) % nb != k
         assert len(seen) == nb ** 3
-        # the first task of each step (but the last) is its look-ahead tile
+        # the first task of each step (but the last) is its look-ahead tile, alone
+        n1 = nb - 1
+        half = (n1 + 1) // 2
+        u_reg = 1 + n1 // 2 + (n1 - 1) * half + 2 * n1 + 1
         for k in range(nb - 1):
-            assert decode(1 + k * nb * nb, nb) == ("interior", k, k + 1, k + 1)
+            assert decode(1 + k * u_reg, nb) == ("unit", k, k + 1, (k + 1,))
