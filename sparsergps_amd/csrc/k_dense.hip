@@ -596,7 +596,9 @@ __global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const do
           if (Bij) aij[fm][fn][q] = fma(beta, Bij[rr * lda + c], aij[fm][fn][q]);
         }
   };
-  // out tile (i, j) = aij - acc (and into LDS X when it is the look-ahead's fresh tile)
+  // out tile (i, j) = aij - acc into memory, or (X) only into LDS: the look-ahead's fresh tile
+  // is read by nothing but its own pivot (step k+1's (k+1, k+1) task overwrites the tile with
+  // P_{k+1}, and no task of step k+1 reads it), so it is neither stored nor published
   auto st_out = [&](int i, int j, const double (&aij)[2][2][4], const d4 (&acc)[2][2], double* X) {
     double* Tij = wtile(i, j);
 #pragma unroll
@@ -608,8 +610,8 @@ __global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const do
           const int rr = wr * 32 + fm * 16 + (lane >> 4) + 4 * q;
           const int c = wc * 32 + fn * 16 + (lane & 15);
           const double v = aij[fm][fn][q] - acc[fm][fn][q];
-          st_sc1(&Tij[rr * lda + c], v);
           if (X) X[rr * GJ_LS + c] = v;
+          else st_sc1(&Tij[rr * lda + c], v);
         }
   };
   // units of a step: the look-ahead tile (k+1, k+1) alone (not in the last step), the other
@@ -706,13 +708,14 @@ __global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const do
         gj_mm64(S0, S3, acc);                    // (A_ik P_k) A_kj1
         st_out(i, j1, aij1, acc, nullptr);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        stu_sc1(ver + i * nb + j0, (unsigned)(k + 1));
-        if (two) stu_sc1(ver + i * nb + j1, (unsigned)(k + 1));
-      }
-      if (look_ahead) {
+      if (!look_ahead) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          stu_sc1(ver + i * nb + j0, (unsigned)(k + 1));
+          if (two) stu_sc1(ver + i * nb + j1, (unsigned)(k + 1));
+        }
+      } else {
         __syncthreads();
         gj_pivot_body<true>(S0, GJ_LS, (int64_t)(k + 1) * 64, P + (int64_t)(k + 1) * 4096,
                       logd + k + 1, status, S1);
