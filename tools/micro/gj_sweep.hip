@@ -6,7 +6,8 @@
 //   col: every 16-lane row holds the whole block, lane c column c (16 registers); a sweep is one
 //        v_fmac_f64_dpp per element (src0 = lane k's register by row_newbcast), the pivot lane's
 //        column kept unscaled with a pending factor (applied once after the 16 sweeps).
-//   pipe: cur pipelined one sweep ahead (the product since round 5);
+//   pipe: cur pipelined one sweep ahead (measured, not kept);
+//   dpp: cur with one DPP64 v_fmac_f64_dpp per register instead of DPP moves and selects;
 //   build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form -o gj_sweep gj_sweep.hip
 #include <cmath>
 #include <cstdio>
@@ -78,6 +79,42 @@ __device__ __forceinline__ void sweep_pipe(d4& t, double (&dk)[16]) {
   }
 }
 
+// dpp: the accumulator layout with one DPP64 v_fmac_f64_dpp per register (W_iK read from lane K
+// of the row, nvj = -r W_Kj per lane, r - 1 on column K), row K set apart afterwards
+template <int K>
+__device__ __forceinline__ void sweep_dpp_step(d4& t, double (&dk)[16], int lr, int lc) {
+  constexpr int kq = K >> 2, kr = K & 3;
+  const double vc = __shfl(t[kq], lc + 16 * kr, 64);
+  const double d = readlane_f64(t[kq], K + 16 * kr);
+  const double r = rcp_nr(d);
+  dk[K] = d;
+  const double rowk = t[kq];
+  const double nvj = (lc == K) ? r - 1.0 : -(r * vc);
+  double a0 = t[0], a1 = t[1], a2 = t[2], a3 = t[3];
+  asm volatile("s_nop 1\n"
+               "v_fmac_f64_dpp %0, %0, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf\n"
+               "v_fmac_f64_dpp %1, %1, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf\n"
+               "v_fmac_f64_dpp %2, %2, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf\n"
+               "v_fmac_f64_dpp %3, %3, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf\n"
+               : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)
+               : "v"(nvj), "i"(K));
+  t[0] = a0; t[1] = a1; t[2] = a2; t[3] = a3;
+  const double rk = (lc == K) ? -r : r * rowk;
+  t[kq] = (lr == kr) ? rk : t[kq];
+}
+
+__device__ __forceinline__ void sweep_dpp(d4& t, double (&dk)[16]) {
+  const int lane = threadIdx.x & 63, lr = lane >> 4, lc = lane & 15;
+  sweep_dpp_step<0>(t, dk, lr, lc);   sweep_dpp_step<1>(t, dk, lr, lc);
+  sweep_dpp_step<2>(t, dk, lr, lc);   sweep_dpp_step<3>(t, dk, lr, lc);
+  sweep_dpp_step<4>(t, dk, lr, lc);   sweep_dpp_step<5>(t, dk, lr, lc);
+  sweep_dpp_step<6>(t, dk, lr, lc);   sweep_dpp_step<7>(t, dk, lr, lc);
+  sweep_dpp_step<8>(t, dk, lr, lc);   sweep_dpp_step<9>(t, dk, lr, lc);
+  sweep_dpp_step<10>(t, dk, lr, lc);  sweep_dpp_step<11>(t, dk, lr, lc);
+  sweep_dpp_step<12>(t, dk, lr, lc);  sweep_dpp_step<13>(t, dk, lr, lc);
+  sweep_dpp_step<14>(t, dk, lr, lc);  sweep_dpp_step<15>(t, dk, lr, lc);
+}
+
 template <int K>
 __device__ __forceinline__ void sweep_col_step(double (&R)[16], double (&dk)[16], double& sig,
                                                int c) {
@@ -145,6 +182,25 @@ __global__ void __launch_bounds__(64) k_pipe(const double* B, double* out, doubl
   }
 }
 
+__global__ void __launch_bounds__(64) k_dpp(const double* B, double* out, double* piv, int reps) {
+  const int lane = threadIdx.x, lr = lane >> 4, lc = lane & 15;
+  double dk[16];
+  d4 t;
+  for (int r = 0; r < reps; ++r) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] = B[(lr + 4 * q) * 16 + lc];
+    sweep_dpp(t, dk);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[(lr + 4 * q) * 16 + lc] = t[q];
+  }
+  if (lane < 16) {
+    double v = dk[0];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) v = (lane == k) ? dk[k] : v;
+    piv[lane] = v;
+  }
+}
+
 __global__ void __launch_bounds__(64) k_col(const double* B, double* out, double* piv, int reps) {
   const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
   double dk[16], R[16];
@@ -183,15 +239,17 @@ int main() {
   hipMalloc(&dB, 16 * 16 * 8); hipMalloc(&dO, 16 * 16 * 8); hipMalloc(&dP, 16 * 8);
   hipMemcpy(dB, B.data(), 16 * 16 * 8, hipMemcpyHostToDevice);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
-  const char* names[3] = {"cur (accumulator layout)", "col (v_fmac_f64_dpp)", "pipe (one sweep ahead)"};
+  const char* names[4] = {"cur (accumulator layout)", "col (v_fmac_f64_dpp)", "pipe (one sweep ahead)",
+                          "dpp (DPP64 fmac, acc layout)"};
   std::vector<double> O0(16 * 16), P0(16);
   for (int it = 0; it < 3; ++it)
-    for (int v = 0; v < 3; ++v) {
+    for (int v = 0; v < 4; ++v) {
       const int reps = 20000;
       hipEventRecord(e0, 0);
       if (v == 0) hipLaunchKernelGGL(k_cur, dim3(1), dim3(64), 0, 0, dB, dO, dP, reps);
       else if (v == 1) hipLaunchKernelGGL(k_col, dim3(1), dim3(64), 0, 0, dB, dO, dP, reps);
-      else hipLaunchKernelGGL(k_pipe, dim3(1), dim3(64), 0, 0, dB, dO, dP, reps);
+      else if (v == 2) hipLaunchKernelGGL(k_pipe, dim3(1), dim3(64), 0, 0, dB, dO, dP, reps);
+      else hipLaunchKernelGGL(k_dpp, dim3(1), dim3(64), 0, 0, dB, dO, dP, reps);
       hipEventRecord(e1, 0); hipEventSynchronize(e1);
       float ms; hipEventElapsedTime(&ms, e0, e1);
       hipMemcpy(O.data(), dO, 16 * 16 * 8, hipMemcpyDeviceToHost);
@@ -206,7 +264,7 @@ int main() {
         }
       }
       if (v == 0) { O0 = O; P0 = pv; }
-      const bool same = v == 1 || (O == O0 && pv == P0);
+      const bool same = v == 1 || v == 3 || (O == O0 && pv == P0);
       printf("%-26s %7.3f us per 16 sweeps (%6.1f ns/sweep)  |B inv - I| %.2e  sum log piv %.15f%s\n",
              names[v], ms * 1e3 / reps, ms * 1e6 / reps / 16, err, ld,
              v == 2 ? (same ? "  bit-identical to cur" : "  DIFFERS from cur") : "");
