@@ -266,6 +266,11 @@ struct sgp_ctx {
   hipEvent_t ev_s = nullptr, ev_m3 = nullptr, ev_bm = nullptr;
   hipEvent_t ev_lo = nullptr;             // VI phase 1: builder done (main) / side work done (aux_lo)
   bool vi_k22_ordered = true;             // VI phase 1 ordered main behind K22's build (ev_lo)
+  // sgp_eval_vi (no reduction between the phases): at m_p = 256 t's row sums leave phase 1's
+  // critical path for aux_lo in phase 2 (t is first read by the m-vectors, after the Bm chain)
+  bool fused_vi = false, t_deferred = false;
+  int64_t t_rows_def = 0;
+  hipEvent_t ev_t = nullptr;
   bool pack_red1 = false;                 // VI red1 carries S as packed lower 64-blocks
   bool borrowed_streams = false;          // own / aux / aux_lo belong to another context
   double* Sfull = nullptr;                // S unpacked from a packed red1 (mp_max^2)
@@ -464,6 +469,7 @@ void ctx_free(sgp_ctx* c) {
   if (c->ev_m3) hipEventDestroy(c->ev_m3);
   if (c->ev_bm) hipEventDestroy(c->ev_bm);
   if (c->ev_lo) hipEventDestroy(c->ev_lo);
+  if (c->ev_t) hipEventDestroy(c->ev_t);
   if (c->aux && !c->borrowed_streams) hipStreamDestroy(c->aux);
   if (c->aux_lo && !c->borrowed_streams) hipStreamDestroy(c->aux_lo);
   for (hipEvent_t e : c->pool) hipEventDestroy(e);
@@ -768,7 +774,8 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
       hipEventCreateWithFlags(&c->ev_s, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_m3, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_bm, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_lo, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_lo, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_t, hipEventDisableTiming) != hipSuccess) {
     set_err("hipStream/hipEvent creation failed");
     ctx_free(c);
     delete c;
@@ -1216,6 +1223,7 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   // for K22's build itself
   const bool small_syrk = syrk_use_s256(mpv, false);
   c->vi_k22_ordered = !small_syrk;
+  c->t_deferred = false;
   {
     // K12, and t = K^T r riding along in the memory-bound builder (keeps the SYRK's
     // diagonal tiles as cheap as the others); the first HIP call of the evaluation, so the
@@ -1252,7 +1260,10 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   if (st) return st;
   // red1 = [S (full, or its packed lower 64-blocks), t, r'r]
   const int64_t toff = vi_red1_toff(c, mpv);
-  if (small_syrk) {
+  if (small_syrk && c->fused_vi) {
+    c->t_deferred = true;   // summed on aux_lo in phase 2
+    c->t_rows_def = t_rows;
+  } else if (small_syrk) {
     HIPCHK(launch_knot_reduce(c->tslab, t_rows, mpv, 1, c->T1, c->mp_max * c->mp_max,
                               red1 + toff, false, c->stream));
   } else {
@@ -1384,6 +1395,12 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
     // inversion (T22 and K22inv are final once the K22 chain on `aux` has finished).  Beside
     // the K12 contraction instead, the GEMMs' workgroups starved and slowed it more.
     HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_s, 0));
+    if (c->t_deferred) {   // t = K^T r from the builder's partials (phase 1 deferred it; only
+                           // sgp_eval_vi does, whose red1 is the context's own)
+      HIPCHK(launch_knot_reduce(c->tslab, c->t_rows_def, mp, 1, c->T1, c->mp_max * c->mp_max,
+                                c->red1 + toff, false, c->aux_lo));
+      HIPCHK(hipEventRecord(c->ev_t, c->aux_lo));
+    }
     HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_k22, 0));
     Scope ta(c, "m3_aux", c->aux_lo);
     HIPCHK(launch_dot(c->K22inv, S, mm, c->slab_aux, c->sc + SC_TRKS, c->aux_lo));
@@ -1398,6 +1415,10 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
   }
   {
     Scope tm(c, "mm_vectors");
+    if (c->t_deferred) {
+      HIPCHK(hipStreamWaitEvent(c->stream, c->ev_t, 0));
+      c->t_deferred = false;
+    }
     if (flags & SGP_FLAG_OBJ_ONLY) {   // elbo_fun alone: no adjoint work
       HIPCHK(dense_gemv(c->Binv, mp, t, 1.0 / z, c->uvec, c->stream));       // u = Binv t / z
       HIPCHK(launch_dot(t, c->uvec, mp, c->slab_small, c->sc + SC_TU, c->stream));
@@ -1511,7 +1532,9 @@ int sgp_eval_vi(sgp_ctx* c, int kernel, const double* theta, const double* U, in
                 int64_t ldu, double delta, unsigned flags, double* obj, double* grad) {
   MULTI_FWD(c, obj && (grad || (flags & SGP_FLAG_OBJ_ONLY)) ? multi_eval_vi(c->multi, kernel, theta, U, m, ldu, delta, flags, obj, grad) : multi_bad_args());
   if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
+  c->fused_vi = true;   // nothing reduces red1 between the phases
   int st = sgp_vi_phase1(c, kernel, theta, U, m, ldu, delta, c->red1);
+  c->fused_vi = false;
   if (st) return st;
   st = sgp_vi_phase2(c, c->red1, c->n, flags, c->red2);
   if (st) return st;
