@@ -431,6 +431,12 @@ int dalloc(T** p, int64_t count) {
 // the evaluation is the same either way.
 bool tstore_ready(sgp_ctx* c) {
   if (c->tstore_state == 0) {
+    // SGP_TSTORE=0: the recompute-everything passes, as when the memory is not there (tests)
+    const char* env = getenv("SGP_TSTORE");
+    if (env && env[0] == '0') {
+      c->tstore_state = -1;
+      return false;
+    }
     const int64_t cnt = c->n_pad * c->mp_max;
     if (hipMalloc(reinterpret_cast<void**>(&c->tq), sizeof(double) * cnt) == hipSuccess &&
         hipMalloc(reinterpret_cast<void**>(&c->tp), sizeof(double) * cnt) == hipSuccess) {
@@ -445,6 +451,9 @@ bool tstore_ready(sgp_ctx* c) {
   }
   return c->tstore_state == 1;
 }
+
+// FITC / Laplace: both stored products read in ONE gradient pass (ConArgs::tin2; d <= 8)
+static bool fuse_tt(sgp_ctx* c) { return c->kp.d <= 8 && tstore_ready(c); }
 
 void ctx_free(sgp_ctx* c) {
   void* ptrs[] = {c->X,      c->r,     c->K,      c->alpha,   c->zinv,  c->U,    c->K22,
@@ -1670,10 +1679,18 @@ int sgp_fitc_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned f
       a1.tin = c->tp;
       a1.alpha_in = c->alpha;
     }
+    if (fuse_tt(c)) {
+      // with both products stored, pass 2's term -diag(omega) K K22^-1 joins this pass (one
+      // read of K instead of two; its records stay zero -- the finish sums the two sets)
+      a1.tin2 = c->tq;
+      a1.M2 = c->K22inv;
+      a1.rs_vec2 = c->omega;
+      a1.rs2 = -1.0;
+    }
     st = contract_pass(c, c->Binv, a1, red2 + off, kout, false);
     if (st) return st;
   }
-  {
+  if (!fuse_tt(c)) {
     Scope tm(c, "contract_knm_b");
     // pass 2: G2 = -diag(omega) K K22^-1
     ConArgs a2;
@@ -2125,8 +2142,21 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
     a1.rs_vec = lvec(c, LV_B);
     a1.rs = -1.0;
     if (tstore_ready(c)) a1.tin = c->tp;   // K C from lap_grad_a's row-quadratic pass
+    if (fuse_tt(c)) {
+      // and G2 = -diag(2a) K K22^-1 from lap_begin's rowquad_q in the same pass (one read of
+      // K; the second record set stays zero -- the finish sums the two)
+      a1.tin2 = c->tq;
+      a1.M2 = c->K22inv;
+      a1.rs_vec2 = lvec(c, LV_A);
+      a1.rs2 = -2.0;
+    }
     int st = contract_pass(c, c->Binv, a1, red_out + off, kout, false);
     if (st) return st;
+    if (fuse_tt(c)) {
+      *count = off + 2 * nrec + (c->knot_on ? mp * kp.d : 0);
+      c->lap_state = LS_FIN;
+      return SGP_OK;
+    }
     // G2 = -diag(2a) K K22^-1
     ConArgs a2;
     a2.rs_vec = lvec(c, LV_A);

@@ -884,7 +884,9 @@ k_syrk_reduce_t(const double* __restrict__ slab_t, const double* __restrict__ sl
 enum { EPI_GRAD = 0, EPI_ROWQUAD = 1 };
 
 // KU (row quadratic forms without u: the Z pass): false compiles the K u fold out of the k-loop
-template <int DT, int EPI, bool V2 = false, bool KNOT = false, bool FROM_T = false, bool KU = true>
+// T2 (FROM_T only): a second stored product folded in (ConArgs::tin2)
+template <int DT, int EPI, bool V2 = false, bool KNOT = false, bool FROM_T = false, bool KU = true,
+          bool T2 = false>
 __global__ void __launch_bounds__(256, 2)
 k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict__ M,
            const double* __restrict__ X, int64_t ldx, int64_t n, int64_t n_pad,
@@ -1019,6 +1021,10 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   double* s_xs = s_v + T128;                // MFMA B image [x~ | x~^2] of one coordinate chunk
   double* s_us = s_xs + T128 * 16;          // 128 x 9 ([col][c], scaled; odd stride: 16
                                             // columns on distinct banks)
+  // T2: the second product's row scales, past the gradient epilogue's K stage (s_us, 2 x 16
+  // x 136 doubles of stage: 3968 + 4352 doubles in)
+  double* s_rs2 = lds + 8320;
+  static_assert(8320 + T128 <= 2 * (A_SZ + B_SZ), "s_rs2 fits the LDS image");
   ku += __shfl_xor(ku, 1, 64);                       // the two halves of row `arow`
   double a2 = 0.0;                                    // alpha^2, counted once (tj == 0)
   if ((tid & 1) == 0) {
@@ -1028,6 +1034,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
                                   : (with_u ? (r[i] - ku) * iz : 0.0);   // padded rows -> 0
     s_alpha[arow] = al;
     s_rs[arow] = ca.rs_vec ? ca.rs * ca.rs_vec[i] : ca.rs;
+    if constexpr (T2) s_rs2[arow] = ca.rs_vec2 ? ca.rs2 * ca.rs_vec2[i] : ca.rs2;
     s_beta[arow] = with_v ? ca.beta_in[i] : 0.0;
     if (tj == 0) {
       if (ca.count_a2 && i < n) a2 = al * al;
@@ -1146,8 +1153,21 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
             (__attribute__((address_space(3))) void*)(kst + ((s_) & 1) * 16 * KST + rho_ * KST), \
             16, 0, 0);                                                                   \
       }
+      // T2: the second stored product's values of a half-stage (rows 2h, 2h + 1 of fragment fm,
+      // four column fragments), loaded into registers one half-stage ahead beside the K stage's
+      // DMA (the same vmcnt(0) waits cover both)
+      double t2n[2][4];
+#define CON_T2LOAD(s_)                                                                   \
+      if constexpr (T2) {                                                                \
+        _Pragma("unroll") for (int r2_ = 0; r2_ < 2; ++r2_)                              \
+        _Pragma("unroll") for (int fn_ = 0; fn_ < 4; ++fn_)                              \
+          t2n[r2_][fn_] = ca.tin2[(i0 + wr * 64 + ((s_) >> 1) * 16 + (lane >> 4) +        \
+                                   4 * (2 * ((s_) & 1) + r2_)) * mp + j0 + wc * 64 +      \
+                                  fn_ * 16 + (lane & 15)];                                \
+      }
       CON_KHALF(0);
       CON_KHALF(1);
+      CON_T2LOAD(0);
       CON_XSTAGE(0);
       __builtin_amdgcn_s_waitcnt(0);            // K stage 0 (LDS-DMA) landed
       __syncthreads();
@@ -1176,6 +1196,14 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
             __syncthreads();
             if (hs < 7) { CON_KHALF(hs + 1); }
           }
+          double t2c[2][4];
+          if constexpr (T2) {
+#pragma unroll
+            for (int r2 = 0; r2 < 2; ++r2)
+#pragma unroll
+              for (int fn = 0; fn < 4; ++fn) t2c[r2][fn] = t2n[r2][fn];
+            if (hs < 7) { CON_T2LOAD(hs + 1); }
+          }
           const double* kb = kst + h * 16 * KST;
           double xb[2];
 #pragma unroll
@@ -1193,6 +1221,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
               const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
               const bool valid = cval[fn] && ((i0 + row) < n);
               double G = s_rs[row] * acc[fm][fn][q];
+              if constexpr (T2) G = fma(s_rs2[row], t2c[r2][fn], G);
               if constexpr (V2) G = fma(s_beta[row], vcol[fn], G);
               G = fma(s_alpha[row], ucol[fn], G);
               const double w = valid ? G * kv[r2] : 0.0;
@@ -1211,6 +1240,7 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
         __syncthreads();                        // everyone is done reading the last stage
       }
 #undef CON_KHALF
+#undef CON_T2LOAD
       SGP_PROBE_CON_STAMP(5);
       // D fragment fn: lane l, register q -> column wc*64 + fn*16 + (l>>4) + 4q, c' = l & 15
       const int cp = lane & 15, cc = cp & 7;
@@ -1379,6 +1409,7 @@ struct CoincArgs {
   const double* alpha; const double* uvec; const double* beta; const double* vvec;
   const double* rs_vec; double rs; const double* cdiag;
   uint8_t* cflag; int flag_mode;
+  const double* M2; const double* rs_vec2; double rs2;   // ConArgs::M2 (fused two-product pass)
 };
 
 __device__ __forceinline__ void coinc_body(const CoincArgs& ca, int64_t bid, int64_t nblk,
@@ -1416,6 +1447,11 @@ __device__ __forceinline__ void coinc_body(const CoincArgs& ca, int64_t bid, int
       double t = 0.0;
       for (int64_t k = 0; k < m; ++k) t = fma(K[i * mp + k], M[k * mp + j], t);
       double g = (rs_vec ? rs * rs_vec[i] : rs) * t;
+      if (ca.M2) {
+        double t2 = 0.0;
+        for (int64_t k = 0; k < m; ++k) t2 = fma(K[i * mp + k], ca.M2[k * mp + j], t2);
+        g = fma(ca.rs_vec2 ? ca.rs2 * ca.rs_vec2[i] : ca.rs2, t2, g);
+      }
       if (beta) g = fma(beta[i], vvec[j], g);
       if (alpha && uvec) g = fma(alpha[i], uvec[j], g);
       a[0] += g;
@@ -1983,7 +2019,8 @@ hipError_t launch_records(const double* slab, int64_t nrow, int64_t len, const d
   double* part_r = part;
   double* part_c = part + nrow * G;
   CoincArgs ca{X, ldx, n, d, U, ldu, m, khash, kidx, K, mp, M, alpha, cg.uvec, cg.beta_in,
-               cg.vvec, cg.rs_vec, cg.rs, cg.cdiag, cflag, flag_mode};
+               cg.vvec, cg.rs_vec, cg.rs, cg.cdiag, cflag, flag_mode, cg.M2, cg.rs_vec2,
+               cg.rs2};
   hipLaunchKernelGGL(k_rec_pass1, dim3((unsigned)(nbc + nrow * G)), dim3(256), 0, s, ca,
                      (int)nbc, slab, len, G, part_r, part_c);
   hipLaunchKernelGGL(k_rec_pass2, dim3(1), dim3(256), 0, s, part_r, G, (int)nrow, part_c,
@@ -2029,25 +2066,42 @@ static void launch_con_grad(bool v2, const KernParams& kp, const double* K, cons
 }
 
 // the gradient pass over a stored product T = K M (FROM_T: no k-loop)
+template <int DT, bool T2>
+static void launch_con_from_t2(bool v2, bool kn, const KernParams& kp, const double* K,
+                               const double* M, const double* X, int64_t ldx, int64_t n,
+                               int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
+                               const ConArgs& ca, double* slab, int nrec, int64_t nwg,
+                               hipStream_t s) {
+  const dim3 g((unsigned)nwg), b(256);
+  if (v2 && kn)
+    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, true, true, true, true, T2>), g, b, 0, s, kp, K,
+                       M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
+  else if (v2)
+    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, true, false, true, true, T2>), g, b, 0, s, kp, K,
+                       M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
+  else if (kn)
+    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, false, true, true, true, T2>), g, b, 0, s, kp, K,
+                       M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
+  else
+    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, false, false, true, true, T2>), g, b, 0, s, kp,
+                       K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
+}
+
 template <int DT>
 static void launch_con_from_t(bool v2, bool kn, const KernParams& kp, const double* K,
                               const double* M, const double* X, int64_t ldx, int64_t n,
                               int64_t n_pad, const double* U, int64_t ldu, int64_t m, int64_t mp,
                               const ConArgs& ca, double* slab, int nrec, int64_t nwg,
                               hipStream_t s) {
-  const dim3 g((unsigned)nwg), b(256);
-  if (v2 && kn)
-    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, true, true, true>), g, b, 0, s, kp, K, M, X, ldx,
-                       n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
-  else if (v2)
-    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, true, false, true>), g, b, 0, s, kp, K, M, X, ldx,
-                       n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
-  else if (kn)
-    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, false, true, true>), g, b, 0, s, kp, K, M, X, ldx,
-                       n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
-  else
-    hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, false, false, true>), g, b, 0, s, kp, K, M, X,
-                       ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, (double*)nullptr);
+  if constexpr (DT == 8) {   // the two-product pass: d <= 8 only (spill-free at 246-256 VGPRs)
+    if (ca.tin2 != nullptr) {
+      launch_con_from_t2<DT, true>(v2, kn, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab,
+                                   nrec, nwg, s);
+      return;
+    }
+  }
+    launch_con_from_t2<DT, false>(v2, kn, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab,
+                                  nrec, nwg, s);
 }
 
 hipError_t launch_contract_args(const KernParams& kp, const double* K, const double* M,
@@ -2059,6 +2113,8 @@ hipError_t launch_contract_args(const KernParams& kp, const double* K, const dou
   const int nrec = kp.L + 5;
   *nrec_out = nrec;
   *nwg_out = nwg;
+  if ((ca.tin2 != nullptr) != (ca.M2 != nullptr) || (ca.tin2 && (!ca.tin || kp.d > 8)))
+    return hipErrorInvalidValue;   // the second product: beside a first, with its M, d <= 8
   if (ca.tin != nullptr) {   // stored product: no k-loop (alpha from alpha_in)
     if (ca.uvec != nullptr && ca.alpha_in == nullptr) return hipErrorInvalidValue;
     const bool v2 = ca.beta_in != nullptr, kn = ca.knot_slab != nullptr;

@@ -201,6 +201,13 @@ struct ConArgs {
   // from alpha_in; d <= 8)
   double* tstore = nullptr;
   const double* tin = nullptr;
+  // a second stored product folded into the same pass (FITC / Laplace: the K Bm^-1 and
+  // K K22^-1 gradient terms summed in one read of K): G_ij += rs2_i (K M2)_ij with
+  // rs2_i = rs2 * rs_vec2[i] (or rs2), T2 = K M2 read from tin2; M2 serves the coincidence sums
+  const double* tin2 = nullptr;
+  const double* M2 = nullptr;
+  const double* rs_vec2 = nullptr;
+  double rs2 = 0.0;
 };
 hipError_t launch_contract_args(const KernParams& kp, const double* K, const double* M,
                                 const double* X, int64_t ldx, int64_t n, int64_t n_pad,
