@@ -269,6 +269,9 @@ struct sgp_ctx {
   // sgp_eval_vi (no reduction between the phases): at m_p = 256 t's row sums leave phase 1's
   // critical path for aux_lo in phase 2 (t is first read by the m-vectors, after the Bm chain)
   bool fused_vi = false, t_deferred = false;
+  // sgp_eval_vi's phase 2: the contraction records' second pass is left to the readback kernel
+  bool defer_rec = false;
+  RecPass2 rec_defer{};
   int64_t t_rows_def = 0;
   hipEvent_t ev_t = nullptr;
   bool pack_red1 = false;                 // VI red1 carries S as packed lower 64-blocks
@@ -277,6 +280,7 @@ struct sgp_ctx {
   hipStream_t aux_lo = nullptr;           // ... at normal priority (the Bm chain keeps its CUs)
   double* slab_aux = nullptr;             // partials of the aux stream's small reductions
   double* rr_dev = nullptr;               // r^T r of the resident r (set with r)
+  double* mmpart = nullptr;               // VI's m-vector row terms (mp), read on aux_lo
   // launch-bound Bm factorisation captured once per (mp, S pointer) and replayed
   // Poisson-Laplace state (row/knot vectors allocated on first use)
   double *y = nullptr, *mu = nullptr;     // per-row data (n_pad), kept for the Laplace path
@@ -314,19 +318,7 @@ constexpr int RB_N = 256;             // pinned readback doubles at the end of c
 // memory (device-visible, hipHostMalloc) and unpacked into the caller's host arrays after one
 // synchronisation.  (Three hipMemcpyAsync D2H copies were three blit kernels plus their launch
 // gaps on the critical path of every evaluation: ~15 us at C2.)
-constexpr int RB_SEGS = 4;
-struct GatherSegs {
-  const double* src[RB_SEGS];
-  int off[RB_SEGS];   // destination offset (doubles)
-  int n[RB_SEGS];     // doubles
-  int count;
-};
-
-__global__ void __launch_bounds__(64) k_gather_host(GatherSegs g, double* __restrict__ dst) {
-  for (int q = 0; q < g.count; ++q)
-    for (int i = threadIdx.x; i < g.n[q]; i += 64) dst[g.off[q] + i] = g.src[q][i];
-  __threadfence_system();
-}
+constexpr int RB_SEGS = SGP_RB_SEGS;
 
 struct Readback {
   sgp_ctx* c;
@@ -350,8 +342,8 @@ struct Readback {
     return hipSuccess;
   }
   hipError_t wait() {
-    hipLaunchKernelGGL(k_gather_host, dim3(1), dim3(64), 0, c->stream, segs, base);
-    hipError_t e = hipGetLastError();
+    hipError_t e = launch_rec_gather(c->rec_defer, segs, base, c->stream);
+    c->rec_defer = RecPass2{};
     if (e != hipSuccess) return e;
     e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return e;
@@ -463,7 +455,7 @@ void ctx_free(sgp_ctx* c) {
                   c->Xt22,   c->T22,    c->dinv22, c->omega, c->pvec, c->rowq, c->red2f,
                   c->y,      c->mu,     c->lv,     c->lm,    c->lslab, c->lred[0], c->lred[1],
                   c->Cprev,  c->knot_slab, c->knot_part, c->knot_kmm, c->tslab, c->tq, c->tp,
-                  c->rr_dev, c->Sfull, c->gjs};
+                  c->rr_dev, c->Sfull, c->gjs, c->mmpart};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->khash) hipFree(c->khash);
@@ -834,6 +826,7 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->slab_small, c->slab_small_cap);
   st = st ? st : dalloc(&c->slab_aux, c->slab_small_cap);
   st = st ? st : dalloc(&c->rr_dev, 1);
+  st = st ? st : dalloc(&c->mmpart, mp);
   st = st ? st : dalloc(&c->sc, SC_N);
   st = st ? st : dalloc(&c->y, np_);
   st = st ? st : dalloc(&c->mu, np_);
@@ -1096,7 +1089,7 @@ static int contract_pass(sgp_ctx* c, const double* M, ConArgs ca, double* rec_ou
   HIPCHK(launch_records(c->slab_con, nrec, nwg, c->X, c->n_pad, c->n, c->kp.d, c->U, c->mp, c->m,
                         c->khash, c->kidx, c->K, c->mp, M, ca, fused ? c->alpha : ca.alpha_in,
                         c->slab_small, c->slab_small_cap, 1 + c->kp.L, rec_out, c->cflag,
-                        flags_known ? 2 : 1, c->stream));
+                        flags_known ? 2 : 1, c->stream, c->defer_rec ? &c->rec_defer : nullptr));
   c->cflag_gen = c->knots_gen;
   if (c->knot_on)
     HIPCHK(launch_knot_reduce(c->knot_slab, c->n_pad / SGP_TILE, c->mp, c->kp.d, c->knot_part,
@@ -1437,18 +1430,20 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
       c->phase = 2;
       return SGP_OK;
     }
-    // u = Binv t / z, P = tau^-2 K22inv - z^-1 Binv, t.u, tr(Binv S) and r^T r in two
-    // launches (they sit between the Bm chain and the contraction, on the critical path)
+    // u = Binv t / z, P = tau^-2 K22inv - z^-1 Binv and tr(Binv S)'s row terms in one launch
+    // between the Bm chain and the contraction (the critical path); t.u, tr(Binv S) and r^T r
+    // on aux_lo below (only the finish reads them)
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
-    HIPCHK(launch_vi_mm_vectors(c->Binv, c->K22inv, S, t, red1 + toff + mp, mp, 1.0 / z,
-                                1.0 / kp.tau2, -1.0 / z, c->uvec, c->Pm, c->slab_small,
-                                c->sc + SC_TU, c->sc + SC_TRBS, c->sc + SC_RR, c->stream));
+    HIPCHK(launch_vi_mm_rows(c->Binv, c->K22inv, S, t, mp, 1.0 / z, 1.0 / kp.tau2, -1.0 / z,
+                             c->uvec, c->Pm, c->mmpart, c->stream));
     HIPCHK(hipEventRecord(c->ev_bm, c->stream));
   }
   {
     // sum G22 o dK22/dtheta needs only m x m operands: on aux_lo beside the K12 contraction
     // (off the critical path; joined before the phase ends)
     HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_bm, 0));
+    HIPCHK(launch_vi_mm_scalars(t, c->uvec, c->mmpart, mp, red1 + toff + mp, c->sc + SC_TU,
+                                c->sc + SC_TRBS, c->sc + SC_RR, c->aux_lo));
     Scope tm(c, "contract_kmm", c->aux_lo);
     int nb = 0;
     HIPCHK(launch_contract_kmm(kp, c->U, c->mp, c->m, mp, c->uvec, c->K22inv, c->Binv, c->M3,
@@ -1545,8 +1540,14 @@ int sgp_eval_vi(sgp_ctx* c, int kernel, const double* theta, const double* U, in
   int st = sgp_vi_phase1(c, kernel, theta, U, m, ldu, delta, c->red1);
   c->fused_vi = false;
   if (st) return st;
+  c->rec_defer = RecPass2{};
+  c->defer_rec = true;   // the records' pass 2 runs in sgp_vi_finish's readback kernel
   st = sgp_vi_phase2(c, c->red1, c->n, flags, c->red2);
-  if (st) return st;
+  c->defer_rec = false;
+  if (st) {
+    c->rec_defer = RecPass2{};
+    return st;
+  }
   return sgp_vi_finish(c, c->red2, obj, grad);
 }
 

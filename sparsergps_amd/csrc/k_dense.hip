@@ -959,12 +959,17 @@ __global__ void __launch_bounds__(256) k_vi_mm_scalars(const double* __restrict_
 
 }  // namespace
 
-hipError_t launch_vi_mm_vectors(const double* Binv, const double* K22inv, const double* S,
-                                const double* t, const double* rr, int64_t mp, double invz,
-                                double a, double b, double* u, double* P, double* part,
-                                double* tu_out, double* trbs_out, double* rr_out, hipStream_t s) {
+hipError_t launch_vi_mm_rows(const double* Binv, const double* K22inv, const double* S,
+                             const double* t, int64_t mp, double invz, double a, double b,
+                             double* u, double* P, double* part, hipStream_t s) {
   hipLaunchKernelGGL(k_vi_mm_rows, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, s, Binv, K22inv,
                      S, t, mp, invz, a, b, u, P, part);
+  return hipGetLastError();
+}
+
+hipError_t launch_vi_mm_scalars(const double* t, const double* u, const double* part, int64_t mp,
+                                const double* rr, double* tu_out, double* trbs_out,
+                                double* rr_out, hipStream_t s) {
   hipLaunchKernelGGL(k_vi_mm_scalars, dim3(1), dim3(256), 0, s, t, u, part, mp, rr, tu_out,
                      trbs_out, rr_out);
   return hipGetLastError();

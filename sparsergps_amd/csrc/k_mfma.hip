@@ -1495,16 +1495,14 @@ k_rec_pass1(CoincArgs ca, int nbc, const double* __restrict__ slab, int64_t len,
 
 // Second pass (one block, fixed summation orders): rec[c] = sum_g part_r[c][g] for c < nrow,
 // and the coincidence sums added to rec[coff + 0..2].
-__global__ void __launch_bounds__(256)
-k_rec_pass2(const double* __restrict__ part_r, int G, int nrow, const double* __restrict__ part_c,
-            int nbc, int coff, double* __restrict__ rec) {
+__device__ __forceinline__ void rec_pass2_body(const RecPass2& p) {
   __shared__ double sh[3][4];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-  for (int b = tid; b < nbc; b += 256) {
-    s0 += part_c[b * 3];
-    s1 += part_c[b * 3 + 1];
-    s2 += part_c[b * 3 + 2];
+  for (int b = tid; b < p.nbc; b += 256) {
+    s0 += p.part_c[b * 3];
+    s1 += p.part_c[b * 3 + 1];
+    s2 += p.part_c[b * 3 + 2];
   }
   s0 = wave_sum(s0);
   s1 = wave_sum(s1);
@@ -1515,13 +1513,28 @@ k_rec_pass2(const double* __restrict__ part_r, int G, int nrow, const double* __
     sh[2][wv] = s2;
   }
   __syncthreads();
-  if (tid < nrow) {
+  if (tid < p.nrow) {
     double v = 0.0;
-    for (int g = 0; g < G; ++g) v += part_r[tid * G + g];
-    const int q = tid - coff;
+    for (int g = 0; g < p.G; ++g) v += p.part_r[tid * p.G + g];
+    const int q = tid - p.coff;
     if (q >= 0 && q < 3) v += sh[q][0] + sh[q][1] + sh[q][2] + sh[q][3];
-    rec[tid] = v;
+    p.rec[tid] = v;
   }
+}
+
+__global__ void __launch_bounds__(256) k_rec_pass2(RecPass2 p) { rec_pass2_body(p); }
+
+// The readback kernel (capi.hip Readback::wait): the deferred pass 2, then the segments into
+// pinned host memory (the records it just wrote among them: same workgroup, ordered by the barrier)
+__global__ void __launch_bounds__(256) k_rec_gather(RecPass2 p, GatherSegs g,
+                                                    double* __restrict__ dst) {
+  if (p.rec != nullptr) {
+    rec_pass2_body(p);
+    __syncthreads();
+  }
+  for (int q = 0; q < g.count; ++q)
+    for (int i = threadIdx.x; i < g.n[q]; i += 256) dst[g.off[q] + i] = g.src[q][i];
+  __threadfence_system();
 }
 
 // rowq[tj][i] summed over the column tiles -> out[i] (deterministic order)
@@ -2004,12 +2017,17 @@ hipError_t launch_gemm_tn(const double* A, int64_t lda, int64_t ma, const double
   return hipGetLastError();
 }
 
+hipError_t launch_rec_gather(const RecPass2& p2, const GatherSegs& g, double* dst, hipStream_t s) {
+  hipLaunchKernelGGL(k_rec_gather, dim3(1), dim3(256), 0, s, p2, g, dst);
+  return hipGetLastError();
+}
+
 hipError_t launch_records(const double* slab, int64_t nrow, int64_t len, const double* X,
                           int64_t ldx, int64_t n, int d, const double* U, int64_t ldu, int64_t m,
                           const uint64_t* khash, const int* kidx, const double* K, int64_t mp,
                           const double* M, const ConArgs& cg, const double* alpha, double* part,
                           int64_t part_cap, int coff, double* rec, uint8_t* cflag, int flag_mode,
-                          hipStream_t s) {
+                          hipStream_t s, RecPass2* defer) {
   if (nrow <= 0 || nrow > 256 || coff < 0 || coff + 3 > nrow) return hipErrorInvalidValue;
   const int G = 32;
   int64_t nbc = (n + 255) / 256;
@@ -2023,8 +2041,16 @@ hipError_t launch_records(const double* slab, int64_t nrow, int64_t len, const d
                cg.rs2};
   hipLaunchKernelGGL(k_rec_pass1, dim3((unsigned)(nbc + nrow * G)), dim3(256), 0, s, ca,
                      (int)nbc, slab, len, G, part_r, part_c);
-  hipLaunchKernelGGL(k_rec_pass2, dim3(1), dim3(256), 0, s, part_r, G, (int)nrow, part_c,
-                     (int)nbc, coff, rec);
+  RecPass2 p2;
+  p2.part_r = part_r;
+  p2.part_c = part_c;
+  p2.rec = rec;
+  p2.G = G;
+  p2.nrow = (int)nrow;
+  p2.nbc = (int)nbc;
+  p2.coff = coff;
+  if (defer != nullptr) *defer = p2;
+  else hipLaunchKernelGGL(k_rec_pass2, dim3(1), dim3(256), 0, s, p2);
   return hipGetLastError();
 }
 

@@ -253,12 +253,16 @@ hipError_t dense_spd_inverse_sum(const double* A0, double beta, const double* B0
 // C = a*A + b*B elementwise over mp x mp
 hipError_t dense_axpby(double a, const double* A, double b, const double* B, double* C,
                        int64_t count, hipStream_t s);
-// VI phase 2's m-vectors in two launches: u = invz Binv t, P = a K22inv + b Binv,
-// *tu_out = t.u, *trbs_out = tr(Binv S), *rr_out = *rr (part: mp doubles of scratch)
-hipError_t launch_vi_mm_vectors(const double* Binv, const double* K22inv, const double* S,
-                                const double* t, const double* rr, int64_t mp, double invz,
-                                double a, double b, double* u, double* P, double* part,
-                                double* tu_out, double* trbs_out, double* rr_out, hipStream_t s);
+// VI phase 2's m-vectors: the row pass u = invz Binv t, P = a K22inv + b Binv, part_j =
+// sum_k Binv_jk S_jk (part: mp doubles), and the scalars *tu_out = t.u, *trbs_out = sum part
+// (= tr(Binv S)), *rr_out = *rr (one block; only the finish reads them, so they can run on
+// another stream behind the row pass)
+hipError_t launch_vi_mm_rows(const double* Binv, const double* K22inv, const double* S,
+                             const double* t, int64_t mp, double invz, double a, double b,
+                             double* u, double* P, double* part, hipStream_t s);
+hipError_t launch_vi_mm_scalars(const double* t, const double* u, const double* part, int64_t mp,
+                                const double* rr, double* tu_out, double* trbs_out,
+                                double* rr_out, hipStream_t s);
 // y = scale * A x  (A: mp x mp row-major)
 hipError_t dense_gemv(const double* A, int64_t mp, const double* x, double scale, double* y,
                       hipStream_t s);
@@ -372,9 +376,27 @@ hipError_t launch_colnorm2(const double* K, int64_t n_pad, int64_t mp, double* p
 // coincidence sums {sum G_ij, #pairs, sum cdiag_j} over the pairs x_i == u_j added to
 // rec[coff + 0..2]; alpha = the pass's alpha_i (alpha_in, or the fused alpha written through
 // alpha_out).  part: nrow * 32 + 3 * 1024 doubles (both passes' partials).
+// With defer != nullptr the second launch is only described in *defer, for the end-of-evaluation
+// readback kernel to run first (launch_rec_gather: one launch fewer on the critical path).
+struct RecPass2 {
+  const double* part_r = nullptr;
+  const double* part_c = nullptr;
+  double* rec = nullptr;   // nullptr: nothing deferred
+  int G = 0, nrow = 0, nbc = 0, coff = 0;
+};
 hipError_t launch_records(const double* slab, int64_t nrow, int64_t len, const double* X,
                           int64_t ldx, int64_t n, int d, const double* U, int64_t ldu, int64_t m,
                           const uint64_t* khash, const int* kidx, const double* K, int64_t mp,
                           const double* M, const ConArgs& cg, const double* alpha, double* part,
                           int64_t part_cap, int coff, double* rec, uint8_t* cflag, int flag_mode,
-                          hipStream_t s);
+                          hipStream_t s, RecPass2* defer = nullptr);
+// The end-of-evaluation readback, one block: a deferred records pass 2 (p2.rec set) and then
+// dst[off[q] + i] = src[q][i] for each segment (dst: pinned host memory, device-visible).
+constexpr int SGP_RB_SEGS = 4;
+struct GatherSegs {
+  const double* src[SGP_RB_SEGS];
+  int off[SGP_RB_SEGS];   // destination offset (doubles)
+  int n[SGP_RB_SEGS];     // doubles
+  int count;
+};
+hipError_t launch_rec_gather(const RecPass2& p2, const GatherSegs& g, double* dst, hipStream_t s);
