@@ -281,6 +281,7 @@ struct sgp_ctx {
   double* slab_aux = nullptr;             // partials of the aux stream's small reductions
   double* rr_dev = nullptr;               // r^T r of the resident r (set with r)
   double* mmpart = nullptr;               // VI's m-vector row terms (mp), read on aux_lo
+  unsigned* rsync = nullptr;              // the SYRK reduction's slice tickets (kept zeroed)
   // launch-bound Bm factorisation captured once per (mp, S pointer) and replayed
   // Poisson-Laplace state (row/knot vectors allocated on first use)
   double *y = nullptr, *mu = nullptr;     // per-row data (n_pad), kept for the Laplace path
@@ -455,7 +456,7 @@ void ctx_free(sgp_ctx* c) {
                   c->Xt22,   c->T22,    c->dinv22, c->omega, c->pvec, c->rowq, c->red2f,
                   c->y,      c->mu,     c->lv,     c->lm,    c->lslab, c->lred[0], c->lred[1],
                   c->Cprev,  c->knot_slab, c->knot_part, c->knot_kmm, c->tslab, c->tq, c->tp,
-                  c->rr_dev, c->Sfull, c->gjs, c->mmpart};
+                  c->rr_dev, c->Sfull, c->gjs, c->mmpart, c->rsync};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->khash) hipFree(c->khash);
@@ -808,6 +809,11 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->gjs, 2 * SGP_GJ_SYNC_WORDS);
   if (!st && hipMemset(c->gjs, 0, sizeof(unsigned) * 2 * SGP_GJ_SYNC_WORDS) != hipSuccess) {
     set_err("hipMemset of the Gauss-Jordan sync words failed");
+    st = SGP_EHIP;
+  }
+  st = st ? st : dalloc(&c->rsync, SGP_SYRK_RSYNC_WORDS);
+  if (!st && hipMemset(c->rsync, 0, sizeof(unsigned) * SGP_SYRK_RSYNC_WORDS) != hipSuccess) {
+    set_err("hipMemset of the SYRK reduction tickets failed");
     st = SGP_EHIP;
   }
   st = st ? st : dalloc(&c->logd22, mp / SGP_DB);
@@ -1285,7 +1291,8 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
     // S into red1, and r^T r (the context's constant; the 7 words past it zeroed)
     Scope t(c, "syrk_reduce");
     HIPCHK(launch_syrk_aug(c->K, c->n_pad, mpv, c->r, nullptr, c->slab_syrk, c->slab_syrk_cap,
-                           red1, c->stream, 2, nullptr, 0, c->rr_dev, c->pack_red1));
+                           red1, c->stream, 2, nullptr, 0, c->rr_dev, c->pack_red1, false,
+                           c->rsync));
   }
   // K22's inverse (aux) is queued behind the SYRK here rather than in phase 2: it needs only
   // theta and U, so with several ranks it runs while the first all-reduce is in flight (the
@@ -1354,14 +1361,17 @@ static int k22_launch(sgp_ctx* c, double diag_sub) {
 
 // Binv = (K22 + S * s_scale)^-1 (one Gauss-Jordan launch per pivot; the sum is formed by the
 // chain's first pivot and step as they read K22 and S)
-static int bm_stage(sgp_ctx* c, const double* S, double s_scale, bool k22_ordered = false) {
+// logdet_later: the caller sums the pivots' log-determinants itself (VI: on aux_lo, where only
+// the finish waits for it, instead of one more launch between the chain and the m-vectors)
+static int bm_stage(sgp_ctx* c, const double* S, double s_scale, bool k22_ordered = false,
+                    bool logdet_later = false) {
   const int64_t mp = c->mp;
   Scope t(c, "dense_bm");
   if (!k22_ordered)   // Bm needs K22, not its inverse (VI: ordered through phase 1's ev_lo)
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22m, 0));
   HIPCHK(dense_spd_inverse_sum(c->K22, s_scale, S, c->Binv, mp, c->Xt, c->dinv, c->logdB,
                                c->status + 1, c->gjs, c->stream));
-  HIPCHK(launch_sum_small(c->logdB, mp / SGP_DB, c->sc + SC_LDB, c->stream));
+  if (!logdet_later) HIPCHK(launch_sum_small(c->logdB, mp / SGP_DB, c->sc + SC_LDB, c->stream));
   return SGP_OK;
 }
 
@@ -1390,7 +1400,8 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
   // chain at C2 (kernel trace)
   HIPCHK(hipEventRecord(c->ev_s, c->stream));   // S (red1, summed) is ready
   // K22's build ordered by phase 1's ev_lo (or waited for here when phase 1 had no side work)
-  int st = bm_stage(c, S, 1.0 / z, c->vi_k22_ordered);
+  const bool obj_only = (flags & SGP_FLAG_OBJ_ONLY) != 0;
+  int st = bm_stage(c, S, 1.0 / z, c->vi_k22_ordered, !obj_only);
   if (st) return st;
   {
     // tr(K22inv S) and M3 = K22inv S K22inv need S and K22inv only: on aux_lo beside the Bm
@@ -1444,6 +1455,7 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
     HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_bm, 0));
     HIPCHK(launch_vi_mm_scalars(t, c->uvec, c->mmpart, mp, red1 + toff + mp, c->sc + SC_TU,
                                 c->sc + SC_TRBS, c->sc + SC_RR, c->aux_lo));
+    HIPCHK(launch_sum_small(c->logdB, mp / SGP_DB, c->sc + SC_LDB, c->aux_lo));   // bm_stage's
     Scope tm(c, "contract_kmm", c->aux_lo);
     int nb = 0;
     HIPCHK(launch_contract_kmm(kp, c->U, c->mp, c->m, mp, c->uvec, c->K22inv, c->Binv, c->M3,

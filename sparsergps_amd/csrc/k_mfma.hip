@@ -615,6 +615,73 @@ k_syrk_reduce_blk(const double* __restrict__ slab, int splits, int64_t nblk, int
   red[b * mp + a] = v;
 }
 
+// k_syrk_reduce_grp and k_syrk_reduce_blk in one launch (one slab region, splits > SYRK_RGRP):
+// group g of a 256-element slice sums its SYRK_RGRP slabs as k_syrk_reduce_grp does and stores
+// the total write-through (sc1); the slice's last group to finish (a ticket per slice,
+// rsync[bid * 16 + x]) sums the group totals in group order -- the same order and values as
+// k_syrk_reduce_blk -- and resets the ticket.  Nothing waits on another workgroup.
+__global__ void __launch_bounds__(256)
+k_syrk_reduce_last(double* __restrict__ slab, int splits, int64_t nblk, int64_t mp,
+                   double* __restrict__ red, const double* __restrict__ rr_src,
+                   double* __restrict__ rr_dst, int packed, unsigned* __restrict__ rsync) {
+  const int64_t bid = blockIdx.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int ng = (int)gridDim.z;
+  const int s0 = blockIdx.z * SYRK_RGRP;
+  const int s1 = s0 + SYRK_RGRP < splits ? s0 + SYRK_RGRP : splits;
+  double a[SYRK_RGRP];
+#pragma unroll
+  for (int q = 0; q < SYRK_RGRP; ++q)
+    a[q] = s0 + q < s1 ? slab[((int64_t)(s0 + q) * nblk + bid) * 4096 + e] : 0.0;
+  double v = 0.0;
+#pragma unroll
+  for (int q = 0; q < SYRK_RGRP; ++q)
+    if (s0 + q < s1) v += a[q];
+  __hip_atomic_store(slab + ((int64_t)s0 * nblk + bid) * 4096 + e, v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's totals have landed
+  __syncthreads();
+  __shared__ int s_last;
+  unsigned* tk = rsync + bid * 16 + blockIdx.x;
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (int)(t == (unsigned)(ng - 1));
+    if (s_last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (rr_src && bid == 0 && e < 8) rr_dst[e] = e == 0 ? *rr_src : 0.0;
+  int rp = (int)((sqrtf(8.0f * (float)bid + 1.0f) - 1.0f) * 0.5f);
+  while ((int64_t)(rp + 1) * (rp + 2) / 2 <= bid) ++rp;
+  while ((int64_t)rp * (rp + 1) / 2 > bid) --rp;
+  const int cp = (int)(bid - (int64_t)rp * (rp + 1) / 2);
+  // which elements write, as in k_syrk_reduce_blk
+  const bool upper = rp == cp && (e / 64) / 16 < (e % 64) / 16;
+  if (upper && !packed) return;
+  if (!packed && rp == cp && (e / 64) < (e % 64)) return;
+  double t = 0.0;
+  if (!upper)
+    for (int g0 = 0; g0 < ng; g0 += 16) {   // 16 loads in flight, summed in group order
+      double b[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        b[q] = g0 + q < ng ? __hip_atomic_load(slab + ((int64_t)(g0 + q) * SYRK_RGRP * nblk +
+                                                       bid) * 4096 + e,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (g0 + q < ng) t += b[q];
+    }
+  if (packed) {
+    red[bid * 4096 + e] = t;
+    return;
+  }
+  const int64_t ra = (int64_t)rp * 64 + e / 64, rb = (int64_t)cp * 64 + e % 64;
+  red[ra * mp + rb] = t;
+  red[rb * mp + ra] = t;
+}
+
 // Full symmetric S (mp x mp) from its packed lower 64-blocks (k_syrk_reduce_blk, packed): an
 // element on or below the diagonal is read as stored, the rest from its mirror.
 __global__ void __launch_bounds__(256)
@@ -1860,7 +1927,7 @@ int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp) {
 hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const double* r,
                            const double* w, double* slab, int64_t slab_cap, double* red,
                            hipStream_t s, int part, const double* tv, int with_t,
-                           const double* rr_src, bool packed, bool w_nonneg) {
+                           const double* rr_src, bool packed, bool w_nonneg, unsigned* rsync) {
   if (packed && with_t) return hipErrorInvalidValue;   // the packed layout is VI's (no t)
   {   // the packed 64-block kernel (no redundant diagonal-tile halves), or at mp = 256 the
       // fragment-balanced k_syrk_s256 (same slab layout and reduction)
@@ -1953,6 +2020,16 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
       // many splits (small m): a first pass sums groups of SYRK_RGRP slabs in parallel, the
       // final pass then sums the group totals (fixed order either way: deterministic)
       int stride = 1, stride_d = 1;
+      if (rsync && !bal.on && q.splits > SYRK_RGRP && nblk * 16 <= SGP_SYRK_RSYNC_WORDS) {
+        const unsigned ng = (unsigned)((q.splits + SYRK_RGRP - 1) / SYRK_RGRP);
+        hipLaunchKernelGGL(k_syrk_reduce_last, dim3(4096 / 256, (unsigned)nblk, ng), dim3(256),
+                           0, s, sl_s, q.splits, nblk, mp, red, rr_src,
+                           red + (packed ? nblk * 4096 : mp * mp) + mp, packed ? 1 : 0, rsync);
+        if (with_t)
+          hipLaunchKernelGGL(k_syrk_reduce_t, dim3((unsigned)((mp + 255) / 256)), dim3(256), 0, s,
+                             sl_t, sl_rr, t_splits, q.nb, mp, red);
+        return hipGetLastError();
+      }
       if (q.splits > SYRK_RGRP) {
         const unsigned ng = (unsigned)((q.splits + SYRK_RGRP - 1) / SYRK_RGRP);
         hipLaunchKernelGGL(k_syrk_reduce_grp, dim3(4096 / 256, (unsigned)nblk, ng), dim3(256), 0,

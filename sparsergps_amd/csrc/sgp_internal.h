@@ -162,7 +162,12 @@ hipError_t launch_syrk_aug(const double* K, int64_t n_pad, int64_t mp, const dou
                            int with_t = 1,               // 0: S only (red[mm..] untouched)
                            const double* rr_src = nullptr,    // part 2: copy *rr_src to rr's slot
                            bool packed = false,    // part 2: S as its packed lower 64-blocks
-                           bool w_nonneg = false);   // w >= 0: sqrt(w) scales the staged rows
+                           bool w_nonneg = false,  // w >= 0: sqrt(w) scales the staged rows
+                           // part 2, many splits, one slab region: the two reduction passes in
+                           // one launch (the last group of each 256-element slice sums the group
+                           // totals); SGP_SYRK_RSYNC_WORDS zeroed words, left zeroed
+                           unsigned* rsync = nullptr);
+#define SGP_SYRK_RSYNC_WORDS 4096
 // doubles of S's packed lower 64-blocks, and the full S from them (sgp_ctx_set_packed_reduction)
 int64_t syrk_packed_doubles(int64_t mp);
 hipError_t launch_unpack_lower64(const double* packed, int64_t mp, double* S, hipStream_t s);
