@@ -13,6 +13,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <string>
@@ -321,6 +322,19 @@ constexpr int RB_N = 256;             // pinned readback doubles at the end of c
 // gaps on the critical path of every evaluation: ~15 us at C2.)
 constexpr int RB_SEGS = SGP_RB_SEGS;
 
+#ifdef SGP_HOST_PROBE
+// host time of sgp_eval_vi: entry -> the readback's synchronisation (issue) and the wait in it;
+// averages printed to stderr every 200 evaluations (variant builds only)
+static double hp_now() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+static double hp_t0 = 0.0, hp_issue = 0.0, hp_wait = 0.0, hp_tail = 0.0, hp_prev_end = 0.0,
+              hp_gap = 0.0;
+static long hp_n = 0;
+#endif
+
 struct Readback {
   sgp_ctx* c;
   double* base;
@@ -346,7 +360,18 @@ struct Readback {
     hipError_t e = launch_rec_gather(c->rec_defer, segs, base, c->stream);
     c->rec_defer = RecPass2{};
     if (e != hipSuccess) return e;
+#ifdef SGP_HOST_PROBE
+    const double t1 = hp_now();
+#endif
     e = hipStreamSynchronize(c->stream);
+#ifdef SGP_HOST_PROBE
+    const double t2 = hp_now();
+    if (hp_t0 > 0.0) {
+      hp_issue += t1 - hp_t0;
+      hp_wait += t2 - t1;
+      hp_tail = t2;
+    }
+#endif
     if (e != hipSuccess) return e;
     for (const Item& it : items) memcpy(it.host, base + it.off, it.bytes);
     return hipSuccess;
@@ -1548,6 +1573,10 @@ int sgp_eval_vi(sgp_ctx* c, int kernel, const double* theta, const double* U, in
                 int64_t ldu, double delta, unsigned flags, double* obj, double* grad) {
   MULTI_FWD(c, obj && (grad || (flags & SGP_FLAG_OBJ_ONLY)) ? multi_eval_vi(c->multi, kernel, theta, U, m, ldu, delta, flags, obj, grad) : multi_bad_args());
   if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
+#ifdef SGP_HOST_PROBE
+  hp_t0 = hp_now();
+  if (hp_prev_end > 0.0) hp_gap += hp_t0 - hp_prev_end;
+#endif
   c->fused_vi = true;   // nothing reduces red1 between the phases
   int st = sgp_vi_phase1(c, kernel, theta, U, m, ldu, delta, c->red1);
   c->fused_vi = false;
@@ -1560,7 +1589,23 @@ int sgp_eval_vi(sgp_ctx* c, int kernel, const double* theta, const double* U, in
     c->rec_defer = RecPass2{};
     return st;
   }
+#ifdef SGP_HOST_PROBE
+  const int fst = sgp_vi_finish(c, c->red2, obj, grad);
+  const double t3 = hp_now();
+  hp_prev_end = t3;
+  hp_tail = t3 - hp_tail;
+  static double tail_sum = 0.0;
+  tail_sum += hp_tail;
+  if (++hp_n % 200 == 0) {
+    fprintf(stderr, "[host probe] %ld evals: issue %.1f us, sync wait %.1f us, after sync %.1f us, "
+            "caller gap %.1f us per eval\n", hp_n, 1e6 * hp_issue / 200, 1e6 * hp_wait / 200,
+            1e6 * tail_sum / 200, 1e6 * hp_gap / 200);
+    hp_issue = hp_wait = hp_gap = tail_sum = 0.0;
+  }
+  return fst;
+#else
   return sgp_vi_finish(c, c->red2, obj, grad);
+#endif
 }
 
 // ------------------------------------------------------------------------- FITC phases

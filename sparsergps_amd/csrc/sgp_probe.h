@@ -43,7 +43,7 @@
      defined(SGP_SYRK_W3) || defined(SGP_CON_ROWQ_KU) ||                                      \
      defined(SGP_LAP_RS_CFG) || defined(SGP_GJ_MM_UNROLL) || defined(SGP_VI_BUILD_NO_T) ||        \
      defined(SGP_GJ_STEPS) || defined(SGP_GJ_GMAX) || defined(SGP_CHAIN_US_STEP) ||         \
-     defined(SGP_CHAIN_US_FIX)) &&                                 \
+     defined(SGP_CHAIN_US_FIX) || defined(SGP_HOST_PROBE)) &&      \
     !defined(SGP_PROBE_BUILD)
 #error "timing probes and experiment knobs are for variant builds only (SGP_PROBE_BUILD)"
 #endif
