@@ -21,6 +21,12 @@
 
 #include "../../include/sgp.h"
 #include "sgp_internal.h"
+
+#ifdef SGP_HOST_PROBE
+// entry, before the readback's synchronisation, after it, exit of the last sgp_eval_vi
+// (CLOCK_MONOTONIC seconds: Python's time.perf_counter reads the same clock)
+extern "C" __attribute__((visibility("default"))) double sgp_probe_t[4] = {0.0, 0.0, 0.0, 0.0};
+#endif
 #include "sgp_probe.h"
 #include "sgp_multi.h"
 
@@ -362,10 +368,12 @@ struct Readback {
     if (e != hipSuccess) return e;
 #ifdef SGP_HOST_PROBE
     const double t1 = hp_now();
+    sgp_probe_t[1] = t1;
 #endif
     e = hipStreamSynchronize(c->stream);
 #ifdef SGP_HOST_PROBE
     const double t2 = hp_now();
+    sgp_probe_t[2] = t2;
     if (hp_t0 > 0.0) {
       hp_issue += t1 - hp_t0;
       hp_wait += t2 - t1;
@@ -1575,6 +1583,7 @@ int sgp_eval_vi(sgp_ctx* c, int kernel, const double* theta, const double* U, in
   if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
 #ifdef SGP_HOST_PROBE
   hp_t0 = hp_now();
+  sgp_probe_t[0] = hp_t0;
   if (hp_prev_end > 0.0) hp_gap += hp_t0 - hp_prev_end;
 #endif
   c->fused_vi = true;   // nothing reduces red1 between the phases
@@ -1592,6 +1601,7 @@ int sgp_eval_vi(sgp_ctx* c, int kernel, const double* theta, const double* U, in
 #ifdef SGP_HOST_PROBE
   const int fst = sgp_vi_finish(c, c->red2, obj, grad);
   const double t3 = hp_now();
+  sgp_probe_t[3] = t3;
   hp_prev_end = t3;
   hp_tail = t3 - hp_tail;
   static double tail_sum = 0.0;

@@ -142,31 +142,36 @@ class SparseGPContext:
     def _flags(r_det, obj_only):
         return (_lib.SGP_FLAG_R_DET if r_det else 0) | (_lib.SGP_FLAG_OBJ_ONLY if obj_only else 0)
 
+    # sgp_eval_vi / sgp_eval_fitc called with raw addresses: an optimizer calls them once per
+    # step, and at C2 (~0.6 ms per evaluation) ctypes' pointer objects were ~4 us of it
+    _EVAL_PROTO = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int64,
+                              C.c_int64, C.c_double, C.c_uint, C.c_void_p, C.c_void_p)
+
+    def _eval_fast(self, name, theta, cov_fun, xu, delta, r_det, obj_only):
+        fns = self.__dict__.setdefault("_fast_fns", {})
+        fn = fns.get(name)
+        if fn is None:
+            fn = fns[name] = self._EVAL_PROTO(C.cast(getattr(self._lib, name), C.c_void_p).value)
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        if theta.ndim != 1:
+            theta = theta.reshape(-1)
+        U, m = self._knots(xu)
+        out = np.zeros(theta.size + 1, dtype=np.float64)   # [objective, gradient]
+        a = out.ctypes.data
+        st = fn(self.handle.value, _lib.KERNELS[cov_fun], theta.ctypes.data, U.ctypes.data, m, m,
+                float(delta), self._flags(r_det, obj_only), a, None if obj_only else a + 8)
+        _lib.check(st)
+        return float(out[0]), (None if obj_only else out[1:])
+
     def eval_vi(self, theta, cov_fun, xu, delta=1e-6, r_det=False, obj_only=False):
         """ELBO and d ELBO / d log(theta) with theta in [sigma, l.., tau] layout
         (obj_only: elbo_fun alone, grad None)."""
-        theta = np.ascontiguousarray(theta, dtype=np.float64)
-        U, m = self._knots(xu)
-        obj = C.c_double(0.0)
-        grad = None if obj_only else np.zeros(theta.size, dtype=np.float64)
-        st = self._lib.sgp_eval_vi(self.handle, _lib.KERNELS[cov_fun], _lib.dptr(theta),
-                                   _lib.dptr(U), m, m, float(delta), self._flags(r_det, obj_only),
-                                   C.byref(obj), None if grad is None else _lib.dptr(grad))
-        _lib.check(st)
-        return obj.value, grad
+        return self._eval_fast("sgp_eval_vi", theta, cov_fun, xu, delta, r_det, obj_only)
 
     def eval_fitc(self, theta, cov_fun, xu, delta=1e-6, r_det=False, obj_only=False):
         """FITC log marginal likelihood and d/d log(theta) (obj_fun_norm + dlogp_dcov_par;
         obj_only: obj_fun_norm alone, grad None)."""
-        theta = np.ascontiguousarray(theta, dtype=np.float64)
-        U, m = self._knots(xu)
-        obj = C.c_double(0.0)
-        grad = None if obj_only else np.zeros(theta.size, dtype=np.float64)
-        st = self._lib.sgp_eval_fitc(self.handle, _lib.KERNELS[cov_fun], _lib.dptr(theta),
-                                     _lib.dptr(U), m, m, float(delta), self._flags(r_det, obj_only),
-                                     C.byref(obj), None if grad is None else _lib.dptr(grad))
-        _lib.check(st)
-        return obj.value, grad
+        return self._eval_fast("sgp_eval_fitc", theta, cov_fun, xu, delta, r_det, obj_only)
 
     def eval_full(self, theta, cov_fun, delta=1e-6, obj_only=False):
         """Full Gaussian GP over this context's rows (m_max >= n): log dmvnorm(y; mu, Sigma11)
