@@ -1445,9 +1445,11 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
                            // sgp_eval_vi does, whose red1 is the context's own)
       HIPCHK(launch_knot_reduce(c->tslab, c->t_rows_def, mp, 1, c->T1, c->mp_max * c->mp_max,
                                 c->red1 + toff, false, c->aux_lo));
-      HIPCHK(hipEventRecord(c->ev_t, c->aux_lo));
     }
     HIPCHK(hipStreamWaitEvent(c->aux_lo, c->ev_k22, 0));
+    // ev_t: t summed AND K22's inverse done -- the m-vectors then wait on one event, not two
+    // (each cross-stream wait in front of them cost the critical path several us at C2)
+    if (c->t_deferred) HIPCHK(hipEventRecord(c->ev_t, c->aux_lo));
     Scope ta(c, "m3_aux", c->aux_lo);
     HIPCHK(launch_dot(c->K22inv, S, mm, c->slab_aux, c->sc + SC_TRKS, c->aux_lo));
     if (!(flags & SGP_FLAG_OBJ_ONLY)) {
@@ -1461,6 +1463,7 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
   }
   {
     Scope tm(c, "mm_vectors");
+    const bool k22_via_t = c->t_deferred;   // ev_t covers K22's inverse too
     if (c->t_deferred) {
       HIPCHK(hipStreamWaitEvent(c->stream, c->ev_t, 0));
       c->t_deferred = false;
@@ -1477,7 +1480,7 @@ int sgp_vi_phase2(sgp_ctx* c, const double* red1, int64_t n_global, unsigned fla
     // u = Binv t / z, P = tau^-2 K22inv - z^-1 Binv and tr(Binv S)'s row terms in one launch
     // between the Bm chain and the contraction (the critical path); t.u, tr(Binv S) and r^T r
     // on aux_lo below (only the finish reads them)
-    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
+    if (!k22_via_t) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_k22, 0));
     HIPCHK(launch_vi_mm_rows(c->Binv, c->K22inv, S, t, mp, 1.0 / z, 1.0 / kp.tau2, -1.0 / z,
                              c->uvec, c->Pm, c->mmpart, c->stream));
     HIPCHK(hipEventRecord(c->ev_bm, c->stream));
