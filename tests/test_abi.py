@@ -151,3 +151,21 @@ def test_multi_context_argument_validation(lib):
         assert h.value is None
     ns, nd = C.c_int(0), C.c_int(0)
     assert lib.sgp_ctx_shards(None, C.byref(ns), C.byref(nd)) == _lib.SGP_EINVAL
+
+
+def test_fast_eval_prototype_matches_the_table():
+    """SparseGPContext.eval_vi / eval_fitc call sgp_eval_vi / sgp_eval_fitc through a raw-address
+    CFUNCTYPE: same return type and argument count and kinds as the checked prototype table
+    (pointers as c_void_p, scalars identical)."""
+    from sparsergps_amd import _lib
+    from sparsergps_amd.vi import SparseGPContext
+    proto = SparseGPContext._EVAL_PROTO
+    for name in ("sgp_eval_vi", "sgp_eval_fitc"):
+        res, args = _lib.PROTOTYPES[name]
+        assert proto._restype_ is res
+        assert len(proto._argtypes_) == len(args)
+        for fast, ref in zip(proto._argtypes_, args):
+            if fast is C.c_void_p:
+                assert ref is C.c_void_p or issubclass(ref, C._Pointer), (name, ref)
+            else:
+                assert fast is ref, (name, fast, ref)
