@@ -1,6 +1,6 @@
 # round 5 closing: GPU suite on HEAD, default bench line, rocprofv3 kernel stats, mode lines
 set -o pipefail
-D=gpurun_out/r5final4
+D=gpurun_out/r5final5
 mkdir -p $D
 timeout -k 10 1100 python -u -m pytest --maxfail=5 -v -s --timeout 300 --timeout-method thread -m gpu tests/ > $D/suite.log 2>&1 || { tail -30 $D/suite.log; exit 1; }
 tail -1 $D/suite.log
