@@ -4,12 +4,16 @@
 One step = one full evaluation of the reference's optimizer-iteration body
 (norm_grad_ascent_vi, R/vi_functions.R:1089-1128): build K12/K22 at (theta, U), the Titsias
 ELBO and its gradient w.r.t. all P = 10 log-hyperparameters (knots fixed), on synthetic C3
-inputs already resident in HBM.  N > 1: the n rows are split into N contiguous blocks (C4),
-one process per GPU, RCCL all-reduce of the two reduction buffers (sparsergps_amd/dist.py);
-total work is fixed, so scaling is "strong".
+inputs already resident in HBM.  N > 1: the n rows are split into N contiguous blocks (C4)
+and the two reduction buffers are all-reduced over RCCL; total work is fixed, so scaling is
+"strong".  --gpus N always means N GPUs (plan_run):
+  * under torch.distributed.run (RANK in the environment): one process per GPU
+    (sparsergps_amd/dist.py); --gpus must equal WORLD_SIZE;
+  * without it and N > 1: one process over devices 0..N-1 through the in-library multi-device
+    context (sgp_ctx_create_multi, RCCL inside libsgp) -- the path the R drop-in takes;
+  * N larger than the visible devices, or < 1, is an error: never a silent one-GPU run.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N > 1 under torch.distributed.run, one rank per GPU)
 """
 from __future__ import annotations
 
@@ -181,20 +185,41 @@ def cpu_baseline_full(n_target=1_000_000, m=1024):
             "adjoint_direct": adjoint_direct(n_target, m)}
 
 
-def kernel_rooflines(mode, phase_avg, n_loc, m):
+def store_ceiling(n_loc, m, device=0):
+    """This box's HBM store ceiling for the K12 builder, measured in the same run
+    (sgp_diag_store_bw: plain 16-byte non-temporal stores in the builder's 4-row x 256 B shape
+    over the builder's byte count, best of 5 passes).  None when it cannot be measured."""
+    import ctypes as C
+
+    from sparsergps_amd import _lib
+    n_pad = -(-n_loc // 128) * 128
+    m_p = -(-m // 128) * 128
+    gbs = C.c_double(0.0)
+    st = _lib.lib().sgp_diag_store_bw(device, int(8 * n_pad * m_p), 5, 1, C.byref(gbs))
+    return gbs.value if st == _lib.SGP_OK and gbs.value > 0 else None
+
+
+def kernel_rooflines(mode, phase_avg, n_loc, m, ceiling=None):
     """The other hot kernels of the step against their own bounds (same HIP-event phase
     timings as roofline.achieved): the K12 builder writes 8 B per (row, knot) pair of the
-    padded n_pad x m_p matrix (HBM-write bound); the SYRK does n m^2 algorithmic flops
-    (fp64 MFMA bound)."""
+    padded n_pad x m_p matrix (HBM-write bound; also against `ceiling`, this box's measured
+    store rate); the SYRK does n m^2 algorithmic flops (fp64 MFMA bound)."""
     n_pad = -(-n_loc // 128) * 128
     m_p = -(-m // 128) * 128
     out = []
     t = phase_avg.get("build_knm", 0.0) * 1e-3
     if t > 0:
         gbs = 8.0 * n_pad * m_p / t / 1e9
-        out.append({"kernel": "build_knm (k_build_knm_mfma)", "bound": "hbm", "achieved": gbs,
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
-                    "bytes_per_launch": 8.0 * n_pad * m_p})
+        row = {"kernel": "build_knm (k_build_knm_mfma)", "bound": "hbm", "achieved": gbs,
+               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+               "bytes_per_launch": 8.0 * n_pad * m_p}
+        if ceiling:
+            row["store_ceiling_gbs"] = ceiling
+            row["frac_of_store_ceiling"] = gbs / ceiling
+            row["store_ceiling_note"] = ("sgp_diag_store_bw on this box in this run: plain "
+                                         "non-temporal 16-byte stores, the builder's shape and "
+                                         "byte count, best of 5")
+        out.append(row)
     key = {"vi": "syrk", "fitc": "syrk", "laplace": "syrk_z"}.get(mode)
     t = phase_avg.get(key, 0.0) * 1e-3
     if t > 0:
@@ -203,6 +228,53 @@ def kernel_rooflines(mode, phase_avg, n_loc, m):
                     "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": tf / FP64_MFMA_PEAK_TFLOPS, "flops_per_launch": float(n_loc) * m * m})
     return out
+
+
+class PlanError(ValueError):
+    """bench.py's --gpus / --devices / launcher combination cannot run as asked."""
+
+
+def plan_run(gpus, devices, env, visible):
+    """How `bench.py --gpus N` runs.  Returns ("torchrun", world) when launched by
+    torch.distributed.run (RANK in env), ("library", device list) for the in-library
+    multi-device context, or ("single", [0]).  `visible` is a callable giving the visible GPU
+    count (only asked when needed).  Raises PlanError for every request that would otherwise
+    time a different number of GPUs than N."""
+    if gpus < 1:
+        raise PlanError(f"--gpus {gpus}: at least one GPU")
+    under_torchrun = "RANK" in env
+    world = int(env.get("WORLD_SIZE", "1"))
+    if devices is not None:
+        if under_torchrun or world > 1:
+            raise PlanError("--devices runs one process over several devices (not under "
+                            "torchrun)")
+        if not devices:
+            raise PlanError("--devices: empty list")
+        distinct = len(set(devices))
+        if gpus != 1 and gpus != distinct:
+            raise PlanError(f"--gpus {gpus} but --devices names {distinct} distinct device(s)")
+        nvis = visible()
+        bad = [dv for dv in devices if dv < 0 or dv >= nvis]
+        if bad:
+            raise PlanError(f"--devices {bad}: {nvis} device(s) visible")
+        return "library", list(devices)
+    if under_torchrun:
+        if gpus != world:
+            raise PlanError(f"--gpus {gpus} but torchrun started WORLD_SIZE={world} rank(s)")
+        return "torchrun", world
+    if world > 1:
+        raise PlanError(f"WORLD_SIZE={world} without RANK: launch with torch.distributed.run")
+    if gpus == 1:
+        return "single", [0]
+    nvis = visible()
+    if gpus > nvis:
+        raise PlanError(f"--gpus {gpus} but only {nvis} device(s) are visible")
+    return "library", list(range(gpus))
+
+
+def _visible_gpus():
+    import torch
+    return torch.cuda.device_count()
 
 
 def main():
@@ -248,10 +320,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.devices is not None:
-        if world > 1 or "RANK" in os.environ:
-            ap.error("--devices runs one process over several devices (not under torchrun)")
-        return bench_library_shards(args, [int(v) for v in args.devices.split(",")])
+    try:
+        devs = None if args.devices is None else [int(v) for v in args.devices.split(",") if v]
+        kind, what = plan_run(args.gpus, devs, os.environ, _visible_gpus)
+    except (PlanError, ValueError) as e:
+        ap.error(str(e))
+    if kind == "library":
+        return bench_library_shards(args, what)
 
     import torch
     import torch.distributed as dist
@@ -409,7 +484,8 @@ def main():
                          "traffic": traffic if args.mode == "vi" else None,
                          "kernel": con_key + (" (k_contract<8>)" if d <= 8 else " (k_contract<32>)"),
                          "flops_per_launch": flops},
-            "kernel_rooflines": kernel_rooflines(args.mode, phase_avg, n_loc, m),
+            "kernel_rooflines": kernel_rooflines(args.mode, phase_avg, n_loc, m,
+                                                 store_ceiling(n_loc, m, dev_index)),
             "phases_ms": {k: round(v, 4) for k, v in phase_avg.items()},
             "phases_note": "HIP-event phase times from 3 evaluations after the timed steps "
                            "(inside the timed steps only the roofline kernel's phase is timed)",
@@ -441,11 +517,13 @@ def main():
 
 
 def bench_library_shards(args, devices):
-    """The in-library multi-device context: the rows split into len(devices) shards, each
-    evaluation's reductions summed on the devices and over them by RCCL inside libsgp (one host
-    worker thread per distinct device).  With every shard on one GPU (e.g. --devices
-    0,0,0,0,0,0,0,0) this times C4's eight-way composition on a one-GPU box; on a node,
-    --devices 0,1,...,7 is the R drop-in's 8-GPU path."""
+    """`--gpus N` without torchrun (devices 0..N-1) or `--devices LIST`: the in-library
+    multi-device context.  The rows are split into len(devices) shards, each evaluation's
+    reductions summed on the devices and over them by RCCL inside libsgp (one host worker
+    thread per distinct device).  With every shard on one GPU (e.g. --devices 0,0,0,0,0,0,0,0)
+    this times C4's eight-way composition on a one-GPU box; on a node, --gpus 8 is the R
+    drop-in's 8-GPU path.  The line carries the same roofline / kernel_rooflines fields as the
+    one-GPU line, for shard 0's kernels."""
     import torch
 
     import sparsergps_amd as S
@@ -460,6 +538,8 @@ def bench_library_shards(args, devices):
     U = np.asfortranarray(P["U"])
     if args.mode == "laplace":
         ctx.lap_set_f(P["f0"])
+    del P["X"]
+    nr_iters = []
 
     def run(k):
         th = theta0 * np.exp(1e-3 * np.sin(np.arange(theta0.size) + k))
@@ -467,7 +547,8 @@ def bench_library_shards(args, devices):
             return ctx.eval_vi(th, cov_fun, U, P["delta"])
         if args.mode == "fitc":
             return ctx.eval_fitc(th, cov_fun, U, P["delta"])
-        o, g, _ = ctx.eval_laplace(th, cov_fun, U, P["delta"], P["a"], args.tol_nr, 1000)
+        o, g, it = ctx.eval_laplace(th, cov_fun, U, P["delta"], P["a"], args.tol_nr, 1000)
+        nr_iters.append(it)
         return o, g
 
     for k in range(args.warmup):
@@ -486,28 +567,61 @@ def bench_library_shards(args, devices):
     elapsed = time.perf_counter() - t0
     evals = max(ctx.timing_evals(), 1)
     t_con = dict(ctx.timings()).get(con_key, float("nan")) / evals * 1e-3
+    # per-phase times of shard 0 from a short untimed pass (as the one-GPU line)
+    ctx.timing_filter(None)
+    ctx.enable_timing(True)
+    for k in range(min(args.steps, 3)):
+        run(args.warmup + args.steps + k)
+    for dv in sorted(set(devices)):
+        torch.cuda.synchronize(dv)
+    pevals = max(ctx.timing_evals(), 1)
+    phase_avg = {name: ms / pevals for name, ms in ctx.timings()}
     ctx.enable_timing(False)
     n0 = shard_rows(n, nshards, 0)[1]
     flops = 2.0 * n0 * m * m
     achieved = flops / t_con / 1e12 if t_con > 0 else float("nan")
+    traffic = None
+    tp = os.path.join(ROOT, "profiles", "pmc_traffic_contract_knm.json")
+    if args.mode == "vi" and os.path.exists(tp):
+        try:
+            rec = json.load(open(tp))
+            if rec.get("n") == n0 and rec.get("m") == m:
+                traffic = rec.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
     metric = {"vi": "sparse-GP objective+gradient evals/sec at n=1e6, m=1024, d=8",
               "fitc": "FITC objective+gradient evals/sec (secondary mode)",
               "laplace": "Poisson sparse-Laplace NR+objective+gradient evals/sec (C5, secondary)"}
+    if args.mode == "vi" and (n, m, d) != (1_000_000, 1024, 8):
+        metric["vi"] = f"sparse-GP objective+gradient evals/sec at n={n}, m={m}, d={d}"
     out = {"metric": metric[args.mode], "value": args.steps / elapsed, "unit": "evals/s",
            "n_gpus": ndev, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
            "data": f"synthetic (SURVEY.md 8(d) {args.config} generator, numpy PCG64)",
-           "config": {"workload": f"{args.config} {args.mode}, n={n}, m={m}, d={d}, {cov_fun}",
+           "config": {"workload": f"{args.config} {args.mode}, n={n}, m={m}, d={d}, {cov_fun}, "
+                                  f"P={len(names)}, knots fixed",
                       "n": n, "m": m, "d": d, "kernel": cov_fun,
-                      "parallelism": f"library-rows{nshards} on {ndev} device(s)",
+                      "parallelism": f"library-rows{nshards}",
                       "devices": devices},
            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
                         "unit": "TFLOP/s", "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
-                        "kernel": con_key + " of shard 0", "flops_per_launch": flops},
+                        "traffic": traffic,
+                        "kernel": con_key + " of shard 0"
+                                  + (" (k_contract<8>)" if d <= 8 else " (k_contract<32>)"),
+                        "flops_per_launch": flops},
+           "kernel_rooflines": kernel_rooflines(args.mode, phase_avg, n0, m,
+                                                store_ceiling(n0, m, devices[0])),
+           "phases_ms": {k: round(v, 4) for k, v in phase_avg.items()},
+           "phases_note": "shard 0's HIP-event phase times from 3 evaluations after the timed "
+                          "steps",
            "objective": obj,
-           "note": "in-library multi-device context (sgp_ctx_create_multi); shards on one "
-                   "device run one after another on it"}
+           "collectives": "rccl (in-library, ncclCommInitAll over the distinct devices)",
+           "note": "in-library multi-device context (sgp_ctx_create_multi): one process, one "
+                   "host worker per distinct device; shards on one device run one after another "
+                   "on it"}
+    if args.mode == "laplace":
+        out["nr_iters_per_eval"] = nr_iters[args.warmup:args.warmup + args.steps]
     print(json.dumps(out), flush=True)
     ctx.close()
 

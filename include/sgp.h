@@ -115,7 +115,8 @@ int sgp_ctx_destroy(sgp_ctx* ctx);
  * devices by an in-process RCCL all-reduce (ncclCommInitAll over the distinct devices, on each
  * device's stream, in place).  A device may repeat (several shards on one GPU).
  * The handle is used with the ordinary entry points: sgp_eval_vi / sgp_eval_fitc /
- * sgp_eval_laplace / sgp_lap_nr, sgp_lap_set_f / sgp_lap_get_f / sgp_lap_get_grad_psi (n values
+ * sgp_eval_laplace / sgp_lap_nr, sgp_lap_set_f / sgp_lap_set_expo / sgp_lap_get_f /
+ * sgp_lap_get_grad_psi (n values
  * in the global row order) / sgp_lap_objective_values, sgp_posterior_u, sgp_ctx_enable_knot_grad,
  * sgp_knot_gradient (bounds NULL = the knot bounds of ALL rows), sgp_ctx_row_bounds (all rows),
  * sgp_ctx_set_data, sgp_ctx_rows (all rows), the three candidate scorers (each VI candidate as an
@@ -180,13 +181,24 @@ int sgp_fitc_finish(sgp_ctx* ctx, const double* red2, double* obj, double* grad)
  * (R/laplace_approx_gradient.R:25-553), exactly as one iteration of laplace_grad_ascent
  * (R/laplace_gradient_ascent.R:510-541).  K22 = Kuu + (tau^2 + delta) I (quirk Q1).
  * expo = the Poisson exposure `m` of the reference's likelihood helpers
- * (R/derivative_functions_of_data_likelihoods.R:7-61); tol/maxit = tol_nr/maxit_nr.
+ * (R/derivative_functions_of_data_likelihoods.R:7-61): a positive scalar for every row, or
+ * SGP_EXPO_ROWS for the per-row exposure of sgp_lap_set_expo; tol/maxit = tol_nr/maxit_nr.
  * The mode f stays resident in the context and warm-starts the next evaluation; its value
  * at context creation is 0, the reference starts at log(mean(y)) - log(expo)
  * (R/optimize_gp.R:480): set it with sgp_lap_set_f.  obj = the last NR objective value
  * (log q(y | theta, xu, f_hat)); nr_iters = length(objective_function_values).
  * maxit = 0 skips the NR loop: objective and dlogq_dcov_par at the resident f as given. */
 int sgp_lap_set_f(sgp_ctx* ctx, const double* f /* n host values, or NULL */, double fill);
+/* Per-row Poisson exposure: the reference's `m` is "a vector of the areas of each grid cell"
+ * (R/derivative_functions_of_data_likelihoods.R:38), passed through unchanged from
+ * optimize_gp's `a` (R/optimize_gp.R:461-468) and used element-wise (-m * exp(ff), y * log(m)).
+ * a = n host values (each > 0 and finite; SGP_EINVAL names the first that is not), or NULL for
+ * every row = fill.  The vector stays resident; a Laplace evaluation (sgp_eval_laplace,
+ * sgp_lap_nr, sgp_lap_begin, sgp_lap_candidates) called with expo = SGP_EXPO_ROWS uses it, and
+ * a positive expo keeps meaning that exposure on every row.  Multi-device contexts take the n
+ * values in the global row order. */
+#define SGP_EXPO_ROWS 0.0
+int sgp_lap_set_expo(sgp_ctx* ctx, const double* a /* n host values, or NULL */, double fill);
 int sgp_lap_get_f(sgp_ctx* ctx, double* f /* n host values */);
 /* grad psi of the last Newton-Raphson step (n host values): the `gradient` element
  * newtrap_sparseGP returns (R/newtrap_sparseGP.R:183-184) -- evaluated at the mode estimate

@@ -287,7 +287,10 @@ def eval_laplace(kernel, theta, X, y, mu, U, f0, expo=1.0, delta=1e-6, tol=1e-5,
     f = np.array(f0, dtype=np.float64).reshape(-1)
     n, d = X.shape
     m = U.shape[0]
-    a_ = float(expo)
+    # the exposure a (the reference's `m`): a scalar or one value per row, used element-wise
+    # (R/derivative_functions_of_data_likelihoods.R:7-61, R/laplace_approx_obj_funs.R:125-129)
+    a_ = np.broadcast_to(np.asarray(expo, dtype=np.float64).reshape(-1) if np.size(expo) > 1
+                         else np.float64(expo), (n,))
     L, sigma, tau, ls = _params(kernel, theta, d)
     sig2, tau2 = sigma * sigma, tau * tau
     center = U.mean(axis=0)
@@ -301,7 +304,7 @@ def eval_laplace(kernel, theta, X, y, mu, U, f0, expo=1.0, delta=1e-6, tol=1e-5,
     ld22 = np.linalg.slogdet(K22)[1]
     from scipy.special import gammaln
     lgy = gammaln(y + 1.0)
-    log_a = math.log(a_)
+    log_a = np.log(a_)
 
     def chunks():
         for s0 in range(0, n, chunk):
@@ -315,12 +318,13 @@ def eval_laplace(kernel, theta, X, y, mu, U, f0, expo=1.0, delta=1e-6, tol=1e-5,
     def obj_partials(K, sl):
         """S_B, t_Z and the scalar sums of obj_fun_pois at the current f (rows sl)."""
         fz, Zc = f[sl], Z[sl]
-        W = -a_ * np.exp(fz)
+        W = -a_[sl] * np.exp(fz)
         B = W / (Zc * W - 1.0)
         r = fz - mu[sl]
         rz = r / Zc
         return (K.T @ (B[:, None] * K), K.T @ rz,
-                np.array([r @ rz, float(np.sum(y[sl] * log_a - lgy[sl] - a_ * np.exp(fz) + y[sl] * fz)),
+                np.array([r @ rz, float(np.sum(y[sl] * log_a[sl] - lgy[sl] - a_[sl] * np.exp(fz)
+                                               + y[sl] * fz)),
                           float(np.sum(np.log(1.0 - W * Zc)))]))
 
     # ---- begin: Z, S_Z and the first objective's partials
@@ -361,9 +365,9 @@ def eval_laplace(kernel, theta, X, y, mu, U, f0, expo=1.0, delta=1e-6, tol=1e-5,
         for s0, s1, _, _, K in chunks():
             sl = slice(s0, s1)
             fz, Zc = f[sl], Z[sl]
-            W = -a_ * np.exp(fz)
+            W = -a_[sl] * np.exp(fz)
             omzw[sl] = 1.0 - Zc * W
-            g[sl] = y[sl] - a_ * np.exp(fz)
+            g[sl] = y[sl] - a_[sl] * np.exp(fz)
             rv[sl] = fz - mu[sl]
             y1[sl] = K @ x1
             gpsi = g[sl] - (rv[sl] - y1[sl]) / Zc
@@ -392,10 +396,10 @@ def eval_laplace(kernel, theta, X, y, mu, U, f0, expo=1.0, delta=1e-6, tol=1e-5,
     for s0, s1, _, _, K in chunks():
         sl = slice(s0, s1)
         fz, Zc = f[sl], Z[sl]
-        W = -a_ * np.exp(fz)
+        W = -a_[sl] * np.exp(fz)
         B = W / (Zc * W - 1.0)
         Bv[sl] = B
-        g[sl] = y[sl] - a_ * np.exp(fz)
+        g[sl] = y[sl] - a_[sl] * np.exp(fz)
         c2[sl] = (fz - mu[sl] - K @ x1) / Zc
         p = np.einsum("ij,ij->i", K, K @ C)
         dMt[sl] = B - B * B * p

@@ -20,7 +20,7 @@
 ## fused evaluation on a device-resident context.  They run the package's original driver
 ## whenever the fused path does not apply: a user-supplied objective, non-package derivative
 ## closures, a knot derivative that does not match cov_fun, the "exp" kernel, a non-Poisson
-## likelihood or a per-row exposure.
+## likelihood or an exposure that is not positive and finite.
 ##
 ## elbo_fun / obj_fun_norm receive the already-built Sigma12 / Sigma22 in the reference; called
 ## directly they take the fused path only when the caller also passes xy = , xu = , cov_fun =
@@ -32,10 +32,10 @@
 
 ## Multi-GPU (north star C4): the rows of a fit are split into contiguous blocks over the GPUs of
 ## the node and every evaluation's row sums are combined inside libsgp by an RCCL all-reduce
-## (sgp_ctx_create_multi).  sgp_options(ngpus = k) uses devices 0..k-1; ngpus = NULL (the
-## default) uses every visible GPU once each shard keeps >= 125 000 rows (one GPU below that:
-## the replicated m x m work would dominate); sgp_options(devices = c(...)) names the device of
-## each shard explicitly (repeats allowed).
+## (sgp_ctx_create_multi).  Multi-GPU is opt-in: ngpus = NULL (the default) is one GPU;
+## sgp_options(ngpus = k) uses devices 0..k-1; ngpus = "auto" uses every visible GPU once each
+## shard keeps >= 125 000 rows (one GPU below that: the replicated m x m work would dominate);
+## sgp_options(devices = c(...)) names the device of each shard explicitly (repeats allowed).
 .sgp <- new.env(parent = emptyenv())
 .sgp$opts <- list(r_det = TRUE, ngpus = NULL, devices = NULL)
 .sgp$orig <- list()
@@ -69,7 +69,8 @@ sgp_install <- function(ns = asNamespace("sparseRGPs")) {
   dv <- .sgp$opts$devices
   if (!is.null(dv)) return(as.integer(dv))
   ng <- .sgp$opts$ngpus
-  if (is.null(ng)) {
+  if (is.null(ng)) return(integer(0))
+  if (identical(ng, "auto")) {
     nd <- .Call("sgp_R_device_count")
     ng <- max(1L, min(nd, n %/% 125000L))
   }
@@ -210,13 +211,21 @@ sgp_dlogp_dcov_par <- function(cov_par, cov_fun, dcov_fun_dtheta, dcov_fun_dknot
 
 ## ---------------------------------------------------------------- Poisson sparse Laplace
 
-## the fused path implements the Poisson likelihood with a scalar exposure m
+## the fused path implements the Poisson likelihood with the exposure m a scalar or one value
+## per row (a vector of cell areas, derivative_functions_of_data_likelihoods.R:38), each
+## positive and finite (anything else runs the reference's own R code)
 .sgp_poisson <- function(d2log_py_dff, args) {
   pois <- tryCatch(get("d2log_py_dff_pois", envir = asNamespace("sparseRGPs")),
                    error = function(e) NULL)
-  m <- if (is.null(args$m)) 1 else args$m
-  !is.null(pois) && identical(body(d2log_py_dff), body(pois)) &&
-    length(unique(as.numeric(m))) == 1
+  m <- as.numeric(if (is.null(args$m)) 1 else args$m)
+  !is.null(pois) && identical(body(d2log_py_dff), body(pois)) && length(m) >= 1 &&
+    all(is.finite(m) & m > 0)
+}
+
+## the exposure as the shim takes it: one value, or one per row (R's recycling of -m * exp(ff))
+.sgp_expo <- function(args, n) {
+  m <- as.numeric(if (is.null(args$m)) 1 else args$m)
+  if (length(m) == 1L || length(unique(m)) == 1L) m[1] else rep_len(m, n)
 }
 
 sgp_newtrap_sparseGP <- function(start_vals, obj_fun, grad_loglik_fn, dlog_py_dff,
@@ -236,7 +245,7 @@ sgp_newtrap_sparseGP <- function(start_vals, obj_fun, grad_loglik_fn, dlog_py_df
   .sgp$last <- NULL
   .Call("sgp_R_lap_set_f", ptr, as.numeric(start_vals))
   theta <- .sgp_theta(cov_par, cov_fun, ncol(xu))
-  expo <- as.numeric(if (is.null(args$m)) 1 else args$m)[1]
+  expo <- .sgp_expo(args, nrow(as.matrix(xy)))
   ## newtrap_sparseGP.R:79-96 performs the first update whatever maxit is
   .Call("sgp_R_eval_laplace", ptr, cov_fun, unname(theta), xu, as.numeric(delta), expo,
         as.numeric(tol), as.integer(max(maxit, 1)), FALSE)
@@ -273,7 +282,7 @@ sgp_dlogq_dcov_par <- function(cov_par, cov_fun, dcov_fun_dtheta, dcov_fun_dknot
   .sgp_knots(ptr, knots)
   .Call("sgp_R_lap_set_f", ptr, as.numeric(ff))
   theta <- .sgp_theta(cov_par, cov_fun, ncol(xu))
-  expo <- as.numeric(if (is.null(args$m)) 1 else args$m)[1]
+  expo <- .sgp_expo(args, nrow(as.matrix(xy)))
   ## maxit = 0: objective and gradient at the given ff, no NR step
   ev <- .Call("sgp_R_eval_laplace", ptr, cov_fun, unname(theta), xu, as.numeric(delta), expo,
               0, 0L, TRUE)
@@ -616,7 +625,7 @@ sgp_laplace_grad_ascent <- function(cov_par_start,
   if (!is.numeric(mu)) mu <- rep(mean(y), times = length(y))
   if (!is.numeric(muu)) muu <- rep(mean(y), times = nrow(xu))
   y <- as.numeric(y)
-  expo <- as.numeric(if (is.null(args$m)) 1 else args$m)[1]
+  expo <- .sgp_expo(args, nrow(as.matrix(xy)))
   knots <- is.function(dcov_fun_dknot)
   ptr <- .sgp_ctx(xy, y, mu, nrow(xu))
   .sgp$last <- NULL

@@ -528,9 +528,27 @@ SEXP sgp_R_eval(SEXP ctx, SEXP method, SEXP cov_fun, SEXP theta, SEXP xu, SEXP d
   return out;
 }
 
+/* the Poisson exposure argument `m` (R/derivative_functions_of_data_likelihoods.R:7-61, "a vector
+ * of the areas of each grid cell", l.38): one value -> that exposure on every row; one value per
+ * context row -> made resident (sgp_lap_set_expo) and passed as SGP_EXPO_ROWS */
+static double expo_arg(sgp_ctx* c, SEXP expo) {
+  SEXP er = PROTECT(as_real(expo));
+  double v = 0.0;
+  if (Rf_length(er) == 1) {
+    v = REAL(er)[0];
+  } else if (Rf_length(er) == sgp_ctx_rows(c)) {
+    check(sgp_lap_set_expo(c, REAL(er), 0.0));
+    v = SGP_EXPO_ROWS;
+  } else {
+    Rf_error("the exposure m must have length 1 or one value per row");
+  }
+  UNPROTECT(1);
+  return v;
+}
+
 /* sgp_R_eval_laplace(ctx, cov_fun, theta, xu, delta, expo, tol, maxit, grad):
  * newtrap_sparseGP from the resident f + (grad != 0) dlogq_dcov_par at the mode.
- * maxit = 0: objective and gradient at the resident f (no NR step).
+ * maxit = 0: objective and gradient at the resident f (no NR step).  expo: length 1 or n.
  * -> list(objective, gradient, nr_iter) */
 SEXP sgp_R_eval_laplace(SEXP ctx, SEXP cov_fun, SEXP theta, SEXP xu, SEXP delta, SEXP expo,
                         SEXP tol, SEXP maxit, SEXP want_grad) {
@@ -540,12 +558,12 @@ SEXP sgp_R_eval_laplace(SEXP ctx, SEXP cov_fun, SEXP theta, SEXP xu, SEXP delta,
   SEXP grad = PROTECT(Rf_allocVector(REALSXP, Rf_length(th)));
   double obj = 0.0;
   int it = 0;
+  const double ex = expo_arg(c, expo);
   if (Rf_asLogical(want_grad))
-    check(sgp_eval_laplace(c, kernel, REAL(th), REAL(ur), m, m, Rf_asReal(delta),
-                           Rf_asReal(expo), Rf_asReal(tol), Rf_asInteger(maxit), &obj,
-                           REAL(grad), &it));
+    check(sgp_eval_laplace(c, kernel, REAL(th), REAL(ur), m, m, Rf_asReal(delta), ex,
+                           Rf_asReal(tol), Rf_asInteger(maxit), &obj, REAL(grad), &it));
   else
-    check(sgp_lap_nr(c, kernel, REAL(th), REAL(ur), m, m, Rf_asReal(delta), Rf_asReal(expo),
+    check(sgp_lap_nr(c, kernel, REAL(th), REAL(ur), m, m, Rf_asReal(delta), ex,
                      Rf_asReal(tol), Rf_asInteger(maxit), &obj, &it));
   static const char* nm[3] = {"objective", "gradient", "nr_iter"};
   SEXP v[3] = {PROTECT(Rf_ScalarReal(obj)), grad, PROTECT(Rf_ScalarInteger(it))};
@@ -672,8 +690,8 @@ SEXP sgp_R_candidates(SEXP ctx, SEXP method, SEXP cov_fun, SEXP theta, SEXP xu, 
                              REAL(cr), T, T, REAL(out));
   else
     st = sgp_lap_candidates(c, kernel, REAL(th), REAL(ur), m, m, Rf_asReal(delta),
-                            Rf_asReal(expo), Rf_asReal(tol), Rf_asInteger(maxit), REAL(cr), T, T,
-                            REAL(out));
+                            expo_arg(c, expo), Rf_asReal(tol), Rf_asInteger(maxit), REAL(cr), T,
+                            T, REAL(out));
   check(st);
   UNPROTECT(4);
   return out;

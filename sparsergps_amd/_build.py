@@ -23,8 +23,9 @@ LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libsgp.so")
 VARIANT_ROOT = os.path.join(ROOT, "tools", "ab")
 SOURCES = ["capi.hip", "k_cov.hip", "k_mfma.hip", "k_dense.hip", "k_lap.hip", "multi.hip"]
-HEADERS = ["sgp_internal.h", "sgp_probe.h", "sgp_multi.h",
-           os.path.join("..", "..", "include", "sgp.h")]
+HEADERS = ["sgp_internal.h", "sgp_probe.h", "sgp_multi.h", "sgp_pool.h",
+           os.path.join("..", "..", "include", "sgp.h"),
+           os.path.join("..", "..", "include", "sgp_diag.h")]
 ARCH = "gfx950"
 
 
@@ -186,7 +187,7 @@ def build_variant(name: str, defs=(), force: bool = False, verbose: bool = False
         # the revision's sources (csrc + include/sgp.h) exported under tools/ab/<name>/src
         src_root = os.path.join(outdir, "src")
         os.makedirs(src_root, exist_ok=True)
-        for path in ["sparsergps_amd/csrc/" + f for f in SOURCES + HEADERS[:3]] + ["include/sgp.h"]:
+        for path in ["sparsergps_amd/csrc/" + f for f in SOURCES + HEADERS[:4]] + ["include/sgp.h", "include/sgp_diag.h"]:
             res = subprocess.run(["git", "-C", ROOT, "show", f"{rev}:{path}"],
                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE)
             if res.returncode != 0:   # a file the revision does not have yet

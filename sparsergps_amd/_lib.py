@@ -22,6 +22,7 @@ KERNELS = {"sqexp": 0, "ard": 1, "exp": 2}
 SGP_FLAG_R_DET = 1
 SGP_FLAG_OBJ_ONLY = 2
 SGP_PRED_VI, SGP_PRED_LAPLACE, SGP_PRED_FULL = 0, 1, 2
+SGP_EXPO_ROWS = 0.0   # expo argument: the per-row exposure of sgp_lap_set_expo
 
 # name -> (restype, argtypes); exactly the functions declared in include/sgp.h
 PROTOTYPES = {
@@ -67,6 +68,11 @@ PROTOTYPES = {
     "sgp_fitc_phase2": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_uint, C.c_void_p]),
     "sgp_fitc_finish": (C.c_int, [C.c_void_p, C.c_void_p, c_double_p, c_double_p]),
     "sgp_lap_set_f": (C.c_int, [C.c_void_p, c_double_p, C.c_double]),
+    "sgp_lap_set_expo": (C.c_int, [C.c_void_p, c_double_p, C.c_double]),
+    # include/sgp_diag.h (diagnostics: GPU tests and bench.py)
+    "sgp_diag_gj_pair": (C.c_int, [C.c_int, C.c_int64, c_double_p, c_double_p, C.c_double, C.c_int,
+                                   c_double_p, c_double_p, c_double_p]),
+    "sgp_diag_store_bw": (C.c_int, [C.c_int, C.c_int64, C.c_int, C.c_int, c_double_p]),
     "sgp_lap_get_f": (C.c_int, [C.c_void_p, c_double_p]),
     "sgp_lap_get_grad_psi": (C.c_int, [C.c_void_p, c_double_p]),
     "sgp_lap_objective_values": (C.c_int, [C.c_void_p, c_double_p, C.c_int, c_int_p]),

@@ -9,6 +9,8 @@
 //     G = alpha u^T + K P (one GEMM) contracted with dK/dtheta in the epilogue
 // which is algebraically identical and needs ~3 n m^2 flops in total.
 #include <math.h>
+
+#include <cmath>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -20,6 +22,7 @@
 #include <vector>
 
 #include "../../include/sgp.h"
+#include "../../include/sgp_diag.h"
 #include "sgp_internal.h"
 
 #ifdef SGP_HOST_PROBE
@@ -301,6 +304,8 @@ struct sgp_ctx {
   double* lred[2] = {nullptr, nullptr};   // ping-pong reduction buffers of sgp_eval_laplace
   int lap_state = 0, lap_it = 0, lap_maxit = 0;
   double lap_obj = 0.0, lap_obj_prev = 0.0, lap_cnt = 0.0, lap_tol = 0.0, lap_expo = 1.0;
+  bool lap_expo_rows = false;             // LV_AEXP holds a per-row exposure (sgp_lap_set_expo)
+  const double* lap_av = nullptr;         // this NR run's per-row exposure (nullptr: lap_expo)
   std::vector<double> lap_objs;           // objective_function_values of the last NR run
   // timing
   bool timing = false;
@@ -350,6 +355,9 @@ struct Readback {
   GatherSegs segs{};
   explicit Readback(sgp_ctx* ctx)
       : c(ctx), base(ctx->pin + ctx->mp_max * ctx->d + ctx->m_max + (ctx->m_max + 1) / 2 + 8) {}
+  // a readback abandoned before wait() (a failed add) drops the deferred record pass too: it
+  // belongs to this readback's evaluation, and a later readback must not replay it
+  ~Readback() { c->rec_defer = RecPass2{}; }
   // dev: device memory of `bytes` bytes, 8-byte aligned (copied as whole doubles)
   hipError_t add(void* host, const void* dev, size_t bytes) {
     const size_t nd = (bytes + 7) / 8;
@@ -1524,7 +1532,16 @@ int sgp_vi_finish(sgp_ctx* c, const double* red2, double* obj, double* grad) {
     return SGP_EINVAL;
   }
   if (c->phase != 2) { set_err("sgp_vi_finish called before sgp_vi_phase2"); return SGP_EINVAL; }
-  HIPCHK(hipSetDevice(c->device));
+  {
+    const hipError_t e = hipSetDevice(c->device);
+    if (e != hipSuccess) {
+      // the evaluation is abandoned: no later readback may replay its deferred record pass
+      c->rec_defer = RecPass2{};
+      c->phase = 0;
+      set_err("HIP error '%s' in hipSetDevice", hipGetErrorString(e));
+      return SGP_EHIP;
+    }
+  }
   const KernParams& kp = c->kp;
   const int L = kp.L;
   double sc[SC_N], r2[SGP_MAXD + 8];
@@ -1584,6 +1601,12 @@ int sgp_eval_vi(sgp_ctx* c, int kernel, const double* theta, const double* U, in
                 int64_t ldu, double delta, unsigned flags, double* obj, double* grad) {
   MULTI_FWD(c, obj && (grad || (flags & SGP_FLAG_OBJ_ONLY)) ? multi_eval_vi(c->multi, kernel, theta, U, m, ldu, delta, flags, obj, grad) : multi_bad_args());
   if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
+  // sgp_vi_finish's own argument checks must not be the first to fail: phase 2 below defers the
+  // records' second pass to finish's readback, and an early return there would leave it queued
+  if (!obj || (!grad && !(flags & SGP_FLAG_OBJ_ONLY))) {
+    set_err("obj is NULL, or grad is NULL without SGP_FLAG_OBJ_ONLY");
+    return SGP_EINVAL;
+  }
 #ifdef SGP_HOST_PROBE
   hp_t0 = hp_now();
   sgp_probe_t[0] = hp_t0;
@@ -1865,7 +1888,7 @@ int sgp_eval_fitc(sgp_ctx* c, int kernel, const double* theta, const double* U, 
 //   FIN     : G22 contraction, gradient
 enum { LS_NONE = 0, LS_OBJ0, LS_NRB, LS_OBJ, LS_GRADB, LS_FIN };
 enum { LV_F = 0, LV_Z, LV_ZI, LV_B, LV_RF, LV_TV, LV_OMZW, LV_Y1, LV_Y2, LV_DMT, LV_SV, LV_H,
-       LV_A, LV_V, LV_P, LV_C2, LV_G, LV_BSV, LV_GPSI, LV_N };   // C2, G, BSV adjacent (one K^T pass)
+       LV_A, LV_V, LV_P, LV_C2, LV_G, LV_BSV, LV_GPSI, LV_AEXP, LV_N };   // C2, G, BSV adjacent (one K^T pass)
 enum { LM_X1 = 0, LM_X2, LM_S, LM_GG, LM_NGG, LM_CW, LM_N };
 
 static double* lvec(sgp_ctx* c, int k) { return c->lv + (int64_t)k * c->n_pad; }
@@ -1910,6 +1933,32 @@ int sgp_lap_set_f(sgp_ctx* c, const double* f, double fill) {
   return SGP_OK;
 }
 
+// the reference's `m` per row ("a vector of the areas of each grid cell",
+// R/derivative_functions_of_data_likelihoods.R:38; optimize_gp.R:461-468 passes `a` through as m)
+int sgp_lap_set_expo(sgp_ctx* c, const double* a, double fill) {
+  MULTI_FWD(c, multi_lap_set_expo(c->multi, a, fill));
+  if (!c) { set_err("context is NULL"); return SGP_EINVAL; }
+  if (!a && !(fill > 0.0 && std::isfinite(fill))) {
+    set_err("sgp_lap_set_expo: the fill exposure %g is not a positive finite number", fill);
+    return SGP_EINVAL;
+  }
+  for (int64_t i = 0; a && i < c->n; ++i)
+    if (!(a[i] > 0.0 && std::isfinite(a[i]))) {
+      set_err("sgp_lap_set_expo: exposure a[%lld] = %g is not a positive finite number",
+              (long long)i, a[i]);
+      return SGP_EINVAL;
+    }
+  HIPCHK(hipSetDevice(c->device));
+  int st = lap_ensure(c);
+  if (st) return st;
+  std::vector<double> h((size_t)c->n_pad, 1.0);
+  for (int64_t i = 0; i < c->n; ++i) h[(size_t)i] = a ? a[i] : fill;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(lvec(c, LV_AEXP), h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice));
+  c->lap_expo_rows = true;
+  return SGP_OK;
+}
+
 int sgp_lap_get_grad_psi(sgp_ctx* c, double* out) {
   MULTI_FWD(c, out ? multi_lap_get_grad_psi(c->multi, out) : multi_bad_args());
   if (!c || !out) { set_err("invalid arguments"); return SGP_EINVAL; }
@@ -1940,7 +1989,7 @@ static int lap_obj_partials(sgp_ctx* c, double* red, int64_t o) {
   Scope t(c, "lap_obj");
   int nb = 0;
   HIPCHK(launch_lap_obj(c->n, c->n_pad, lvec(c, LV_F), c->y, c->mu, lvec(c, LV_Z),
-                        lvec(c, LV_ZI), c->lap_expo, lvec(c, LV_B), lvec(c, LV_RF),
+                        lvec(c, LV_ZI), c->lap_expo, c->lap_av, lvec(c, LV_B), lvec(c, LV_RF),
                         lvec(c, LV_TV), c->slab_small, &nb, c->stream));
   HIPCHK(launch_syrk_aug(c->K, c->n_pad, mp, lvec(c, LV_RF), lvec(c, LV_B), c->slab_syrk,
                          c->slab_syrk_cap, red + o, c->stream, 3, lvec(c, LV_TV)));
@@ -1956,8 +2005,12 @@ int sgp_lap_begin(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   int st = check_eval_args(c, kernel, theta, U, m, ldu, delta, &kp);
   if (st) return st;
   if (!red_out || !count) { set_err("red_out/count is NULL"); return SGP_EINVAL; }
-  if (!(expo > 0.0) || !(tol >= 0.0) || maxit < 0) {
+  if (!(expo >= 0.0) || !std::isfinite(expo) || !(tol >= 0.0) || maxit < 0) {
     set_err("invalid Laplace controls (expo=%g, tol=%g, maxit=%d)", expo, tol, maxit);
+    return SGP_EINVAL;
+  }
+  if (expo == SGP_EXPO_ROWS && !c->lap_expo_rows) {
+    set_err("expo = SGP_EXPO_ROWS but no per-row exposure was set (sgp_lap_set_expo)");
     return SGP_EINVAL;
   }
   HIPCHK(hipSetDevice(c->device));
@@ -1970,7 +2023,8 @@ int sgp_lap_begin(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   c->m = m;
   c->mp = round_up(m, SGP_TILE);
   c->delta = delta;
-  c->lap_expo = expo;
+  c->lap_expo = expo == SGP_EXPO_ROWS ? 1.0 : expo;
+  c->lap_av = expo == SGP_EXPO_ROWS ? lvec(c, LV_AEXP) : nullptr;
   c->lap_tol = tol;
   c->lap_maxit = maxit;
   c->flags = flags;
@@ -2090,7 +2144,7 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
         // one pass over K12: y1 = K x1, the row update and K^T v from the same staged rows
         HIPCHK(launch_lap_nr_a_fused(c->K, n, n_pad, mp, lmv(c, LM_X1), lvec(c, LV_F), c->y,
                                      c->mu, lvec(c, LV_Z), lvec(c, LV_ZI), c->lap_expo,
-                                     c->lap_tol, lvec(c, LV_Y1), lvec(c, LV_G), lvec(c, LV_OMZW),
+                                     c->lap_av, c->lap_tol, lvec(c, LV_Y1), lvec(c, LV_G), lvec(c, LV_OMZW),
                                      lvec(c, LV_V), lvec(c, LV_GPSI), c->lslab, c->lslab_cap,
                                      red_out, red_out + mp, c->stream));
       } else {
@@ -2098,7 +2152,7 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
                                 c->stream));
         int nb = 0;
         HIPCHK(launch_lap_nr_a(n, n_pad, lvec(c, LV_F), c->y, c->mu, lvec(c, LV_Z),
-                               lvec(c, LV_ZI), c->lap_expo, lvec(c, LV_Y1), c->lap_tol,
+                               lvec(c, LV_ZI), c->lap_expo, c->lap_av, lvec(c, LV_Y1), c->lap_tol,
                                lvec(c, LV_G), lvec(c, LV_OMZW), lvec(c, LV_V), lvec(c, LV_GPSI),
                                c->slab_small, &nb, c->stream));
         HIPCHK(launch_gemv_cols(c->K, n_pad, mp, lvec(c, LV_V), n_pad, 1, c->lslab, c->lslab_cap,
@@ -2128,7 +2182,7 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
                               lvec(c, LV_ZI), lmv(c, LM_X1), lvec(c, LV_C2), c->rowq,
                               lvec(c, LV_P), c->stream, tstore_ready(c) ? c->tp : nullptr));
     HIPCHK(launch_lap_grad_a(n, n_pad, lvec(c, LV_F), c->y, c->mu, lvec(c, LV_Z), lvec(c, LV_ZI),
-                             c->lap_expo, nullptr, lvec(c, LV_P), lvec(c, LV_C2),
+                             c->lap_expo, c->lap_av, nullptr, lvec(c, LV_P), lvec(c, LV_C2),
                              lvec(c, LV_G), lvec(c, LV_B), lvec(c, LV_DMT), lvec(c, LV_SV),
                              lvec(c, LV_BSV), c->stream));
     HIPCHK(launch_gemv_cols(c->K, n_pad, mp, lvec(c, LV_C2), n_pad, 3, c->lslab, c->lslab_cap,
@@ -2165,7 +2219,7 @@ int sgp_lap_step(sgp_ctx* c, const double* red_in, double* red_out, int64_t* cou
                                      red_out + mm, red_out + mm + mp, c->stream));
       int nb = 0;
       HIPCHK(launch_lap_obj(n, n_pad, lvec(c, LV_F), c->y, c->mu, lvec(c, LV_Z), lvec(c, LV_ZI),
-                            c->lap_expo, lvec(c, LV_B), lvec(c, LV_RF), lvec(c, LV_TV),
+                            c->lap_expo, c->lap_av, lvec(c, LV_B), lvec(c, LV_RF), lvec(c, LV_TV),
                             c->slab_small, &nb, c->stream));
       // B = W / (Z W - 1) >= 0 (W = -a e^f <= 0, Z > 0)
       HIPCHK(launch_syrk_aug(c->K, n_pad, mp, lvec(c, LV_RF), lvec(c, LV_B), c->slab_syrk,
@@ -2638,7 +2692,7 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
 int sgp_vi_candidates(sgp_ctx* c, int kernel, const double* theta, const double* U, int64_t m,
                       int64_t ldu, double delta, unsigned flags, const double* cand, int64_t T,
                       int64_t ldc, double* obj_out) {
-  MULTI_FWD(c, cand && T >= 1 && ldc >= T && obj_out ? multi_vi_candidates(c->multi, kernel, theta, U, m, ldu, delta, flags, cand, T, ldc, obj_out) : multi_bad_args());
+  MULTI_FWD(c, U && cand && T >= 1 && ldc >= T && obj_out && m >= 1 && ldu >= m ? multi_vi_candidates(c->multi, kernel, theta, U, m, ldu, delta, flags, cand, T, ldc, obj_out) : multi_bad_args());
   if (!c || !cand || T < 1 || ldc < T || !obj_out) {
     set_err("invalid sgp_vi_candidates arguments");
     return SGP_EINVAL;
@@ -2844,6 +2898,163 @@ int sgp_lap_candidates(sgp_ctx* c, int kernel, const double* theta, const double
   c->last_mode = 0;   // the context's posterior state belongs to the last candidate
   c->lap_gpsi_valid = false;
   return st;
+}
+
+// ------------------------------------------------------------------------- diagnostics
+// (include/sgp_diag.h)
+
+int sgp_diag_gj_pair(int device, int64_t m, const double* A, const double* B, double beta,
+                     int per_step, double* invA, double* invS, double* logdet) {
+  if (m < 1 || m > 16384 || !A || !B || !invA || !invS || !logdet ||
+      !(beta == beta) || (per_step != 0 && per_step != 1)) {
+    set_err("invalid sgp_diag_gj_pair arguments (m=%lld, per_step=%d)", (long long)m, per_step);
+    return SGP_EINVAL;
+  }
+  const int64_t mp = round_up(m, SGP_TILE), mm = mp * mp, nb = mp / SGP_DB;
+  if (!per_step && nb > 64) {
+    set_err("sgp_diag_gj_pair: the persistent chain takes m <= 4096 (m = %lld)", (long long)m);
+    return SGP_EINVAL;
+  }
+  HIPCHK(hipSetDevice(device));
+  StreamGuard s_main, s_aux;
+  HIPCHK(hipStreamCreateWithFlags(&s_main.s, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&s_aux.s, hipStreamNonBlocking));
+  DevBuf dA, dB, dInvA, dInvS, R1, R2, P1, P2, L1, L2;
+  IntBuf status, sync;
+  int st = dalloc(&dA.p, mm);
+  st = st ? st : dalloc(&dB.p, mm);
+  st = st ? st : dalloc(&dInvA.p, mm);
+  st = st ? st : dalloc(&dInvS.p, mm);
+  st = st ? st : dalloc(&R1.p, mm);
+  st = st ? st : dalloc(&R2.p, mm);
+  st = st ? st : dalloc(&P1.p, mp * 64);
+  st = st ? st : dalloc(&P2.p, mp * 64);
+  st = st ? st : dalloc(&L1.p, nb);
+  st = st ? st : dalloc(&L2.p, nb);
+  st = st ? st : dalloc(&status.p, 4);
+  st = st ? st : dalloc(&sync.p, 2 * SGP_GJ_SYNC_WORDS);
+  if (st) return st;
+  // row-major padded as the contexts hold them: A padded with the identity, B with zeros
+  std::vector<double> hA((size_t)mm, 0.0), hB((size_t)mm, 0.0);
+  for (int64_t i = 0; i < mp; ++i)
+    for (int64_t j = 0; j < mp; ++j) {
+      const bool in = i < m && j < m;
+      hA[(size_t)(i * mp + j)] = in ? A[i + j * m] : (i == j ? 1.0 : 0.0);
+      hB[(size_t)(i * mp + j)] = in ? B[i + j * m] : 0.0;
+    }
+  HIPCHK(hipMemcpy(dA.p, hA.data(), sizeof(double) * mm, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dB.p, hB.data(), sizeof(double) * mm, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dInvA.p, hA.data(), sizeof(double) * mm, hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(status.p, 0, sizeof(int) * 4));
+  HIPCHK(hipMemset(sync.p, 0, sizeof(int) * 2 * SGP_GJ_SYNC_WORDS));
+  unsigned* sy = reinterpret_cast<unsigned*>(sync.p);
+  // both chains in flight together, as VI's phase 2 issues them
+  HIPCHK(dense_spd_inverse_chain(dInvA.p, mp, R1.p, P1.p, L1.p, status.p, sy + SGP_GJ_SYNC_WORDS,
+                                 s_aux.s, per_step != 0));
+  HIPCHK(dense_spd_inverse_sum_chain(dA.p, beta, dB.p, dInvS.p, mp, R2.p, P2.p, L2.p,
+                                     status.p + 1, sy, s_main.s, per_step != 0));
+  HIPCHK(hipStreamSynchronize(s_aux.s));
+  HIPCHK(hipStreamSynchronize(s_main.s));
+  int hs[4];
+  std::vector<double> ld1((size_t)nb), ld2((size_t)nb);
+  HIPCHK(hipMemcpy(hs, status.p, sizeof(hs), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(ld1.data(), L1.p, sizeof(double) * nb, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(ld2.data(), L2.p, sizeof(double) * nb, hipMemcpyDeviceToHost));
+  if (chain_watchdog(hs)) return SGP_EHIP;
+  if (hs[0] || hs[1]) {
+    set_err("chol(): the leading minor of order %d of %s is not positive definite",
+            hs[0] ? hs[0] : hs[1], hs[0] ? "A" : "A + beta B");
+    return SGP_ENOTPD;
+  }
+  HIPCHK(hipMemcpy(hA.data(), dInvA.p, sizeof(double) * mm, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(hB.data(), dInvS.p, sizeof(double) * mm, hipMemcpyDeviceToHost));
+  for (int64_t i = 0; i < m; ++i)
+    for (int64_t j = 0; j < m; ++j) {
+      invA[i + j * m] = hA[(size_t)(i * mp + j)];
+      invS[i + j * m] = hB[(size_t)(i * mp + j)];
+    }
+  // block log-determinant halves summed in block order (the evaluations' order)
+  double a = 0.0, b = 0.0;
+  for (int64_t k = 0; k < nb; ++k) {
+    a += ld1[(size_t)k];
+    b += ld2[(size_t)k];
+  }
+  logdet[0] = 2.0 * a;
+  logdet[1] = 2.0 * b;
+  return SGP_OK;
+}
+
+namespace {
+typedef double sgp_d2 __attribute__((ext_vector_type(2)));
+// pattern 0: one linear stream, 16 B per lane per instruction
+__global__ void __launch_bounds__(256) k_diag_store_lin(sgp_d2* __restrict__ p, int64_t n2,
+                                                        double v) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n2; i += (int64_t)gridDim.x * 256)
+    __builtin_nontemporal_store(sgp_d2{v, v}, &p[i]);
+}
+// pattern 1: the K12 builder's store shape -- per wave instruction 4 rows x 256 B of a
+// row-major matrix with mp = 1024 doubles per row; a workgroup owns 128 columns and walks 64-row
+// blocks
+__global__ void __launch_bounds__(256) k_diag_store_tile(double* __restrict__ K, int64_t nrb,
+                                                         int64_t mp, double v) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, ln = lane & 15, lq = lane >> 4;
+  const int64_t j0 = (int64_t)blockIdx.x * 128;
+  for (int64_t rb = blockIdx.y; rb < nrb; rb += gridDim.y) {
+    const int64_t ib = rb * 64 + 16 * w;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t i = ib + lq + 4 * r;
+        __builtin_nontemporal_store(sgp_d2{v, v},
+                                    reinterpret_cast<sgp_d2*>(&K[i * mp + j0 + 32 * p + 2 * ln]));
+      }
+  }
+}
+}  // namespace
+
+int sgp_diag_store_bw(int device, int64_t bytes, int reps, int pattern, double* gbs) {
+  if (!gbs || bytes < (int64_t)(1 << 20) || reps < 1 || (pattern != 0 && pattern != 1)) {
+    set_err("invalid sgp_diag_store_bw arguments");
+    return SGP_EINVAL;
+  }
+  HIPCHK(hipSetDevice(device));
+  const int64_t mp = 1024;
+  const int64_t nrb = bytes / (64 * mp * 8);
+  if (nrb < 1) { set_err("sgp_diag_store_bw: bytes < one 64-row block"); return SGP_EINVAL; }
+  const int64_t used = nrb * 64 * mp * 8;
+  DevBuf buf;
+  int st = dalloc(&buf.p, used / 8);
+  if (st) return st;
+  int cus = 0;
+  HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+  StreamGuard sg;
+  HIPCHK(hipStreamCreateWithFlags(&sg.s, hipStreamNonBlocking));
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  double best = 0.0;
+  hipError_t err = hipSuccess;
+  for (int r = 0; r <= reps && err == hipSuccess; ++r) {   // pass 0 warms up
+    err = hipEventRecord(e0, sg.s);
+    if (pattern == 0)
+      hipLaunchKernelGGL(k_diag_store_lin, dim3((unsigned)(cus * 16)), dim3(256), 0, sg.s,
+                         reinterpret_cast<sgp_d2*>(buf.p), used / 16, (double)r);
+    else
+      hipLaunchKernelGGL(k_diag_store_tile, dim3((unsigned)(mp / 128), (unsigned)(cus * 2)),
+                         dim3(256), 0, sg.s, buf.p, nrb, mp, (double)r);
+    if (err == hipSuccess) err = hipGetLastError();
+    if (err == hipSuccess) err = hipEventRecord(e1, sg.s);
+    if (err == hipSuccess) err = hipEventSynchronize(e1);
+    float ms = 0.0f;
+    if (err == hipSuccess) err = hipEventElapsedTime(&ms, e0, e1);
+    if (err == hipSuccess && r > 0 && ms > 0.0f) best = std::max(best, (double)used / (ms * 1e6));
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  HIPCHK(err);
+  *gbs = best;
+  return SGP_OK;
 }
 
 }  // extern "C"

@@ -9,6 +9,8 @@
 // Reductions are two-stage with fixed order (deterministic, run-to-run bit-identical).
 #include <stdlib.h>
 
+#include <atomic>
+
 #include "sgp_internal.h"
 #include "sgp_probe.h"
 
@@ -562,12 +564,14 @@ __device__ __forceinline__ void gj_store_acc(double* T, int64_t ld, const d4 (&a
       }
 }
 
+// withhold: a ticket whose flag publish is skipped (fault injection of the watchdog test, armed
+// only in probe builds, SGP_PROBE_GJ_WITHHOLD; -1 in the product)
 __global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const double* src0b,
                                                     double beta, double* buf, int64_t lda,
                                                     int nb, double* __restrict__ P,
                                                     double* __restrict__ logd,
                                                     int* __restrict__ status,
-                                                    unsigned* __restrict__ sync) {
+                                                    unsigned* __restrict__ sync, int withhold) {
   __shared__ double lds[4 * 64 * GJ_LS];
   __shared__ int tk;
   double* S0 = lds;
@@ -658,7 +662,7 @@ __global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const do
       gj_st16(S0, v);
       __syncthreads();
       gj_pivot_body<true>(S0, GJ_LS, 0, P, logd, status, S1);
-      gj_publish(piv, 1u);
+      if (t != withhold) gj_publish(piv, 1u);
       pk_have = -1;
       continue;
     }
@@ -743,7 +747,7 @@ __global__ void __launch_bounds__(256) k_gj_persist(const double* src0, const do
         __syncthreads();
         gj_pivot_body<true>(S0, GJ_LS, (int64_t)(k + 1) * 64, P + (int64_t)(k + 1) * 4096,
                       logd + k + 1, status, S1);
-        gj_publish(piv + k + 1, 1u);
+        if (t != withhold) gj_publish(piv + k + 1, 1u);
         pk_have = -1;   // S1 was the pivot's scratch
       }
       continue;
@@ -1015,22 +1019,55 @@ static int gj_workgroups(int nb) {
   return nb * nb < cap ? nb * nb : cap;
 }
 
+// the ticket whose publish the next launch withholds: -1, except once per process in a probe
+// build run with SGP_PROBE_GJ_WITHHOLD=<ticket> (the watchdog test, tests/test_gpu_gj.py)
+static int gj_withhold_ticket() {
+#ifdef SGP_PROBE_BUILD
+  static std::atomic<int> armed{-2};
+  int a = armed.load();
+  if (a == -2) {
+    const char* e = getenv("SGP_PROBE_GJ_WITHHOLD");
+    int want = e ? atoi(e) : -1;
+    if (armed.compare_exchange_strong(a, want)) a = want;
+  }
+  if (a >= 0 && armed.compare_exchange_strong(a, -1)) return a;
+#endif
+  return -1;
+}
+
 static hipError_t gj_persist(const double* src0, const double* src0b, double beta, double* buf,
                              int64_t mp, double* P, double* logd, int* status, unsigned* sync,
                              hipStream_t s) {
   const int nb = (int)(mp / SGP_DB);
   hipLaunchKernelGGL(k_gj_persist, dim3(gj_workgroups(nb)), dim3(256), 0, s, src0, src0b, beta,
-                     buf, mp, nb, P, logd, status, sync);
+                     buf, mp, nb, P, logd, status, sync, gj_withhold_ticket());
   return hipGetLastError();
 }
 
 hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* P, double* logd,
                              int* status, unsigned* sync, hipStream_t s) {
+  const int nb = (int)(mp / SGP_DB);
+  return dense_spd_inverse_chain(A, mp, R, P, logd, status, sync, s,
+                                 nb > GJ_NB_MAX || SGP_GJ_STEPS);
+}
+
+hipError_t dense_spd_inverse_sum(const double* A0, double beta, const double* B0, double* out,
+                                 int64_t mp, double* R, double* P, double* logd, int* status,
+                                 unsigned* sync, hipStream_t s) {
+  const int nb = (int)(mp / SGP_DB);
+  return dense_spd_inverse_sum_chain(A0, beta, B0, out, mp, R, P, logd, status, sync, s,
+                                     nb > GJ_NB_MAX || SGP_GJ_STEPS);
+}
+
+hipError_t dense_spd_inverse_chain(double* A, int64_t mp, double* R, double* P, double* logd,
+                                   int* status, unsigned* sync, hipStream_t s, bool per_step) {
   // in place; R: mp x mp ping-pong buffer of the launch-per-step chain (nb > GJ_NB_MAX);
   // P: nb 64x64 pivot inverses (mp * 64 doubles)
   const int nb = (int)(mp / SGP_DB);
-  if (nb <= GJ_NB_MAX && !SGP_GJ_STEPS)
+  if (!per_step) {
+    if (nb > GJ_NB_MAX) return hipErrorInvalidValue;
     return gj_persist(A, nullptr, 0.0, A, mp, P, logd, status, sync, s);
+  }
   hipLaunchKernelGGL(k_gj_pivot, dim3(1), dim3(256), 0, s, A, mp, 0, P, logd, status,
                      (const double*)nullptr, 0.0);
   double* src = A;
@@ -1049,15 +1086,17 @@ hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* P, double
   return hipGetLastError();
 }
 
-hipError_t dense_spd_inverse_sum(const double* A0, double beta, const double* B0, double* out,
-                                 int64_t mp, double* R, double* P, double* logd, int* status,
-                                 unsigned* sync, hipStream_t s) {
+hipError_t dense_spd_inverse_sum_chain(const double* A0, double beta, const double* B0,
+                                       double* out, int64_t mp, double* R, double* P, double* logd,
+                                       int* status, unsigned* sync, hipStream_t s, bool per_step) {
   // out = inv(A0 + beta B0), the sum formed as step 0 reads it (no axpby launch).  Launch per
   // step (nb > GJ_NB_MAX): step k writes buf[(nb - 1 - k) % 2] (buf = {out, R}), so the last
   // step always lands in out and no copy follows
   const int nb = (int)(mp / SGP_DB);
-  if (nb <= GJ_NB_MAX && !SGP_GJ_STEPS)
+  if (!per_step) {
+    if (nb > GJ_NB_MAX) return hipErrorInvalidValue;
     return gj_persist(A0, B0, beta, out, mp, P, logd, status, sync, s);
+  }
   double* buf[2] = {out, R};
   hipLaunchKernelGGL(k_gj_pivot, dim3(1), dim3(256), 0, s, A0, mp, 0, P, logd, status, B0, beta);
   for (int k = 0; k < nb; ++k) {

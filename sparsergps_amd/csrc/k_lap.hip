@@ -8,7 +8,9 @@
 // Row semantics follow the reference (R/derivative_functions_of_data_likelihoods.R:7-61,
 // R/newtrap_sparseGP.R:234-325, R/laplace_approx_obj_funs.R:108-174,
 // R/laplace_approx_gradient.R:133-336) with a = exposure (`m` in the reference's Poisson
-// helpers): W = d2 = d3 = -a e^f, d1 = y - a e^f.
+// helpers, "a vector of the areas of each grid cell", derivative_functions_of_data_likelihoods.R:
+// 38): W = d2 = d3 = -a e^f, d1 = y - a e^f.  a is per row: av[i] when the context holds a
+// per-row exposure (sgp_lap_set_expo), the scalar expo otherwise (av == nullptr).
 #include "sgp_internal.h"
 #include "sgp_probe.h"
 
@@ -60,20 +62,22 @@ __global__ void __launch_bounds__(256) k_lap_obj(int64_t n, int64_t n_pad,
                                                  const double* __restrict__ mu,
                                                  const double* __restrict__ Z,
                                                  const double* __restrict__ zinv, double expo,
-                                                 double logexpo, double* __restrict__ B,
+                                                 double logexpo, const double* __restrict__ av,
+                                                 double* __restrict__ B,
                                                  double* __restrict__ rf, double* __restrict__ tv,
                                                  double* __restrict__ slab) {
   double acc[2] = {0.0, 0.0};
   ROW_LOOP(i) {
     if (i < n) {
       const double fi = f[i], yi = y[i], zi = Z[i];
+      const double ai = av ? av[i] : expo, lai = av ? log(ai) : logexpo;
       const double e = exp(fi);
-      const double W = -expo * e;
+      const double W = -ai * e;
       B[i] = 1.0 / (zi - 1.0 / W);
       const double r = fi - mu[i];
       rf[i] = r;
       tv[i] = zinv[i] * r;
-      acc[0] += yi * logexpo - lgamma(yi + 1.0) - expo * e + yi * fi;
+      acc[0] += yi * lai - lgamma(yi + 1.0) - ai * e + yi * fi;
       const double sw = sqrt(-W);
       acc[1] += log(1.0 + sw * zi * sw);
     } else {
@@ -95,6 +99,7 @@ __global__ void __launch_bounds__(256) k_lap_nr_a(int64_t n, int64_t n_pad,
                                                   const double* __restrict__ mu,
                                                   const double* __restrict__ Z,
                                                   const double* __restrict__ zinv, double expo,
+                                                  const double* __restrict__ av,
                                                   const double* __restrict__ y1, double tol,
                                                   double* __restrict__ g, double* __restrict__ omzw,
                                                   double* __restrict__ v,
@@ -103,9 +108,10 @@ __global__ void __launch_bounds__(256) k_lap_nr_a(int64_t n, int64_t n_pad,
   double acc[1] = {0.0};
   ROW_LOOP(i) {
     if (i < n) {
+      const double ai = av ? av[i] : expo;
       const double e = exp(f[i]);
-      const double W = -expo * e;
-      const double gi = -expo * e + y[i];
+      const double W = -ai * e;
+      const double gi = -ai * e + y[i];
       const double zi = Z[i], iz = zinv[i];
       const double om = 1.0 - zi * W;
       const double gp = gi + (-iz * (f[i] - mu[i]) + iz * y1[i]);
@@ -155,6 +161,7 @@ __global__ void __launch_bounds__(256) k_lap_grad_a(int64_t n, int64_t n_pad,
                                                     const double* __restrict__ mu,
                                                     const double* __restrict__ Z,
                                                     const double* __restrict__ zinv, double expo,
+                                                    const double* __restrict__ av,
                                                     const double* __restrict__ y1,
                                                     const double* __restrict__ p,
                                                     double* __restrict__ c2,
@@ -165,13 +172,14 @@ __global__ void __launch_bounds__(256) k_lap_grad_a(int64_t n, int64_t n_pad,
                                                     double* __restrict__ bsv) {
   ROW_LOOP(i) {
     if (i < n) {
+      const double ai = av ? av[i] : expo;
       const double e = exp(f[i]);
-      const double W = -expo * e, W3 = W;
+      const double W = -ai * e, W3 = W;
       const double zi = Z[i], iz = zinv[i];
       const double bi = 1.0 / (zi - 1.0 / W);
       const double pi = p[i];
       if (y1) c2[i] = iz * (f[i] - mu[i]) - iz * y1[i];   // else c2 came with p (fused alpha)
-      g[i] = -expo * e + y[i];
+      g[i] = -ai * e + y[i];
       B[i] = bi;
       dMt[i] = bi - bi * bi * pi;
       const double D = W - 1.0 / zi;
@@ -309,6 +317,7 @@ struct LapPassArgs {
   const double *y, *mu, *Z, *zinv;
   const double *g_in, *omzw_in, *y1_in;       // B
   double expo, tol;                           // A
+  const double* av;                           // A: per-row exposure (nullptr: expo)
   double *y1, *g, *omzw, *v, *gpsi;           // A outputs
   double* part;                               // [nch][mp]
   double* sc;                                 // [nch][NS]
@@ -373,9 +382,10 @@ __global__ void __launch_bounds__(256, OCC) k_lap_rowstream(const double* __rest
         if (im < n) {
           const double fi = pa.f[im], yi = pa.y[im], mui = pa.mu[im], zi = pa.Z[im];
           const double iz = pa.zinv[im];
+          const double ai = pa.av ? pa.av[im] : pa.expo;
           const double e = exp(fi);
-          const double W = -pa.expo * e;
-          const double gi = -pa.expo * e + yi;
+          const double W = -ai * e;
+          const double gi = -ai * e + yi;
           const double om = 1.0 - zi * W;
           const double gp = gi + (-iz * (fi - mui) + iz * dme);
           vme = (1.0 / om) * gp;
@@ -545,23 +555,24 @@ hipError_t launch_lap_z(const double* q, int64_t n, int64_t n_pad, double c0, do
 
 hipError_t launch_lap_obj(int64_t n, int64_t n_pad, const double* f, const double* y,
                           const double* mu, const double* Z, const double* zinv, double expo,
-                          double* B, double* rf, double* tv, double* slab, int* nblocks,
-                          hipStream_t s) {
+                          const double* av, double* B, double* rf, double* tv, double* slab,
+                          int* nblocks, hipStream_t s) {
   const int nb = row_blocks(n_pad);
   *nblocks = nb;
   hipLaunchKernelGGL(k_lap_obj, dim3(nb), dim3(256), 0, s, n, n_pad, f, y, mu, Z, zinv, expo,
-                     log(expo), B, rf, tv, slab);
+                     av ? 0.0 : log(expo), av, B, rf, tv, slab);
   return hipGetLastError();
 }
 
 hipError_t launch_lap_nr_a(int64_t n, int64_t n_pad, const double* f, const double* y,
                            const double* mu, const double* Z, const double* zinv, double expo,
-                           const double* y1, double tol, double* g, double* omzw, double* v,
-                           double* gpsi, double* slab, int* nblocks, hipStream_t s) {
+                           const double* av, const double* y1, double tol, double* g,
+                           double* omzw, double* v, double* gpsi, double* slab, int* nblocks,
+                           hipStream_t s) {
   const int nb = row_blocks(n_pad);
   *nblocks = nb;
-  hipLaunchKernelGGL(k_lap_nr_a, dim3(nb), dim3(256), 0, s, n, n_pad, f, y, mu, Z, zinv, expo, y1,
-                     tol, g, omzw, v, gpsi, slab);
+  hipLaunchKernelGGL(k_lap_nr_a, dim3(nb), dim3(256), 0, s, n, n_pad, f, y, mu, Z, zinv, expo, av,
+                     y1, tol, g, omzw, v, gpsi, slab);
   return hipGetLastError();
 }
 
@@ -614,12 +625,12 @@ hipError_t launch_rowpass(const double* K, int64_t n, int64_t n_pad, int64_t mp,
 hipError_t launch_lap_nr_a_fused(const double* K, int64_t n, int64_t n_pad, int64_t mp,
                                  const double* x1, const double* f, const double* y,
                                  const double* mu, const double* Z, const double* zinv,
-                                 double expo, double tol, double* y1, double* g, double* omzw,
-                                 double* v, double* gpsi, double* part, int64_t part_cap,
-                                 double* out, double* out_cnt, hipStream_t s) {
+                                 double expo, const double* av, double tol, double* y1, double* g,
+                                 double* omzw, double* v, double* gpsi, double* part,
+                                 int64_t part_cap, double* out, double* out_cnt, hipStream_t s) {
   LapPassArgs pa{};
   pa.x = x1; pa.f = f; pa.y = y; pa.mu = mu; pa.Z = Z; pa.zinv = zinv;
-  pa.expo = expo; pa.tol = tol;
+  pa.expo = expo; pa.av = av; pa.tol = tol;
   pa.y1 = y1; pa.g = g; pa.omzw = omzw; pa.v = v; pa.gpsi = gpsi;
   return launch_rowpass<LAP_PASS_A>(K, n, n_pad, mp, pa, part, part_cap, out, out_cnt, s);
 }
@@ -647,10 +658,11 @@ hipError_t launch_lap_nr_b(int64_t n, int64_t n_pad, double* f, const double* mu
 
 hipError_t launch_lap_grad_a(int64_t n, int64_t n_pad, const double* f, const double* y,
                              const double* mu, const double* Z, const double* zinv, double expo,
-                             const double* y1, const double* p, double* c2, double* g, double* B,
-                             double* dMt, double* sv, double* bsv, hipStream_t s) {
+                             const double* av, const double* y1, const double* p, double* c2,
+                             double* g, double* B, double* dMt, double* sv, double* bsv,
+                             hipStream_t s) {
   hipLaunchKernelGGL(k_lap_grad_a, dim3(row_blocks(n_pad)), dim3(256), 0, s, n, n_pad, f, y, mu,
-                     Z, zinv, expo, y1, p, c2, g, B, dMt, sv, bsv);
+                     Z, zinv, expo, av, y1, p, c2, g, B, dMt, sv, bsv);
   return hipGetLastError();
 }
 

@@ -32,20 +32,17 @@
 #include <string.h>
 
 #include <atomic>
-#include <chrono>
-#include <condition_variable>
+#include <cmath>
 #include <functional>
-#include <mutex>
+#include <memory>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "sgp_internal.h"
 #include "sgp_multi.h"
+#include "sgp_pool.h"
 
 namespace {
-
-constexpr int ABORTED = -1;   // a worker that stopped because another one failed
 
 // RCCL, bound at the first multi-device context rather than at load time: a process that also
 // runs torch.distributed carries torch's own librccl (NEEDED as "librccl.so", SONAME
@@ -59,6 +56,7 @@ struct Rccl {
   ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                              hipStream_t) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
   bool ok = false;
   std::string err;
@@ -81,9 +79,11 @@ const Rccl& rccl() {
     x.comm_init_all = reinterpret_cast<decltype(x.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
     x.all_reduce = reinterpret_cast<decltype(x.all_reduce)>(dlsym(h, "ncclAllReduce"));
     x.comm_destroy = reinterpret_cast<decltype(x.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    x.comm_abort = reinterpret_cast<decltype(x.comm_abort)>(dlsym(h, "ncclCommAbort"));
     x.error_string = reinterpret_cast<decltype(x.error_string)>(dlsym(h, "ncclGetErrorString"));
-    x.ok = x.comm_init_all && x.all_reduce && x.comm_destroy && x.error_string;
-    if (!x.ok) x.err = "librccl lacks ncclCommInitAll / ncclAllReduce / ncclCommDestroy";
+    x.ok = x.comm_init_all && x.all_reduce && x.comm_destroy && x.comm_abort && x.error_string;
+    if (!x.ok)
+      x.err = "librccl lacks ncclCommInitAll / ncclAllReduce / ncclCommDestroy / ncclCommAbort";
     return x;
   }();
   return r;
@@ -103,12 +103,6 @@ struct Group {
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
   double* red[2] = {nullptr, nullptr};   // summed buffers (ping-pong)
-  // results of the last job (every group computes the same; group 0's are returned)
-  int status = SGP_OK;
-  std::string err;
-  double obj = 0.0;
-  std::vector<double> grad;
-  int nr_iters = 0;
 };
 
 struct PartPtrs {
@@ -141,144 +135,15 @@ struct MultiCtx {
   int d = 0;
   bool knot_on = false;
   std::vector<double> xmin, xmax;   // column ranges of all rows
-
-  // ---- workers: the calling thread runs group 0, one thread each the other groups.  Hand-offs
-  // spin (bounded, then yield / sleep on the condition variable): a condition-variable wake-up
-  // costs tens to hundreds of microseconds, paid at the start of every evaluation and at every
-  // barrier (measured: the builder started ~0.4 ms after the previous evaluation's readback
-  // with blocking hand-offs)
-  static constexpr int SPIN = 1 << 16;
-  std::vector<std::thread> threads;
-  std::mutex mu;
-  std::condition_variable cv_job;
-  std::function<int(int)> job;
-  std::atomic<uint64_t> job_gen{0};
-  std::atomic<int> pending{0};
-  std::atomic<bool> quit{false};
-
-  // ---- barrier with a vote (all ok? any / all done?)
-  std::mutex bmu;
-  std::atomic<uint64_t> b_gen{0};
-  int b_count = 0;
-  bool b_all_ok = true, b_any = false, b_all = true;
-  bool r_ok = true, r_any = false, r_all = true;
-
-  static void relax(int& spins) {
-    if (++spins < SPIN) {
-      __builtin_ia32_pause();
-    } else {
-      std::this_thread::yield();
-    }
-  }
-
-  void run_group(int g, const std::function<int(int)>& f) {
-    Group& gr = groups[(size_t)g];
-    gr.err.clear();
-    gr.status = f(g);
-    if (gr.status != SGP_OK && gr.status != ABORTED) gr.err = sgp_last_error();
-  }
-
-  void worker(int g) {
-    uint64_t seen = 0;
-    for (;;) {
-      int spins = 0;
-      while (job_gen.load(std::memory_order_acquire) == seen && !quit.load()) {
-        if (spins < SPIN) {
-          relax(spins);
-        } else {   // idle for long: sleep until the next job
-          std::unique_lock<std::mutex> lk(mu);
-          cv_job.wait_for(lk, std::chrono::milliseconds(2), [&] {
-            return quit.load() || job_gen.load(std::memory_order_acquire) != seen;
-          });
-        }
-      }
-      if (quit.load()) return;
-      seen = job_gen.load(std::memory_order_acquire);
-      run_group(g, job);
-      pending.fetch_sub(1, std::memory_order_acq_rel);
-    }
-  }
-
-  void start_workers() {
-    for (int g = 1; g < (int)groups.size(); ++g) threads.emplace_back([this, g] { worker(g); });
-  }
-
-  void stop_workers() {
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      quit.store(true);
-    }
-    cv_job.notify_all();
-    for (std::thread& t : threads) t.join();
-    threads.clear();
-  }
-
-  // run f(g) for every group (group 0 on this thread) and wait; the first real error is
-  // reported
-  int run_all(std::function<int(int)> f) {
-    const int G = (int)groups.size();
-    if (G > 1) {
-      {
-        std::lock_guard<std::mutex> lk(mu);
-        job = f;
-        pending.store(G - 1, std::memory_order_release);
-        job_gen.fetch_add(1, std::memory_order_acq_rel);
-      }
-      cv_job.notify_all();
-    }
-    run_group(0, f);
-    int spins = 0;
-    while (pending.load(std::memory_order_acquire) > 0) relax(spins);
-    int st = SGP_OK;
-    for (const Group& g : groups)
-      if (g.status != SGP_OK && g.status != ABORTED) {
-        sgp_internal_set_err(g.err.c_str());
-        return g.status;
-      }
-    for (const Group& g : groups)
-      if (g.status == ABORTED) st = SGP_EHIP;
-    if (st) sgp_internal_set_err("multi-device evaluation aborted");
-    return st;
-  }
-
-  // every group arrives with its status (and a done flag); returns false for all when any
-  // group failed, and sets *any_done / *all_done from the votes
-  bool arrive(bool ok, bool done = false, bool* any_done = nullptr, bool* all_done = nullptr) {
-    const int G = (int)groups.size();
-    if (G == 1) {
-      if (any_done) *any_done = done;
-      if (all_done) *all_done = done;
-      return ok;
-    }
-    uint64_t gen;
-    bool last = false;
-    {
-      std::lock_guard<std::mutex> lk(bmu);
-      gen = b_gen.load(std::memory_order_relaxed);
-      b_all_ok = b_all_ok && ok;
-      b_any = b_any || done;
-      b_all = b_all && done;
-      if (++b_count == G) {
-        r_ok = b_all_ok;
-        r_any = b_any;
-        r_all = b_all;
-        b_all_ok = true;
-        b_any = false;
-        b_all = true;
-        b_count = 0;
-        last = true;
-        b_gen.store(gen + 1, std::memory_order_release);
-      }
-    }
-    if (!last) {
-      int spins = 0;
-      while (b_gen.load(std::memory_order_acquire) == gen) relax(spins);
-    }
-    std::lock_guard<std::mutex> lk(bmu);   // r_* of this round: the next round needs every group
-    if (any_done) *any_done = r_any;
-    if (all_done) *all_done = r_all;
-    return r_ok;
-  }
+  // the host workers (sgp_pool.h: one per distinct device, barriers with votes, the job bodies)
+  std::unique_ptr<sgp_pool::Pool> pool;
+  std::vector<sgp_pool::Result> res;   // per group; every group computes the same, group 0's
+                                       // are returned
+  // a collective failed to enqueue on one device after its peers' were queued: the
+  // communicators are aborted and rebuilt before any stream of this context is synchronised
+  std::atomic<bool> broken{false};
+  bool dead = false;   // the rebuild failed: every evaluation is refused
+  std::string dead_msg;
 
   sgp_ctx* ctx(const Group& g, int q) { return shards[(size_t)g.shards[(size_t)q]].ctx; }
   // where shard q of group g writes its partial sums (straight into the summed buffer when
@@ -288,8 +153,7 @@ struct MultiCtx {
   }
 
   // the device's shards' partials -> red (fixed shard order)
-  void sum_parts(Group& g, double* red, int64_t count, int& st) {
-    if (st != SGP_OK || g.shards.size() < 2 || count <= 0) return;
+  int sum_parts(Group& g, double* red, int64_t count) {
     PartPtrs pp{};
     pp.k = (int)g.shards.size();
     for (int q = 0; q < pp.k; ++q) pp.p[q] = shards[(size_t)g.shards[(size_t)q]].part;
@@ -299,32 +163,31 @@ struct MultiCtx {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       sgp_internal_set_err(hip_msg(e, "k_sum_parts").c_str());
-      st = SGP_EHIP;
+      return SGP_EHIP;
     }
+    return SGP_OK;
   }
 
   // the all-reduce over the devices, in place on the device's stream
-  void all_reduce(Group& g, double* red, int64_t count, int& st) {
-    if (st != SGP_OK || count <= 0) return;
+  int all_reduce(Group& g, double* red, int64_t count) {
+#ifdef SGP_PROBE_BUILD
+    // fault injection (probe builds only): SGP_PROBE_FAIL_COLLECTIVE=<device> makes that
+    // device's next collective fail to enqueue after its peers' were queued
+    static const char* fail = getenv("SGP_PROBE_FAIL_COLLECTIVE");
+    if (fail && atoi(fail) == g.device) {
+      sgp_internal_set_err("RCCL all-reduce failed: injected (SGP_PROBE_FAIL_COLLECTIVE)");
+      return SGP_EHIP;
+    }
+#endif
     const ncclResult_t r = rccl().all_reduce(red, red, (size_t)count, ncclDouble, ncclSum, g.comm,
                                              g.stream);
     if (r != ncclSuccess) {
       char b[256];
       snprintf(b, sizeof(b), "RCCL all-reduce failed: %s", rccl().error_string(r));
       sgp_internal_set_err(b);
-      st = SGP_EHIP;
+      return SGP_EHIP;
     }
-  }
-
-  // partials summed on the device, a barrier, then the collective.  false: some worker failed
-  // before the barrier, stop now (nobody enters the collective).  A failure of the collective
-  // itself is left in st and stops every worker at the next barrier (or ends the job), so no
-  // worker is ever left waiting at a barrier the failed one will not reach.
-  bool reduce(Group& g, double* red, int64_t count, int& st) {
-    sum_parts(g, red, count, st);
-    if (!arrive(st == SGP_OK)) return false;
-    all_reduce(g, red, count, st);
-    return true;
+    return SGP_OK;
   }
 
   int set_dev(const Group& g) {
@@ -336,8 +199,61 @@ struct MultiCtx {
     return SGP_OK;
   }
 
+  // one communicator per distinct device, all in this process
+  int init_comms() {
+    std::vector<ncclComm_t> comms(groups.size());
+    std::vector<int> devs;
+    for (const Group& g : groups) devs.push_back(g.device);
+    const ncclResult_t r = rccl().comm_init_all(comms.data(), (int)devs.size(), devs.data());
+    if (r != ncclSuccess) {
+      char b[256];
+      snprintf(b, sizeof(b), "ncclCommInitAll over %d devices failed: %s", (int)devs.size(),
+               rccl().error_string(r));
+      sgp_internal_set_err(b);
+      return SGP_EHIP;
+    }
+    for (size_t g = 0; g < comms.size(); ++g) groups[g].comm = comms[g];
+    return SGP_OK;
+  }
+
+  // after a broken collective: abort every communicator (its queued collectives exit), drain
+  // the streams, rebuild the communicators.  The evaluation's own error stays the reported one.
+  void recover() {
+    if (!broken.load()) return;
+    broken.store(false);
+    for (Group& g : groups) {
+      (void)hipSetDevice(g.device);
+      if (g.comm) (void)rccl().comm_abort(g.comm);
+      g.comm = nullptr;
+    }
+    for (Group& g : groups) {
+      (void)hipSetDevice(g.device);
+      if (g.stream) (void)hipStreamSynchronize(g.stream);
+    }
+    const std::string keep = sgp_last_error();
+    if (init_comms() != SGP_OK) {
+      dead = true;
+      dead_msg = std::string("multi-device context unusable: rebuilding its communicators after "
+                             "a failed collective failed (") + sgp_last_error() + ")";
+    }
+    sgp_internal_set_err(keep.c_str());
+  }
+
+  // run a job on every group (sgp_pool.h), then the communicator repair it may need
+  int run(const std::function<int(int)>& job) {
+    if (dead) {
+      sgp_internal_set_err(dead_msg.c_str());
+      return SGP_EHIP;
+    }
+    std::string msg;
+    const int st = pool->run_all(job, &msg);
+    if (st) sgp_internal_set_err(msg.c_str());
+    recover();
+    return st;
+  }
+
   void release() {
-    if (!threads.empty()) stop_workers();
+    pool.reset();   // joins the workers
     for (Group& g : groups) {
       (void)hipSetDevice(g.device);
       if (g.stream) (void)hipStreamSynchronize(g.stream);
@@ -364,6 +280,10 @@ struct MultiCtx {
     shards.clear();
   }
 };
+
+namespace {
+std::string last_error_copy() { return sgp_last_error(); }
+}  // namespace
 
 // ------------------------------------------------------------------------------ creation
 int multi_create(MultiCtx** out, const int* devices, int nshards, const double* X, int64_t n,
@@ -437,29 +357,16 @@ int multi_create(MultiCtx** out, const int* devices, int nshards, const double* 
     sgp_internal_set_err(rccl().err.c_str());
     st = SGP_EHIP;
   }
-  if (!st) {
-    std::vector<ncclComm_t> comms(mc->groups.size());
-    std::vector<int> devs;
-    for (const Group& g : mc->groups) devs.push_back(g.device);
-    const ncclResult_t r = rccl().comm_init_all(comms.data(), (int)devs.size(), devs.data());
-    if (r != ncclSuccess) {
-      char b[256];
-      snprintf(b, sizeof(b), "ncclCommInitAll over %d devices failed: %s", (int)devs.size(),
-               rccl().error_string(r));
-      sgp_internal_set_err(b);
-      st = SGP_EHIP;
-    } else {
-      for (size_t g = 0; g < comms.size(); ++g) mc->groups[g].comm = comms[g];
-    }
-  }
+  if (!st) st = mc->init_comms();
   if (st) {
     mc->release();
     delete mc;
     return st;
   }
-  mc->start_workers();
+  mc->pool.reset(new sgp_pool::Pool((int)mc->groups.size(), last_error_copy));
+  mc->res.assign(mc->groups.size(), sgp_pool::Result{});
   // the shards' contexts, created by their device's worker (uploads run side by side)
-  st = mc->run_all([&](int gi) {
+  st = mc->run([&](int gi) {
     Group& g = mc->groups[(size_t)gi];
     int s2 = mc->set_dev(g);
     for (size_t q = 0; q < g.shards.size() && !s2; ++q) {
@@ -504,7 +411,7 @@ int multi_set_data(MultiCtx* mc, const double* y, const double* mu) {
   return SGP_OK;
 }
 
-// ------------------------------------------------------------------------------ VI / FITC
+// ------------------------------------------------------------------------------ evaluations
 namespace {
 
 struct EvalArgs {
@@ -519,50 +426,67 @@ struct EvalArgs {
   int maxit = 0;
 };
 
+// sgp_pool.h's operations on the HIP contexts and the RCCL communicators
+struct HipOps {
+  MultiCtx* mc;
+  const EvalArgs& a;
+  bool fitc;
+
+  int begin(int g) { return mc->set_dev(mc->groups[(size_t)g]); }
+  int shards(int g) { return (int)mc->groups[(size_t)g].shards.size(); }
+  double* red(int g, int b) { return mc->groups[(size_t)g].red[b]; }
+  double* out_of(int g, int q, double* r) { return mc->out_of(mc->groups[(size_t)g], q, r); }
+  sgp_ctx* ctx(int g, int q) { return mc->ctx(mc->groups[(size_t)g], q); }
+  int phase1(int g, int q, double* out) {
+    return fitc ? sgp_fitc_phase1(ctx(g, q), a.kernel, a.theta, a.U, a.m, a.ldu, a.delta, out)
+                : sgp_vi_phase1(ctx(g, q), a.kernel, a.theta, a.U, a.m, a.ldu, a.delta, out);
+  }
+  int phase2(int g, int q, const double* red1, double* out) {
+    return fitc ? sgp_fitc_phase2(ctx(g, q), red1, mc->n, a.flags, out)
+                : sgp_vi_phase2(ctx(g, q), red1, mc->n, a.flags, out);
+  }
+  int finish(int g, int q, const double* red2, double* obj, double* grad) {
+    return fitc ? sgp_fitc_finish(ctx(g, q), red2, obj, grad)
+                : sgp_vi_finish(ctx(g, q), red2, obj, grad);
+  }
+  int lap_begin(int g, int q, double* out, int64_t* count) {
+    return sgp_lap_begin(ctx(g, q), a.kernel, a.theta, a.U, a.m, a.ldu, a.delta, a.expo, a.tol,
+                         a.maxit, a.flags, out, count);
+  }
+  int lap_step(int g, int q, const double* in, double* out, int64_t* count, int* done,
+               double* obj, double* grad, int* nr_iters) {
+    return sgp_lap_step(ctx(g, q), in, out, count, done, obj, grad, nr_iters);
+  }
+  int sum_parts(int g, double* r, int64_t count) {
+    return mc->sum_parts(mc->groups[(size_t)g], r, count);
+  }
+  int all_reduce(int g, double* r, int64_t count) {
+    return mc->all_reduce(mc->groups[(size_t)g], r, count);
+  }
+  void collective_broken() { mc->broken.store(true); }
+  void set_err(const char* msg) { sgp_internal_set_err(msg); }
+};
+
 // VI (fitc = false) or FITC: phase 1 -> all-reduce #1 -> phase 2 -> all-reduce #2 -> finish
-int two_phase_job(MultiCtx* mc, int gi, const EvalArgs& a, bool fitc) {
-  Group& g = mc->groups[(size_t)gi];
-  int st = mc->set_dev(g);
-  const int k = (int)g.shards.size();
-  const int npar = sgp_num_params(a.kernel, mc->d);
+int two_phase(MultiCtx* mc, const EvalArgs& a, bool fitc, double* obj, double* grad) {
   const bool obj_only = (a.flags & SGP_FLAG_OBJ_ONLY) != 0;
+  const int npar = sgp_num_params(a.kernel, mc->d);
   const int64_t c1 = fitc ? sgp_fitc_red1_count(a.m) : sgp_vi_red1_packed_count(a.m);
-  for (int q = 0; q < k && !st; ++q) {
-    double* o = mc->out_of(g, q, g.red[0]);
-    st = fitc ? sgp_fitc_phase1(mc->ctx(g, q), a.kernel, a.theta, a.U, a.m, a.ldu, a.delta, o)
-              : sgp_vi_phase1(mc->ctx(g, q), a.kernel, a.theta, a.U, a.m, a.ldu, a.delta, o);
-  }
-  if (!mc->reduce(g, g.red[0], c1, st)) return st ? st : ABORTED;
-  for (int q = 0; q < k && !st; ++q) {
-    double* o = mc->out_of(g, q, g.red[1]);
-    st = fitc ? sgp_fitc_phase2(mc->ctx(g, q), g.red[0], mc->n, a.flags, o)
-              : sgp_vi_phase2(mc->ctx(g, q), g.red[0], mc->n, a.flags, o);
-  }
   // the objective alone leaves the second buffer unwritten: nothing to sum
   const int64_t extra = mc->knot_on ? sgp_knot_red_extra(mc->d, a.m) : 0;
   const int64_t c2 = obj_only ? 0
                               : (fitc ? sgp_fitc_red2_count(a.kernel, mc->d, a.m)
                                       : sgp_vi_red2_count(a.kernel, mc->d)) + extra;
-  if (!mc->reduce(g, g.red[1], c2, st)) return st ? st : ABORTED;
+  HipOps ops{mc, a, fitc};
+  const int st = mc->run([&](int gi) {
+    return sgp_pool::two_phase_job(ops, *mc->pool, gi, c1, c2, obj_only ? 0 : npar,
+                                   mc->res[(size_t)gi]);
+  });
   if (st) return st;
-  g.grad.assign((size_t)(npar > 0 ? npar : 1), 0.0);
-  std::vector<double> tmp(g.grad.size());
-  for (int q = 0; q < k && !st; ++q) {
-    double o = 0.0;
-    double* gp = obj_only ? nullptr : (q == 0 ? g.grad.data() : tmp.data());
-    st = fitc ? sgp_fitc_finish(mc->ctx(g, q), g.red[1], &o, gp)
-              : sgp_vi_finish(mc->ctx(g, q), g.red[1], &o, gp);
-    if (q == 0) g.obj = o;
-  }
-  return st;
-}
-
-int copy_result(MultiCtx* mc, int st, double* obj, double* grad, int npar) {
-  if (st) return st;
-  const Group& g = mc->groups[0];
-  *obj = g.obj;
-  if (grad)
-    for (int p = 0; p < npar; ++p) grad[p] = g.grad[(size_t)p];
+  const sgp_pool::Result& r = mc->res[0];
+  *obj = r.obj;
+  if (grad && !obj_only)
+    for (int p = 0; p < npar; ++p) grad[p] = r.grad[(size_t)p];
   return SGP_OK;
 }
 
@@ -571,97 +495,16 @@ int copy_result(MultiCtx* mc, int st, double* obj, double* grad, int npar) {
 int multi_eval_vi(MultiCtx* mc, int kernel, const double* theta, const double* U, int64_t m,
                   int64_t ldu, double delta, unsigned flags, double* obj, double* grad) {
   const EvalArgs a{kernel, theta, U, m, ldu, delta, flags};
-  const int st = mc->run_all([&](int gi) { return two_phase_job(mc, gi, a, false); });
-  return copy_result(mc, st, obj, (flags & SGP_FLAG_OBJ_ONLY) ? nullptr : grad,
-                     sgp_num_params(kernel, mc->d));
+  return two_phase(mc, a, false, obj, grad);
 }
 
 int multi_eval_fitc(MultiCtx* mc, int kernel, const double* theta, const double* U, int64_t m,
                     int64_t ldu, double delta, unsigned flags, double* obj, double* grad) {
   const EvalArgs a{kernel, theta, U, m, ldu, delta, flags};
-  const int st = mc->run_all([&](int gi) { return two_phase_job(mc, gi, a, true); });
-  return copy_result(mc, st, obj, (flags & SGP_FLAG_OBJ_ONLY) ? nullptr : grad,
-                     sgp_num_params(kernel, mc->d));
+  return two_phase(mc, a, true, obj, grad);
 }
 
-// ------------------------------------------------------------------------------ Laplace
-namespace {
-
-// sgp_lap_begin -> all-reduce -> (sgp_lap_step -> all-reduce)* until done: the NR iterations'
-// two exchanges and the gradient's two
-int laplace_job(MultiCtx* mc, int gi, const EvalArgs& a) {
-  Group& g = mc->groups[(size_t)gi];
-  int st = mc->set_dev(g);
-  const int k = (int)g.shards.size();
-  const int npar = sgp_num_params(a.kernel, mc->d);
-  int64_t count = -1;
-  for (int q = 0; q < k && !st; ++q) {
-    int64_t cq = 0;
-    st = sgp_lap_begin(mc->ctx(g, q), a.kernel, a.theta, a.U, a.m, a.ldu, a.delta, a.expo, a.tol,
-                       a.maxit, a.flags, mc->out_of(g, q, g.red[0]), &cq);
-    if (!st && count >= 0 && cq != count) {
-      sgp_internal_set_err("Laplace shards disagree on the reduction size");
-      st = SGP_EINVAL;
-    }
-    count = cq;
-  }
-  if (!mc->reduce(g, g.red[0], count, st)) return st ? st : ABORTED;
-  g.grad.assign((size_t)(npar > 0 ? npar : 1), 0.0);
-  std::vector<double> tmp(g.grad.size());
-  int cur = 0;
-  for (;;) {
-    bool done = false;
-    int64_t cnt = -1;
-    for (int q = 0; q < k && !st; ++q) {
-      int64_t cq = 0;
-      int dq = 0, it = 0;
-      double o = 0.0;
-      st = sgp_lap_step(mc->ctx(g, q), g.red[cur], mc->out_of(g, q, g.red[cur ^ 1]), &cq, &dq,
-                        &o, q == 0 ? g.grad.data() : tmp.data(), &it);
-      if (st) break;
-      if ((q > 0 && ((dq != 0) != done || cq != cnt))) {
-        sgp_internal_set_err("Laplace shards disagree on the NR state");
-        st = SGP_EINVAL;
-        break;
-      }
-      done = dq != 0;
-      cnt = cq;
-      if (q == 0) {
-        g.obj = o;
-        g.nr_iters = it;
-      }
-    }
-    if (st) {
-      mc->arrive(false, done);
-      return st;
-    }
-    if (done) {
-      // every device must stop here too (the stop rule reads summed buffers only)
-      bool any = false, all = false;
-      if (!mc->arrive(true, true, &any, &all)) return ABORTED;
-      if (!all) {
-        sgp_internal_set_err("Laplace devices disagree on the NR stop rule");
-        return SGP_EINVAL;
-      }
-      return SGP_OK;
-    }
-    // the partials -> the other buffer, summed over the device's shards and the devices (this
-    // device votes "not done" at the barrier; a collective failure stops every worker at the
-    // next barrier, after the next steps are skipped)
-    mc->sum_parts(g, g.red[cur ^ 1], cnt, st);
-    bool any = false;
-    if (!mc->arrive(st == SGP_OK, false, &any)) return st ? st : ABORTED;
-    if (any) {
-      sgp_internal_set_err("Laplace devices disagree on the NR stop rule");
-      return SGP_EINVAL;
-    }
-    mc->all_reduce(g, g.red[cur ^ 1], cnt, st);
-    cur ^= 1;
-  }
-}
-
-}  // namespace
-
+// sgp_lap_begin -> all-reduce -> (sgp_lap_step -> all-reduce)* until done (sgp_pool.h)
 int multi_eval_laplace(MultiCtx* mc, int kernel, const double* theta, const double* U,
                        int64_t m, int64_t ldu, double delta, double expo, double tol, int maxit,
                        unsigned flags, double* obj, double* grad, int* nr_iters) {
@@ -669,13 +512,17 @@ int multi_eval_laplace(MultiCtx* mc, int kernel, const double* theta, const doub
   a.expo = expo;
   a.tol = tol;
   a.maxit = maxit;
-  const int st = mc->run_all([&](int gi) { return laplace_job(mc, gi, a); });
+  const int npar = sgp_num_params(kernel, mc->d);
+  HipOps ops{mc, a, false};
+  const int st = mc->run([&](int gi) {
+    return sgp_pool::laplace_job(ops, *mc->pool, gi, npar, mc->res[(size_t)gi]);
+  });
   if (st) return st;
-  const Group& g = mc->groups[0];
-  if (obj) *obj = g.obj;
-  if (nr_iters) *nr_iters = g.nr_iters;
+  const sgp_pool::Result& r = mc->res[0];
+  if (obj) *obj = r.obj;
+  if (nr_iters) *nr_iters = r.nr_iters;
   if (grad && !(flags & SGP_FLAG_OBJ_ONLY))
-    for (int p = 0; p < sgp_num_params(kernel, mc->d); ++p) grad[p] = g.grad[(size_t)p];
+    for (int p = 0; p < npar; ++p) grad[p] = r.grad[(size_t)p];
   return SGP_OK;
 }
 
@@ -683,6 +530,31 @@ int multi_eval_laplace(MultiCtx* mc, int kernel, const double* theta, const doub
 int multi_lap_set_f(MultiCtx* mc, const double* f, double fill) {
   for (Shard& s : mc->shards) {
     const int st = sgp_lap_set_f(s.ctx, f ? f + s.row0 : nullptr, fill);
+    if (st) return st;
+  }
+  return SGP_OK;
+}
+
+// the per-row exposure in the global row order: every value is checked before any shard
+// changes, so a rejected vector leaves the context as it was
+int multi_lap_set_expo(MultiCtx* mc, const double* a, double fill) {
+  if (!a && !(fill > 0.0 && std::isfinite(fill))) {
+    char b[160];
+    snprintf(b, sizeof(b), "sgp_lap_set_expo: the fill exposure %g is not a positive finite number",
+             fill);
+    sgp_internal_set_err(b);
+    return SGP_EINVAL;
+  }
+  for (int64_t i = 0; a && i < mc->n; ++i)
+    if (!(a[i] > 0.0 && std::isfinite(a[i]))) {
+      char b[160];
+      snprintf(b, sizeof(b), "sgp_lap_set_expo: exposure a[%lld] = %g is not a positive finite "
+               "number", (long long)i, a[i]);
+      sgp_internal_set_err(b);
+      return SGP_EINVAL;
+    }
+  for (Shard& s : mc->shards) {
+    const int st = sgp_lap_set_expo(s.ctx, a ? a + s.row0 : nullptr, fill);
     if (st) return st;
   }
   return SGP_OK;

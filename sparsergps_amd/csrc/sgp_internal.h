@@ -255,6 +255,13 @@ hipError_t dense_spd_inverse(double* A, int64_t mp, double* R, double* P, double
 hipError_t dense_spd_inverse_sum(const double* A0, double beta, const double* B0, double* out,
                                  int64_t mp, double* R, double* P, double* logd, int* status,
                                  unsigned* sync, hipStream_t s);
+// the same with the chain chosen by the caller: the persistent one-launch chain (per_step false;
+// nb <= 64) or one launch per pivot step (any nb) -- bit-identical results (sgp_diag_gj_pair)
+hipError_t dense_spd_inverse_chain(double* A, int64_t mp, double* R, double* P, double* logd,
+                                   int* status, unsigned* sync, hipStream_t s, bool per_step);
+hipError_t dense_spd_inverse_sum_chain(const double* A0, double beta, const double* B0,
+                                       double* out, int64_t mp, double* R, double* P, double* logd,
+                                       int* status, unsigned* sync, hipStream_t s, bool per_step);
 // C = a*A + b*B elementwise over mp x mp
 hipError_t dense_axpby(double a, const double* A, double b, const double* B, double* C,
                        int64_t count, hipStream_t s);
@@ -305,25 +312,27 @@ hipError_t launch_gemv_cols(const double* K, int64_t n_pad, int64_t mp, const do
                             int64_t ldv, int nv, double* part, int64_t part_cap, double* out,
                             hipStream_t s);
 int64_t lap_gemv_cols_slab(int64_t n_pad, int64_t mp, int nv);
-// Poisson-Laplace per-row steps (see k_lap.hip for the formulas and reference lines).
+// Poisson-Laplace per-row steps (see k_lap.hip for the formulas and reference lines).  av: the
+// per-row exposure (n_pad values) or nullptr for the scalar expo on every row.
 hipError_t launch_lap_z(const double* q, int64_t n, int64_t n_pad, double c0, double* Z,
                         double* zinv, hipStream_t s);
 hipError_t launch_lap_obj(int64_t n, int64_t n_pad, const double* f, const double* y,
                           const double* mu, const double* Z, const double* zinv, double expo,
-                          double* B, double* rf, double* tv, double* slab, int* nblocks,
-                          hipStream_t s);
+                          const double* av, double* B, double* rf, double* tv, double* slab,
+                          int* nblocks, hipStream_t s);
 hipError_t launch_lap_nr_a(int64_t n, int64_t n_pad, const double* f, const double* y,
                            const double* mu, const double* Z, const double* zinv, double expo,
-                           const double* y1, double tol, double* g, double* omzw, double* v,
-                           double* gpsi, double* slab, int* nblocks, hipStream_t s);
+                           const double* av, const double* y1, double tol, double* g,
+                           double* omzw, double* v, double* gpsi, double* slab, int* nblocks,
+                           hipStream_t s);
 // NR part a as one K pass (y1 = K x1, the row update above, out = K^T v, out_cnt = stop-rule
 // count); mp <= 2048; part: lap_rowpass_slab(n_pad, mp) doubles.
 hipError_t launch_lap_nr_a_fused(const double* K, int64_t n, int64_t n_pad, int64_t mp,
                                  const double* x1, const double* f, const double* y,
                                  const double* mu, const double* Z, const double* zinv,
-                                 double expo, double tol, double* y1, double* g, double* omzw,
-                                 double* v, double* gpsi, double* part, int64_t part_cap,
-                                 double* out, double* out_cnt, hipStream_t s);
+                                 double expo, const double* av, double tol, double* y1, double* g,
+                                 double* omzw, double* v, double* gpsi, double* part,
+                                 int64_t part_cap, double* out, double* out_cnt, hipStream_t s);
 // NR part b + the next objective's t as one K pass: f updated in place (y2 = K x2), out_t =
 // K^T tv and out_rr = sum tv (f - mu) at the new f, tv = (f - mu)/Z.  mp <= 2048.
 hipError_t launch_lap_nr_b_t_fused(const double* K, int64_t n, int64_t n_pad, int64_t mp,
@@ -339,8 +348,9 @@ hipError_t launch_lap_nr_b(int64_t n, int64_t n_pad, double* f, const double* mu
                            const double* y2, hipStream_t s);
 hipError_t launch_lap_grad_a(int64_t n, int64_t n_pad, const double* f, const double* y,
                              const double* mu, const double* Z, const double* zinv, double expo,
-                             const double* y1, const double* p, double* c2, double* g, double* B,
-                             double* dMt, double* sv, double* bsv, hipStream_t s);
+                             const double* av, const double* y1, const double* p, double* c2,
+                             double* g, double* B, double* dMt, double* sv, double* bsv,
+                             hipStream_t s);
 hipError_t launch_lap_grad_b(int64_t n, int64_t n_pad, const double* B, const double* sv,
                              const double* y3, const double* dMt, const double* c2,
                              const double* g, double* h, double* a, double* slab, int* nblocks,

@@ -35,6 +35,7 @@ int multi_eval_laplace(MultiCtx* mc, int kernel, const double* theta, const doub
                        int64_t m, int64_t ldu, double delta, double expo, double tol, int maxit,
                        unsigned flags, double* obj, double* grad, int* nr_iters);
 int multi_lap_set_f(MultiCtx* mc, const double* f, double fill);
+int multi_lap_set_expo(MultiCtx* mc, const double* a, double fill);
 int multi_lap_get_f(MultiCtx* mc, double* f);
 int multi_lap_get_grad_psi(MultiCtx* mc, double* out);
 int multi_enable_knot_grad(MultiCtx* mc, int enable);

@@ -33,6 +33,10 @@
 //   SGP_GJ_GMAX         workgroups of a persistent Gauss-Jordan chain (at most)
 //   SGP_CHAIN_US_STEP   chain_shared_rb's model of a K22 chain beside the builder: us per
 //   SGP_CHAIN_US_FIX    64-wide step, and fixed us
+// Fault injection (environment, read by probe builds only; the product ignores it):
+//   SGP_PROBE_GJ_WITHHOLD=<ticket>  the process's first persistent Gauss-Jordan launch skips the
+//                       flag publish of that task ticket, so the chain's watchdog must fire
+//                       (tests/test_gpu_gj.py)
 #pragma once
 
 #if (defined(SGP_CON_TRACE) || defined(SGP_CON_NO_EPILOGUE) || defined(SGP_GJ_TRACE) ||       \

@@ -228,6 +228,27 @@ class SparseGPContext:
             f = np.ascontiguousarray(np.broadcast_to(np.asarray(f, dtype=np.float64), (self.n,)))
             _lib.check(self._lib.sgp_lap_set_f(self.handle, _lib.dptr(f), 0.0))
 
+    def lap_set_expo(self, a=None, fill=1.0):
+        """Resident per-row Poisson exposure (the reference's `m` as a vector of cell areas,
+        R/derivative_functions_of_data_likelihoods.R:38); a=None fills every row with `fill`."""
+        if a is None:
+            _lib.check(self._lib.sgp_lap_set_expo(self.handle, None, float(fill)))
+        else:
+            a = np.ascontiguousarray(np.asarray(a, dtype=np.float64).reshape(-1))
+            if a.size != self.n:
+                raise ValueError(f"exposure has {a.size} values for {self.n} rows")
+            _lib.check(self._lib.sgp_lap_set_expo(self.handle, _lib.dptr(a), 0.0))
+
+    def _expo(self, expo):
+        """The expo argument of the Laplace entry points: a scalar as is; an n-vector is made
+        resident (sgp_lap_set_expo) and passed as SGP_EXPO_ROWS.  A length-1 vector is the
+        scalar (R recycling)."""
+        a = np.asarray(expo, dtype=np.float64)
+        if a.size == 1:
+            return float(a.reshape(-1)[0])
+        self.lap_set_expo(a)
+        return _lib.SGP_EXPO_ROWS
+
     def lap_get_f(self):
         f = np.zeros(self.n, dtype=np.float64)
         _lib.check(self._lib.sgp_lap_get_f(self.handle, _lib.dptr(f)))
@@ -256,7 +277,7 @@ class SparseGPContext:
         it = C.c_int(0)
         grad = np.zeros(theta.size, dtype=np.float64)
         _lib.check(self._lib.sgp_eval_laplace(self.handle, _lib.KERNELS[cov_fun], _lib.dptr(theta),
-                                              _lib.dptr(U), m, m, float(delta), float(expo),
+                                              _lib.dptr(U), m, m, float(delta), self._expo(expo),
                                               float(tol), int(maxit), C.byref(obj),
                                               _lib.dptr(grad), C.byref(it)))
         return obj.value, grad, it.value
@@ -298,7 +319,7 @@ class SparseGPContext:
         out = np.zeros(T, dtype=np.float64)
         _lib.check(self._lib.sgp_lap_candidates(self.handle, _lib.KERNELS[cov_fun],
                                                 _lib.dptr(theta), _lib.dptr(U), m, m,
-                                                float(delta), float(expo), float(tol),
+                                                float(delta), self._expo(expo), float(tol),
                                                 int(maxit), _lib.dptr(Cd), T, T, _lib.dptr(out)))
         return out
 
@@ -310,7 +331,7 @@ class SparseGPContext:
         obj = C.c_double(0.0)
         it = C.c_int(0)
         _lib.check(self._lib.sgp_lap_nr(self.handle, _lib.KERNELS[cov_fun], _lib.dptr(theta),
-                                        _lib.dptr(U), m, m, float(delta), float(expo), float(tol),
+                                        _lib.dptr(U), m, m, float(delta), self._expo(expo), float(tol),
                                         int(maxit), C.byref(obj), C.byref(it)))
         return obj.value, it.value
 
@@ -322,7 +343,7 @@ class SparseGPContext:
         U, m = self._knots(xu)
         cnt = C.c_int64(0)
         _lib.check(self._lib.sgp_lap_begin(self.handle, _lib.KERNELS[cov_fun], _lib.dptr(theta),
-                                           _lib.dptr(U), m, m, float(delta), float(expo),
+                                           _lib.dptr(U), m, m, float(delta), self._expo(expo),
                                            float(tol), int(maxit),
                                            self._flags(False, obj_only), C.c_void_p(red_ptr),
                                            C.byref(cnt)))

@@ -46,17 +46,21 @@ def make_gaussian_problem(config, n=None, m=None, d=None):
     return dict(X=X, U=U, y=y, mu=mu, cov_par=cov_par, cov_fun=cov_fun, delta=1e-6)
 
 
-def make_poisson_problem(n=None, m=None):
-    """C5: Poisson Laplace, n=5e5, m=512, d=5, sqexp, theta=(1, 2, 0.1); seeds X=8, U=9, y=10."""
+def make_poisson_problem(n=None, m=None, per_row_exposure=False):
+    """C5: Poisson Laplace, n=5e5, m=512, d=5, sqexp, theta=(1, 2, 0.1); seeds X=8, U=9, y=10.
+
+    per_row_exposure: a_i ~ U(0.5, 2) (seed 11) -- the reference's `m` as "a vector of the areas
+    of each grid cell" (R/derivative_functions_of_data_likelihoods.R:38) -- instead of a = 1;
+    y ~ Poisson(a_i e^f_i) and f0 = log(mean y) - log(a) per row (R/optimize_gp.R:480)."""
     n = n or 500_000
     m = m or 512
     d = 5
     X = _rng(8).uniform(0.0, 10.0, size=(n, d))
     U = _rng(9).uniform(0.0, 10.0, size=(m, d))
     f = 0.5 * np.sin(X).sum(axis=1) / math.sqrt(d) + math.log(2.0)
-    a = 1.0
+    a = _rng(11).uniform(0.5, 2.0, size=n) if per_row_exposure else 1.0
     y = _rng(10).poisson(a * np.exp(f)).astype(np.float64)
     mu = np.full(n, math.log(y.mean()))
-    f0 = np.full(n, math.log(y.mean()) - math.log(a))
+    f0 = math.log(y.mean()) - np.log(a) * np.ones(n)
     cov_par = OrderedDict([("sigma", 1.0), ("l", 2.0), ("tau", 0.1)])
     return dict(X=X, U=U, y=y, mu=mu, f0=f0, a=a, cov_par=cov_par, cov_fun="sqexp", delta=1e-6)

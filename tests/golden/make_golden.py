@@ -7,6 +7,7 @@ the reference formulas -- after it has been pinned independently by tests/test_o
 
     python tests/golden/make_golden.py        # all fixtures
     python tests/golden/make_golden.py own    # only the C2 (m=256) / C5 (m=512) fixtures
+    python tests/golden/make_golden.py expo   # only the per-row exposure Poisson fixture
 """
 import os
 import sys
@@ -41,8 +42,8 @@ def gauss_case(name, cfg, n, m, coincide=False):
          fitc_obj=np.array(fitc_obj), fitc_grad=np.array([fitc_grad[k] for k in cp]))
 
 
-def poisson_case(name, n, m):
-    P = O.make_poisson_problem(n=n, m=m)
+def poisson_case(name, n, m, per_row_exposure=False):
+    P = O.make_poisson_problem(n=n, m=m, per_row_exposure=per_row_exposure)
     cp = P["cov_par"]
     nr = O.newtrap_sparseGP(P["f0"], cp, "sqexp", P["X"], P["U"], P["y"], P["mu"], P["a"],
                             tol=1e-5)
@@ -81,10 +82,20 @@ def own_knot_counts():
     poisson_case("poisson_c5_m512.npz", 2000, 512)
 
 
+def per_row_exposure():
+    """Poisson with the exposure `m` as one value per row (a vector of cell areas,
+    R/derivative_functions_of_data_likelihoods.R:38; optimize_gp.R:461-468 passes it through)."""
+    poisson_case("poisson_c5_expo.npz", 400, 24, per_row_exposure=True)
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["own"]:
         own_knot_counts()
         sys.exit(0)
+    if sys.argv[1:] == ["expo"]:
+        per_row_exposure()
+        sys.exit(0)
+    per_row_exposure()
     own_knot_counts()
     fill_case("fills.npz")
     gauss_case("gauss_c2_small.npz", "C2", 200, 16)

@@ -120,6 +120,7 @@ static void einval_checks(void) {
   EINVAL_(sgp_fitc_phase2(NULL, buf, 1, 0u, buf));
   EINVAL_(sgp_fitc_finish(NULL, buf, &o, buf));
   EINVAL_(sgp_lap_set_f(NULL, buf, 0.0));
+  EINVAL_(sgp_lap_set_expo(NULL, buf, 1.0));
   EINVAL_(sgp_lap_get_f(NULL, buf));
   EINVAL_(sgp_lap_objective_values(NULL, buf, 4, &ci));
   EINVAL_(sgp_eval_laplace(NULL, 1, th, buf, 1, 1, 1e-6, 1.0, 1e-5, 10, &o, buf, &it));

@@ -1,6 +1,7 @@
 """C-ABI checks that need no GPU: libsgp.so builds for gfx950, loads, exports every symbol
 include/sgp.h declares, and its host-only entry points behave (values, errors)."""
 import ctypes as C
+import glob
 import os
 import re
 
@@ -11,6 +12,7 @@ from oracle import sgp_oracle as O
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "sgp.h")
+HEADERS = sorted(glob.glob(os.path.join(ROOT, "include", "*.h")))   # sgp.h + sgp_diag.h
 
 
 @pytest.fixture(scope="module")
@@ -19,14 +21,18 @@ def lib():
     return _lib.lib()
 
 
-def declared_functions():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(sgp_[a-z0-9_]+)\s*\(", text)))
+def declared_functions(paths=HEADERS):
+    names = set()
+    for p in paths:
+        text = re.sub(r"/\*.*?\*/", "", open(p).read(), flags=re.S)
+        names.update(re.findall(r"\b(sgp_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
 
 
 def test_header_declares_expected_api():
+    assert HEADER in HEADERS and len(HEADERS) >= 2
     names = declared_functions()
+    assert "sgp_diag_gj_pair" in names and "sgp_lap_set_expo" in names
     for must in ("sgp_make_cov", "sgp_dsig_dtheta", "sgp_ctx_create", "sgp_eval_vi",
                  "sgp_vi_phase1", "sgp_vi_phase2", "sgp_vi_finish", "sgp_last_error"):
         assert must in names

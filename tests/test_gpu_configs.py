@@ -47,6 +47,7 @@ POIS = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLD, "poisson
 
 def test_fixture_lists_cover_own_knot_counts():
     assert "gauss_c2_m256.npz" in GAUSS and "poisson_c5_m512.npz" in POIS
+    assert "poisson_c5_expo.npz" in POIS
 
 
 @pytest.mark.parametrize("name", GAUSS)
@@ -66,7 +67,8 @@ def test_golden_gaussian_vi_fitc(sgp, name):
 def test_golden_poisson_laplace(sgp, name):
     z = np.load(os.path.join(GOLD, name))
     cp = _cp(z)
-    r = sgp.laplace_eval(cp, "sqexp", z["U"], z["X"], z["y"], z["mu"], z["f0"], float(z["a"]),
+    a = z["a"] if z["a"].ndim else float(z["a"])   # poisson_c5_expo: one exposure per row
+    r = sgp.laplace_eval(cp, "sqexp", z["U"], z["X"], z["y"], z["mu"], z["f0"], a,
                          float(z["delta"]), tol=1e-5)
     tr = z["obj_trace"]
     assert r["nr_iter"] == len(tr)
@@ -154,6 +156,39 @@ def test_c5_full_size_against_chunked_laplace_model(sgp):
     assert abs(obj - o) / abs(o) < 1e-9
     assert np.max(np.abs(fg - f)) < 1e-8
     assert _rel(grad, g) < 1e-7
+
+
+def test_c5_full_size_per_row_exposure_against_chunked_laplace_model(sgp):
+    """configs[4]'s shape with the exposure `m` as one value per row (a vector of cell areas,
+    R/derivative_functions_of_data_likelihoods.R:7-61; optimize_gp.R:461-468 passes `a` through
+    unchanged): the resident exposure (sgp_lap_set_expo, expo = SGP_EXPO_ROWS) against
+    adjoint_chunked.eval_laplace with the same vector (pinned to the literal oracle with per-row
+    exposure in tests/test_oracle.py).  NR count exact, NR objectives 1e-9, mode 1e-8, gradient
+    1e-7; then a scalar evaluation on the same context ignores the resident vector."""
+    from oracle import adjoint_chunked as AC
+    from sparsergps_amd.workloads import make_poisson_problem
+    P = make_poisson_problem(per_row_exposure=True)
+    assert P["X"].shape == (500_000, 5) and np.ndim(P["a"]) == 1
+    th = np.array(list(P["cov_par"].values()))
+    o, g, f, objs = AC.eval_laplace("sqexp", th, P["X"], P["y"], P["mu"], P["U"], P["f0"], P["a"],
+                                    P["delta"], tol=1e-5)
+    with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=512) as ctx:
+        ctx.lap_set_f(P["f0"])
+        obj, grad, nit = ctx.eval_laplace(th, "sqexp", P["U"], P["delta"], P["a"], 1e-5, 1000)
+        fg = ctx.lap_get_f()
+        ov = ctx.lap_objective_values()
+        assert nit == len(objs) == len(ov)
+        np.testing.assert_allclose(ov, objs, rtol=1e-9, atol=0)
+        assert abs(obj - o) / abs(o) < 1e-9
+        assert np.max(np.abs(fg - f)) < 1e-8
+        assert _rel(grad, g) < 1e-7
+        # a positive scalar still means that exposure on every row (resident vector unused)
+        ctx.lap_set_f(P["f0"][:1].repeat(P["X"].shape[0]))
+        o1, _, _ = ctx.eval_laplace(th, "sqexp", P["U"], P["delta"], 1.0, 1e-5, 1000)
+        o1c, _, _, _ = AC.eval_laplace("sqexp", th, P["X"], P["y"], P["mu"], P["U"],
+                                       P["f0"][:1].repeat(P["X"].shape[0]), 1.0, P["delta"],
+                                       tol=1e-5)
+        assert abs(o1 - o1c) / abs(o1c) < 1e-9
 
 
 def test_c3_headline_shape_against_chunked_adjoint_model(sgp):

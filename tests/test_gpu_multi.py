@@ -75,7 +75,8 @@ def test_one_device_rccl_laplace_against_golden(sgp, name):
     with sgp.SparseGPContext(z["X"], z["y"], z["mu"], m_max=z["U"].shape[0],
                              devices=[0]) as ctx:
         ctx.lap_set_f(z["f0"])
-        o, g, it = ctx.eval_laplace(th, "sqexp", z["U"], float(z["delta"]), float(z["a"]), 1e-5)
+        a = z["a"] if z["a"].ndim else float(z["a"])   # poisson_c5_expo: per-row exposure
+        o, g, it = ctx.eval_laplace(th, "sqexp", z["U"], float(z["delta"]), a, 1e-5)
         tr = z["obj_trace"]
         assert it == len(tr)
         np.testing.assert_allclose(ctx.lap_objective_values(), tr, rtol=1e-9, atol=0)
@@ -153,6 +154,52 @@ def test_laplace_shards_match_one_context(sgp):
     assert a["nr"][1] == b["nr"][1] and abs(a["nr"][0] - b["nr"][0]) / abs(b["nr"][0]) < 1e-11
 
 
+def test_per_row_exposure_on_three_shards(sgp):
+    """A per-row Poisson exposure (the reference's `m` as a vector of cell areas,
+    R/derivative_functions_of_data_likelihoods.R:7-61) on 3 ragged shards of one GPU: the
+    frozen oracle fixture (NR count exact, objectives 1e-9, gradient 1e-7) and, at n = 30 001,
+    the one-context run (the exposure split by rows like X).  A rejected vector (a zero) leaves
+    the resident one in place; expo = SGP_EXPO_ROWS without a vector is refused."""
+    from sparsergps_amd import _lib
+    from sparsergps_amd.workloads import make_poisson_problem
+    z = np.load(os.path.join(GOLD, "poisson_c5_expo.npz"))
+    th = np.asarray(z["theta"], dtype=np.float64)
+    with sgp.SparseGPContext(z["X"], z["y"], z["mu"], m_max=z["U"].shape[0],
+                             devices=[0, 0, 0]) as ctx:
+        assert ctx.shards() == (3, 1)
+        L = _lib.lib()
+        ctx.lap_set_f(z["f0"])
+        with pytest.raises(_lib.SGPError):   # no per-row exposure yet
+            ctx.eval_laplace(th, "sqexp", z["U"], float(z["delta"]), _lib.SGP_EXPO_ROWS, 1e-5)
+        o, g, it = ctx.eval_laplace(th, "sqexp", z["U"], float(z["delta"]), z["a"], 1e-5)
+        assert it == len(z["obj_trace"])
+        np.testing.assert_allclose(ctx.lap_objective_values(), z["obj_trace"], rtol=1e-9, atol=0)
+        assert np.max(np.abs(ctx.lap_get_f() - z["ff"])) < 1e-8
+        assert _rel(g, z["grad"]) < GRAD_RTOL
+        bad = z["a"].copy()
+        bad[250] = 0.0
+        with pytest.raises(_lib.SGPError, match=r"a\[250\]"):
+            ctx.lap_set_expo(bad)
+        ctx.lap_set_f(z["f0"])   # the resident exposure is still z["a"]
+        o2, g2, it2 = ctx.eval_laplace(th, "sqexp", z["U"], float(z["delta"]),
+                                       _lib.SGP_EXPO_ROWS, 1e-5)
+        assert it2 == it and o2 == o and np.array_equal(g2, g)
+        assert L.sgp_lap_set_expo(ctx.handle, None, -1.0) == _lib.SGP_EINVAL
+    P = make_poisson_problem(n=30_001, m=128, per_row_exposure=True)
+    th = np.array(list(P["cov_par"].values()))
+    res = {}
+    for key, dv in (("one", None), ("multi", [0] * 3)):
+        with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=128, devices=dv) as c:
+            c.lap_set_f(P["f0"])
+            o, g, it = c.eval_laplace(th, "sqexp", P["U"], P["delta"], P["a"], 1e-5, 1000)
+            res[key] = (o, g, it, c.lap_get_f())
+    a, b = res["multi"], res["one"]
+    assert a[2] == b[2]
+    assert abs(a[0] - b[0]) / abs(b[0]) < SAME_RTOL
+    assert _rel(a[1], b[1]) < 1e-10
+    assert np.max(np.abs(a[3] - b[3])) < 1e-10
+
+
 def test_candidates_on_shards(sgp):
     """VI and FITC OAT scoring on a sharded context equal the one-device scorers (VI: bordered
     Schur complements there, objective-only evaluations at [U; x*] here)."""
@@ -200,6 +247,15 @@ def test_refused_entry_points_and_recovery(sgp):
             c.eval_full(th, "sqexp", P["delta"])
         with pytest.raises(_lib.SGPError):
             c.eval_vi(np.array([1.0, 1.0, -0.5]), "sqexp", P["U"], P["delta"])
+        # the VI candidate forward checks U / m / ldu like the FITC and Laplace ones
+        cand = np.asfortranarray(P["X"][:2])
+        out = np.zeros(2)
+        for U_, m_, ldu_ in ((None, 32, 32), (np.asfortranarray(P["U"]), 32, 31),
+                             (np.asfortranarray(P["U"]), 0, 32)):
+            st = L.sgp_vi_candidates(c.handle, 0, _lib.dptr(th),
+                                     None if U_ is None else _lib.dptr(U_), m_, ldu_, 1e-6, 0,
+                                     _lib.dptr(cand), 2, 2, _lib.dptr(out))
+            assert st == _lib.SGP_EINVAL, (m_, ldu_)
         o, g = c.eval_vi(th, "sqexp", P["U"], P["delta"])
     with sgp.SparseGPContext(P["X"], P["y"], P["mu"], m_max=32) as one:
         o1, g1 = one.eval_vi(th, "sqexp", P["U"], P["delta"])

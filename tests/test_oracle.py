@@ -220,13 +220,15 @@ def test_golden_gaussian(name):
     assert np.allclose(list(O.dlogp_dcov_par(*args)["gradient"].values()), z["fitc_grad"], rtol=1e-11, atol=1e-11)
 
 
-@pytest.mark.parametrize("name", ["poisson_c5_small.npz", "poisson_c5_m512.npz"])
+@pytest.mark.parametrize("name", ["poisson_c5_small.npz", "poisson_c5_m512.npz",
+                                  "poisson_c5_expo.npz"])
 def test_golden_poisson(name):
     z = np.load(os.path.join(GOLD, name))
     cp = OrderedDict(zip([str(s) for s in z["names"]], z["theta"]))
-    nr = O.newtrap_sparseGP(z["f0"], cp, "sqexp", z["X"], z["U"], z["y"], z["mu"], float(z["a"]), tol=1e-5)
+    a = z["a"] if z["a"].ndim else float(z["a"])    # per-row exposure in poisson_c5_expo
+    nr = O.newtrap_sparseGP(z["f0"], cp, "sqexp", z["X"], z["U"], z["y"], z["mu"], a, tol=1e-5)
     assert np.allclose(nr["gp"], z["ff"], rtol=1e-12, atol=1e-12)
-    g = O.dlogq_dcov_par(cp, "sqexp", z["U"], z["X"], z["y"], nr["gp"], z["mu"], float(z["a"]))["gradient"]
+    g = O.dlogq_dcov_par(cp, "sqexp", z["U"], z["X"], z["y"], nr["gp"], z["mu"], a)["gradient"]
     assert np.allclose(list(g.values()), z["grad"], rtol=1e-10, atol=1e-10)
 
 
@@ -292,6 +294,36 @@ def test_chunked_laplace_model_matches_literal(cov_fun, coinc, n, m):
     assert o == objs[-1]
     assert np.max(np.abs(f - nr["gp"])) < 1e-10
     assert np.max(np.abs(grad - g) / np.maximum(1, np.abs(g))) < 1e-10
+
+
+def test_chunked_laplace_model_per_row_exposure():
+    """A per-row exposure (the reference's `m` as a vector of cell areas,
+    R/derivative_functions_of_data_likelihoods.R:38, used element-wise at l.7-30 and in
+    obj_fun_pois, R/laplace_approx_obj_funs.R:125-129): adjoint_chunked.eval_laplace (the GPU's
+    full-size checker) equals the literal oracle, and a constant vector equals the scalar."""
+    from oracle import adjoint_chunked as AC
+    P = O.make_poisson_problem(n=600, m=20, per_row_exposure=True)
+    assert np.ndim(P["a"]) == 1 and np.ptp(P["a"]) > 1.0
+    cp = P["cov_par"]
+    th = np.array(list(cp.values()))
+    nr = O.newtrap_sparseGP(P["f0"], cp, "sqexp", P["X"], P["U"], P["y"], P["mu"], P["a"],
+                            P["delta"], tol=1e-5)
+    g = np.array(list(O.dlogq_dcov_par(cp, "sqexp", P["U"], P["X"], P["y"], nr["gp"], P["mu"],
+                                       P["a"], P["delta"])["gradient"].values()))
+    o, grad, f, objs = AC.eval_laplace("sqexp", th, P["X"], P["y"], P["mu"], P["U"], P["f0"],
+                                       P["a"], P["delta"], tol=1e-5, chunk=128)
+    np.testing.assert_allclose(objs, nr["objective_function_values"], rtol=1e-12, atol=0)
+    assert np.max(np.abs(f - nr["gp"])) < 1e-10
+    assert np.max(np.abs(grad - g) / np.maximum(1, np.abs(g))) < 1e-10
+    # the exposure matters (a scalar 1 gives another answer) and a constant vector is the scalar
+    o1 = AC.eval_laplace("sqexp", th, P["X"], P["y"], P["mu"], P["U"], P["f0"], 1.0,
+                         P["delta"], tol=1e-5, chunk=128)[0]
+    assert abs(o1 - o) > 1.0
+    oc = AC.eval_laplace("sqexp", th, P["X"], P["y"], P["mu"], P["U"], P["f0"],
+                         np.full(600, 1.3), P["delta"], tol=1e-5, chunk=128)
+    os_ = AC.eval_laplace("sqexp", th, P["X"], P["y"], P["mu"], P["U"], P["f0"], 1.3,
+                          P["delta"], tol=1e-5, chunk=128)
+    assert oc[0] == os_[0] and np.array_equal(oc[1], os_[1])
 
 
 @pytest.mark.parametrize("cfg", ["C2", "C3"])

@@ -411,6 +411,28 @@ def test_multi_device_context_routines(gR):
                                atol=1e-9)
     np.testing.assert_allclose(out["gradient"], z["grad"], rtol=1e-7, atol=1e-8)
     R.call("sgp_R_ctx_destroy", multi)
+    # a per-row exposure `m` (R/derivative_functions_of_data_likelihoods.R:38, a vector of cell
+    # areas) through the same routine: one context and three shards against the frozen oracle
+    z = np.load(os.path.join(GOLD, "poisson_c5_expo.npz"))
+    X, U, y, mu, th, av = z["X"], z["U"], z["y"], z["mu"], z["theta"], z["a"]
+    delta, m = float(z["delta"]), U.shape[0]
+    tr = z["obj_trace"]
+    for dv in (None, [0.0, 0.0, 0.0]):
+        c = R.call("sgp_R_ctx_create", X, y, mu, float(m + 1), dv)
+        R.call("sgp_R_lap_set_f", c, z["f0"])
+        out = R.call("sgp_R_eval_laplace", c, "sqexp", th, U, delta, av, 1e-5, 1000.0,
+                     R.lgl(True)).py()
+        assert out["nr_iter"][0] == len(tr), dv
+        np.testing.assert_allclose(R.call("sgp_R_lap_objective_values", c).py(), tr, rtol=1e-9)
+        np.testing.assert_allclose(out["gradient"], z["grad"], rtol=1e-7, atol=1e-8)
+        assert "length 1 or one value per row" in _err(R, "sgp_R_eval_laplace", c, "sqexp", th,
+                                                      U, delta, av[:7], 1e-5, 1000.0,
+                                                      R.lgl(True))
+        bad = av.copy()
+        bad[3] = -1.0
+        assert "a[3]" in _err(R, "sgp_R_eval_laplace", c, "sqexp", th, U, delta, bad, 1e-5,
+                              1000.0, R.lgl(True))
+        R.call("sgp_R_ctx_destroy", c)
     _GPU_DONE.append("test_multi_device_context_routines")
 
 
