@@ -282,7 +282,8 @@ class NumpyLaplaceRank:
         B = W / (Z * W - 1.0)
         r = f - self.mu
         K = self.K
-        logpy = np.sum(self.y * math.log(a) - _lgamma1(self.y) - a * np.exp(f) + self.y * f)
+        # a: the exposure, a scalar or this rank's rows (R/laplace_approx_obj_funs.R:125-129)
+        logpy = np.sum(self.y * np.log(a) - _lgamma1(self.y) - a * np.exp(f) + self.y * f)
         return [(K.T @ (B[:, None] * K)).reshape(-1), K.T @ (r / Z),
                 np.array([r @ (r / Z), logpy, np.sum(np.log(1.0 - W * Z))])]
 

@@ -917,7 +917,9 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   if (e == hipSuccess) e = upload_rows(c->y, y, n, np_);
   if (e == hipSuccess) e = upload_rows(c->mu, mu, n, np_);
   if (e == hipSuccess) e = launch_dot(c->r, c->r, np_, c->slab_aux, c->rr_dev, c->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  // the set-up's hipMemset calls (sync words, tickets, K) run on the null stream, which the
+  // context's non-blocking streams do not wait for: finish them before the first evaluation
+  if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     set_err("HIP error '%s' uploading data", hipGetErrorString(e));
     ctx_free(c);
@@ -1916,6 +1918,8 @@ static int lap_ensure(sgp_ctx* c) {
   if (st) return st;
   HIPCHK(hipMemset(c->lv, 0, sizeof(double) * LV_N * np_));
   HIPCHK(hipMemset(c->lm, 0, sizeof(double) * LM_N * mp));
+  // (null-stream memsets: done before the Laplace kernels run on the context's streams)
+  HIPCHK(hipDeviceSynchronize());
   return SGP_OK;
 }
 
@@ -2613,8 +2617,10 @@ int sgp_predict(int device, int kernel, const double* theta, double delta, int m
     HIPCHK(hipMemcpy(Xp.p, hX.data(), sizeof(double) * hX.size(), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(wv.p + mp, hd.data(), sizeof(double) * mp, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(V.p, hV.data(), sizeof(double) * mm, hipMemcpyHostToDevice));
-    HIPCHK(hipMemset(status.p, 0, sizeof(int) * 4));
-    HIPCHK(hipMemset(gsync.p, 0, sizeof(int) * SGP_GJ_SYNC_WORDS));
+    // on the launch stream: the null stream's hipMemset is not ordered before a non-blocking
+    // stream's kernels (the chain's sync words must be zero when it starts)
+    HIPCHK(hipMemsetAsync(status.p, 0, sizeof(int) * 4, s));
+    HIPCHK(hipMemsetAsync(gsync.p, 0, sizeof(int) * SGP_GJ_SYNC_WORDS, s));
   }
   // Sigma22: the gaussian family subtracts tau^2 I again (vi_functions.R:1246-1260,
   // laplace_approx_prediction.R:25-43) -> diagonal sigma^2 + delta; otherwise Kuu+(tau^2+delta)I
@@ -2947,6 +2953,9 @@ int sgp_diag_gj_pair(int device, int64_t m, const double* A, const double* B, do
   HIPCHK(hipMemcpy(dInvA.p, hA.data(), sizeof(double) * mm, hipMemcpyHostToDevice));
   HIPCHK(hipMemset(status.p, 0, sizeof(int) * 4));
   HIPCHK(hipMemset(sync.p, 0, sizeof(int) * 2 * SGP_GJ_SYNC_WORDS));
+  // hipMemset runs on the null stream, which non-blocking streams do not wait for: the chains'
+  // sync words must be zero before either chain starts
+  HIPCHK(hipDeviceSynchronize());
   unsigned* sy = reinterpret_cast<unsigned*>(sync.p);
   // both chains in flight together, as VI's phase 2 issues them
   HIPCHK(dense_spd_inverse_chain(dInvA.p, mp, R1.p, P1.p, L1.p, status.p, sy + SGP_GJ_SYNC_WORDS,

@@ -207,7 +207,9 @@ class RowShardedLaplace:
         self.collective = self.world > 1 or force
 
     def eval(self, theta, U, delta=1e-6, expo=1.0, tol=1e-5, maxit=1000):
-        """-> (objective, gradient d/dlog theta, NR iteration count)"""
+        """-> (objective, gradient d/dlog theta, NR iteration count).  expo: the Poisson
+        exposure, a scalar or THIS rank's rows of a per-row exposure (the reference's `m` as a
+        vector of cell areas, R/derivative_functions_of_data_likelihoods.R:38)."""
         b = self.backend
         with (b.stream_context() if hasattr(b, "stream_context") else contextlib.nullcontext()):
             red = b.lap_begin(theta, U, delta, expo, tol, maxit)

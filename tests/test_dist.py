@@ -116,20 +116,22 @@ class NumpyLaplaceBackend:
         return torch.from_numpy(nxt), False, None
 
 
-def _lap_worker(rank, world, port, n, m, q):
+def _lap_worker(rank, world, port, n, m, q, per_row=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from oracle import sgp_oracle as O
-        P = O.make_poisson_problem(n=n, m=m)
+        P = O.make_poisson_problem(n=n, m=m, per_row_exposure=per_row)
         U = P["U"].copy()
         U[:2] = P["X"][[1, n - 2]]                      # coincident knots on both shards
         s0, s1 = shard_rows(n, world, rank)
         be = NumpyLaplaceBackend(P["X"][s0:s1], P["y"][s0:s1], P["mu"][s0:s1], P["f0"][s0:s1],
                                  "sqexp")
         theta = np.array(list(P["cov_par"].values()))
-        obj, grad, it = RowShardedLaplace(be).eval(theta, U, P["delta"], P["a"], 1e-5, 1000)
+        # a per-row exposure travels with its rows: each rank passes its own slice
+        expo = P["a"][s0:s1] if per_row else P["a"]
+        obj, grad, it = RowShardedLaplace(be).eval(theta, U, P["delta"], expo, 1e-5, 1000)
         if rank == 0:
             nr = O.newtrap_sparseGP(P["f0"], P["cov_par"], "sqexp", P["X"], U, P["y"], P["mu"],
                                     P["a"], P["delta"], tol=1e-5)
@@ -143,12 +145,13 @@ def _lap_worker(rank, world, port, n, m, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_row_sharded_laplace_gloo(world):
+@pytest.mark.parametrize("world,per_row", [(2, False), (3, False), (2, True)])
+def test_row_sharded_laplace_gloo(world, per_row):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_lap_worker, args=(r, world, port, 301, 19, q)) for r in range(world)]
+    procs = [ctx.Process(target=_lap_worker, args=(r, world, port, 301, 19, q, per_row))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

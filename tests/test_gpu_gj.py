@@ -60,11 +60,15 @@ def test_persistent_chain_is_bit_identical_to_per_step(L, m):
     beta = 4.0
     p = _pair(L, A, B, beta, 0)
     s = _pair(L, A, B, beta, 1)
-    again = _pair(L, A, B, beta, 0)
-    for a, b, c, what in zip(p, s, again, ("inv(A)", "inv(A + beta B)", "log dets")):
+    for a, b, what in zip(p, s, ("inv(A)", "inv(A + beta B)", "log dets")):
         assert np.array_equal(a, b), f"{what}: persistent != per-step at m = {m} " \
                                      f"(max diff {np.max(np.abs(a - b)):.3e})"
-        assert np.array_equal(a, c), f"{what}: persistent chain not repeatable at m = {m}"
+    # the hand-offs under repetition: every run of the two concurrent persistent chains gives
+    # the same bits (a visibility race would show as a changed tile or a failed pivot)
+    for rep in range(8 if m < 4096 else 3):
+        again = _pair(L, A, B, beta, 0)
+        for a, c, what in zip(p, again, ("inv(A)", "inv(A + beta B)", "log dets")):
+            assert np.array_equal(a, c), f"{what}: persistent chain run {rep + 2} differs at m = {m}"
     S = A + beta * B
     eye = np.eye(m)
     assert np.max(np.abs(p[0] @ A - eye)) < 1e-9
@@ -105,8 +109,8 @@ CHILD = textwrap.dedent("""
             print("ERR", e.status, str(e).replace(chr(10), " "))
         print("SECONDS", time.time() - t0)
         o, g = ctx.eval_vi(th, "sqexp", P["U"], P["delta"])
-        print("OBJ", repr(o))
-        print("GRAD", " ".join(repr(v) for v in g))
+        print("OBJ", repr(float(o)))
+        print("GRAD", " ".join(repr(float(v)) for v in g))
 """)
 
 

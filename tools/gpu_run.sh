@@ -13,6 +13,7 @@
 #     c2x4              four C2 lines in a row (the C2 measure) -> $D/c2_*.json
 #     pmc               WRITE_SIZE / FETCH_SIZE passes of the bench command (one counter set
 #                       per run, kernel trace only) -> $D/pmc_*/
+#     builderpmc        counter passes over tools/builder_probe.py (K12 builder + store ceiling)
 #     ab:TAG:REPS:VARS:ARGS   tools/ab.sh TAG REPS "VARS" ARGS (ARGS with '+' for spaces)
 set -o pipefail
 D=gpurun_out/${OUT:-run}
@@ -62,6 +63,16 @@ for step in "$@"; do
         timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $ctr --output-format csv -d "$D/pmc_$ctr" -o run -- \
           python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$D/pmc_$ctr.json" 2> "$D/pmc_$ctr.err" || { tail -20 "$D/pmc_$ctr.err"; exit 1; }
         echo "pmc $ctr done"
+      done ;;
+    builderpmc)
+      # the K12 builder and the store ceiling kernel in one process, one counter set per run
+      i=0
+      for set in "WRITE_SIZE" "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_LEVEL_sum" "TCC_EA0_WRREQ_STALL_sum" \
+                 "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_WR SQ_INST_CYCLES_VMEM_WR SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE"; do
+        i=$((i + 1))
+        timeout -s KILL 180 rocprofv3 --kernel-trace --pmc $set --output-format csv -d "$D/bpmc_$i" -o run -- \
+          python3 tools/builder_probe.py > "$D/bpmc_$i.log" 2>&1 || { tail -20 "$D/bpmc_$i.log"; exit 1; }
+        tail -1 "$D/bpmc_$i.log"
       done ;;
     ab:*)
       IFS=: read -r _ tag reps vars args <<< "$step"
