@@ -14,7 +14,7 @@ import argparse
 import csv
 import json
 
-KERNEL_MATCH = "k_contract<8, 0, false, false, false>"   # VI "contract_knm" (EPI_GRAD, GEMM k-loop)
+KERNEL_MATCH = "k_contract<8, 0, false, false, false, true, false>"   # VI "contract_knm" (EPI_GRAD, GEMM k-loop)
 
 
 def per_launch(path, counter, match):
