@@ -238,6 +238,11 @@ struct sgp_ctx {
   int* status = nullptr;
   double *red1 = nullptr, *red2 = nullptr;
   double *slab_syrk = nullptr, *slab_con = nullptr, *slab_small = nullptr, *sc = nullptr;
+  // the balanced gradient contraction's hand-over slots and flags (k_contract_sk)
+  double* sk_ws = nullptr;
+  unsigned* sk_flags = nullptr;
+  unsigned sk_epoch = 0;
+  int sk_slots = 0;
   double* tslab = nullptr;                // builder t = K^T r partials (VI), n_pad/64 x mp
   // stored products of the FITC / Laplace row-quadratic passes (n_pad x mp each, allocated on
   // first use): tq = K K22^-1, tp = K Bm^-1 (FITC) or K C (Laplace).  The gradient
@@ -445,6 +450,10 @@ static bool chain_watchdog(const int* status) {
       set_err("internal error: a Gauss-Jordan chain's wait watchdog expired");
       return true;
     }
+  if (status[3] < 0) {
+    set_err("internal error: the gradient contraction's hand-over wait watchdog expired");
+    return true;
+  }
   return false;
 }
 
@@ -494,6 +503,7 @@ void ctx_free(sgp_ctx* c) {
                   c->K22inv, c->Bm,    c->Binv,   c->Pm,      c->Xt,    c->T1,   c->M3,
                   c->dinv,   c->logd22, c->logdB, c->uvec,    c->cdiag, c->status, c->red1,
                   c->red2,   c->slab_syrk, c->slab_con, c->slab_small, c->slab_aux, c->sc,
+                  c->sk_ws,  c->sk_flags,
                   c->Xt22,   c->T22,    c->dinv22, c->omega, c->pvec, c->rowq, c->red2f,
                   c->y,      c->mu,     c->lv,     c->lm,    c->lslab, c->lred[0], c->lred[1],
                   c->Cprev,  c->knot_slab, c->knot_part, c->knot_kmm, c->tslab, c->tq, c->tp,
@@ -868,6 +878,20 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->red2f, sgp_fitc_red2_count(SGP_KERNEL_ARD, SGP_MAXD, m_max) + mp * d);
   st = st ? st : dalloc(&c->slab_syrk, c->slab_syrk_cap);
   st = st ? st : dalloc(&c->slab_con, c->slab_con_cap);
+  {   // resident workgroups of the contraction: two per CU
+    int cus = 0;
+    if (!st && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) ==
+                   hipSuccess && cus > 0)
+      c->sk_slots = 2 * cus;
+    if (c->sk_slots > 0) {
+      st = st ? st : dalloc(&c->sk_ws, sgp_con_sk_doubles(c->sk_slots));
+      st = st ? st : dalloc(&c->sk_flags, c->sk_slots + 1);
+      if (!st && hipMemset(c->sk_flags, 0, sizeof(unsigned) * (c->sk_slots + 1)) != hipSuccess) {
+        set_err("hipMemset of the contraction hand-over flags failed");
+        st = SGP_EHIP;
+      }
+    }
+  }
   // small-reduction partials: the dot/colsum helpers, and k_contract_kmm's one record per knot
   c->slab_small_cap = std::max<int64_t>(SLAB_SMALL, mp * (SGP_MAXD + 2));
   st = st ? st : dalloc(&c->slab_small, c->slab_small_cap);
@@ -1129,6 +1153,17 @@ static int contract_pass(sgp_ctx* c, const double* M, ConArgs ca, double* rec_ou
   if (c->knot_on) ca.knot_slab = c->knot_slab;
   const bool fused = ca.uvec != nullptr && ca.alpha_in == nullptr;
   if (fused) ca.alpha_out = c->alpha;   // k_coinc needs the fused alpha_i
+  // the balanced launch where the tile grid leaves a mostly idle last round (SGP_CON_SK=0 in the
+  // environment: always the one-tile grid, for A/B runs and the equivalence test)
+  static const bool sk_off = getenv("SGP_CON_SK") && atoi(getenv("SGP_CON_SK")) == 0;
+  if (c->sk_ws && !sk_off) {
+    if (++c->sk_epoch == 0) ++c->sk_epoch;   // 0 is the flags' initial value
+    ca.sk_ws = c->sk_ws;
+    ca.sk_flags = c->sk_flags;
+    ca.sk_epoch = c->sk_epoch;
+    ca.sk_slots = c->sk_slots;
+    ca.sk_status = c->status + 3;
+  }
   HIPCHK(launch_contract_args(c->kp, c->K, M, c->X, c->n_pad, c->n, c->n_pad, c->U, c->mp, c->m,
                               c->mp, ca, c->slab_con, &nrec, &nwg, c->stream));
   // the per-tile records summed, and tau's coincidence sums added to record fields 1+L .. 3+L

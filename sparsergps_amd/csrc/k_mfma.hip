@@ -952,29 +952,49 @@ enum { EPI_GRAD = 0, EPI_ROWQUAD = 1 };
 
 // KU (row quadratic forms without u: the Z pass): false compiles the K u fold out of the k-loop
 // T2 (FROM_T only): a second stored product folded in (ConArgs::tin2)
-template <int DT, int EPI, bool V2 = false, bool KNOT = false, bool FROM_T = false, bool KU = true,
-          bool T2 = false>
-__global__ void __launch_bounds__(256, 2)
-k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict__ M,
-           const double* __restrict__ X, int64_t ldx, int64_t n, int64_t n_pad,
-           const double* __restrict__ U, int64_t ldu, int64_t m, int64_t mp, ConArgs ca,
-           double* __restrict__ slab, int nrec, double* __restrict__ rowq) {
+constexpr int CON_A_SZ = T128 * SA;   // 2176 (keeps the B image 16-byte aligned)
+constexpr int CON_B_SZ = BK * SB;     // 2304
+constexpr int CON_LDS = 2 * (CON_A_SZ + CON_B_SZ);
+
+// The part of a tile's k range one workgroup computes (k_contract_sk, the balanced launch): the
+// whole range (CON_FULL, also every tile of k_contract), its tail (CON_TAIL: the partial product
+// and partial K u are handed to the workgroup that holds the head, no epilogue) or its head
+// (CON_HEAD: adds the handed-over tail, then the epilogue)
+enum { CON_FULL = 0, CON_TAIL = 1, CON_HEAD = 2 };
+constexpr int64_t CON_SK_SLOT = 65 * 256;   // doubles per hand-over slot: 64 accumulators + K u
+struct ConSK {
+  double* ws = nullptr;          // [slots][CON_SK_SLOT]
+  unsigned* flags = nullptr;     // per slot: the launch epoch once the slot is written
+  unsigned epoch = 0;
+  int64_t slot = 0;              // CON_TAIL: the slot written; CON_HEAD: the slot read
+  int* status = nullptr;         // -1: a hand-over wait expired (reported by the host)
+};
+
+__device__ __forceinline__ unsigned con_ldu_sc1(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// SKM: which hand-over code is compiled in -- 0 none (CON_FULL), CON_TAIL (the body ends after
+// the k-loop), CON_HEAD (`part` chooses at run time between CON_HEAD and CON_FULL).  The tail and
+// the head never share one copy of the body: compiled together the accumulators spilled
+// ~250 VGPRs
+template <int DT, int EPI, bool V2, bool KNOT, bool FROM_T, bool KU, bool T2, int SKM>
+__device__ __forceinline__ void con_tile(
+    const KernParams& kp, const double* __restrict__ K, const double* __restrict__ M,
+    const double* __restrict__ X, int64_t ldx, int64_t n, int64_t n_pad,
+    const double* __restrict__ U, int64_t ldu, int64_t m, int64_t mp, const ConArgs& ca,
+    double* __restrict__ slab, int nrec, double* __restrict__ rowq, int64_t ti, int64_t tj,
+    int64_t wgid, int kb, int ke, double* lds, double (*red)[SGP_MAXD + 5], double (*s_uk)[BK],
+    const ConSK& sk, int part, int tid_in) {
   const double* __restrict__ r = ca.r;
   const double* __restrict__ uvec = ca.uvec;
   const double* __restrict__ cdiag = ca.cdiag;
-  constexpr int A_SZ = T128 * SA;   // 2176 (keeps the B image 16-byte aligned)
-  constexpr int B_SZ = BK * SB;     // 2304
-  __shared__ __attribute__((aligned(16))) double lds[2 * (A_SZ + B_SZ)];
-  __shared__ double red[4][SGP_MAXD + 5];
-  __shared__ double s_uk[2][BK];   // u slice of the staged k-step (fused alpha)
-
+  constexpr int A_SZ = CON_A_SZ, B_SZ = CON_B_SZ;
   const int64_t ntj = mp / T128;
-  const int64_t nwg = (n_pad / T128) * ntj;
-  const int64_t wgid = xcd_remap(blockIdx.x, nwg);
-  const int64_t ti = wgid / ntj, tj = wgid % ntj;
+  const int64_t nwg = (n_pad / T128) * ntj;   // tiles (the record slab's row length)
   const int64_t i0 = ti * T128, j0 = tj * T128;
 
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = tid_in, lane = tid & 63, wv = tid >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   const bool with_u = KU && (uvec != nullptr) && (ca.alpha_in == nullptr);   // fuse K u into the loop
   constexpr bool with_v = V2;   // second rank-1 term (Laplace), compiled in only where used
@@ -994,7 +1014,6 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
   const double2* gB = reinterpret_cast<const double2*>(M + (int64_t)bk * mp + j0) + bc;
   const int64_t bstep = BK * mp / 2;
   double2 va0, va1, va2, va3, vb0, vb1, vb2, vb3;
-  const int nsteps = (int)(mp / BK);
   // alpha folded into the k-loop: each thread dots the 8 K values it stages with u.
   double ku = 0.0, vuk = 0.0;
   // the step is one basic block (mfma_interleave): the u slice is fetched, staged and folded
@@ -1043,13 +1062,13 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
           acc[fm][fn][q] = ca.tin[(i0 + wr * 64 + fm * 16 + (lane >> 4) + 4 * q) * mp + j0 +
                                   wc * 64 + fn * 16 + (lane & 15)];
   } else {
-  CON_GLOAD(0);
+  CON_GLOAD(kb);
   CON_SSTORE(0);
   __syncthreads();
-  for (int step = 0; step < nsteps; ++step) {
-    const int cur = step & 1;
+  for (int step = kb; step < ke; ++step) {
+    const int cur = (step - kb) & 1;
     if constexpr (KU) CON_KU(cur);   // va still holds this step's staged K values
-    CON_GLOAD(step + 1 < nsteps ? step + 1 : step);   // the last step reloads its own slice
+    CON_GLOAD(step + 1 < ke ? step + 1 : step);   // the last step reloads its own slice
     const double* As = lds + cur * (A_SZ + B_SZ);
     const double* Bs = As + A_SZ;
 #pragma unroll
@@ -1075,6 +1094,60 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
 #undef CON_GLOAD
 #undef CON_SSTORE
 #undef CON_KU
+
+  if constexpr (SKM == CON_TAIL) {
+    // hand the partial product over: every value stored write-through (sc1), the stores
+    // drained, then the slot's flag (the head's workgroup may run on another XCD)
+    double* w = sk.ws + sk.slot * CON_SK_SLOT;
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          __hip_atomic_store(&w[((fm * 4 + fn) * 4 + q) * 256 + tid], acc[fm][fn][q],
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&w[64 * 256 + tid], ku, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      __hip_atomic_store(&sk.flags[sk.slot], sk.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if (SKM == CON_HEAD && part == CON_HEAD) {
+    // the tail was computed at the start of the next workgroup's range: long done by now.
+    // Watchdog: a wait past ~2^22 polls marks the launch failed and goes on (the grid drains)
+    if (tid == 0) {
+      unsigned it = 0;
+      while (con_ldu_sc1(&sk.flags[sk.slot]) != sk.epoch) {
+        if (++it >= (1u << 22)) {
+          atomicExch(sk.status, -1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    const double* w = sk.ws + sk.slot * CON_SK_SLOT;
+    // in groups of 16 values: the scheduler would otherwise issue all 64 loads up front and
+    // need 128 more VGPRs beside the accumulators
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm) {
+      double t[4][4];
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          t[fn][q] = __hip_atomic_load(&w[((fm * 4 + fn) * 4 + q) * 256 + tid], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[fm][fn][q] += t[fn][q];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    ku += __hip_atomic_load(&w[64 * 256 + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 
   SGP_PROBE_CON_STAMP(1);
   SGP_PROBE_CON_SKIP_EPILOGUE()   // timing probe hook (sgp_probe.h): empty in the product
@@ -1398,6 +1471,77 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
     if (tid < nrec)   // field-major [nrec][nwg]: coalesced for the reduction (launch_rowsum)
       slab[tid * nwg + wgid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
     SGP_PROBE_CON_STAMP(2);
+  }
+}
+
+// one 128 x 128 output tile per workgroup (grid = tiles), XCD-aware tile order
+template <int DT, int EPI, bool V2 = false, bool KNOT = false, bool FROM_T = false, bool KU = true,
+          bool T2 = false>
+__global__ void __launch_bounds__(256, 2)
+k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict__ M,
+           const double* __restrict__ X, int64_t ldx, int64_t n, int64_t n_pad,
+           const double* __restrict__ U, int64_t ldu, int64_t m, int64_t mp, ConArgs ca,
+           double* __restrict__ slab, int nrec, double* __restrict__ rowq) {
+  __shared__ __attribute__((aligned(16))) double lds[CON_LDS];
+  __shared__ double red[4][SGP_MAXD + 5];
+  __shared__ double s_uk[2][BK];   // u slice of the staged k-step (fused alpha)
+  const int64_t ntj = mp / T128;
+  const int64_t nwg = (n_pad / T128) * ntj;
+  const int64_t wgid = xcd_remap(blockIdx.x, nwg);
+  con_tile<DT, EPI, V2, KNOT, FROM_T, KU, T2, 0>(
+      kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, rowq, wgid / ntj, wgid % ntj,
+      wgid, 0, (int)(mp / BK), lds, red, s_uk, ConSK{}, CON_FULL, (int)threadIdx.x);
+}
+
+// The balanced (Stream-K) form of VI's gradient contraction for grids whose last residency
+// round would be mostly empty (C2: 1564 tiles over 512 slots = 3.05 rounds run as 4; the 8-GPU
+// shard: 15.3 as 16).  The tiles' k-steps, in tile order, are split evenly over the G resident
+// workgroups: a workgroup's range starts with the tail of a tile (handed to the previous
+// workgroup, which holds that tile's head at the END of its own range, so it never waits long),
+// then whole tiles, then the head of the next tile.  Every tile gets one epilogue, run by the
+// workgroup that holds its k = 0 step.  Requires range >= k-steps per tile (a tile meets at most
+// two workgroups).
+template <int DT, bool KNOT>
+__global__ void __launch_bounds__(256, 2)
+k_contract_sk(KernParams kp, const double* __restrict__ K, const double* __restrict__ M,
+              const double* __restrict__ X, int64_t ldx, int64_t n, int64_t n_pad,
+              const double* __restrict__ U, int64_t ldu, int64_t m, int64_t mp, ConArgs ca,
+              double* __restrict__ slab, int nrec, ConSK sk) {
+  __shared__ __attribute__((aligned(16))) double lds[CON_LDS];
+  __shared__ double red[4][SGP_MAXD + 5];
+  __shared__ double s_uk[2][BK];
+  const int64_t ntj = mp / T128;
+  const int64_t ntiles = (n_pad / T128) * ntj;
+  const int S = (int)(mp / BK);
+  const int64_t Utot = ntiles * S, G = gridDim.x, w = blockIdx.x;
+  const int64_t u1 = Utot * (w + 1) / G;
+  int64_t u = Utot * w / G;
+  if (u % S != 0) {   // the range starts inside a tile: its tail, handed to workgroup w - 1
+    const int64_t tile = u / S;
+    const int kb = (int)(u % S);
+    ConSK p = sk;
+    p.slot = w;
+    con_tile<DT, EPI_GRAD, false, KNOT, false, true, false, CON_TAIL>(
+        kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, nullptr, tile / ntj,
+        tile % ntj, tile, kb, S, lds, red, s_uk, p, CON_TAIL, (int)threadIdx.x);
+    u += S - kb;
+    __syncthreads();
+  }
+  while (u < u1) {   // whole tiles, then possibly the head of the next (its tail: w + 1's start)
+    const int64_t tile = u / S;
+    const int ke = (int)((u1 - u) < (int64_t)S ? (u1 - u) : S);
+    ConSK p = sk;
+    p.slot = w + 1;
+    // the thread index passed through an opaque move each iteration: every per-thread offset
+    // of the tile body is then recomputed inside the loop instead of hoisted out of it and
+    // kept live across the k-loop
+    int tid;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
+    con_tile<DT, EPI_GRAD, false, KNOT, false, true, false, CON_HEAD>(
+        kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, nullptr, tile / ntj,
+        tile % ntj, tile, 0, ke, lds, red, s_uk, p, ke < S ? CON_HEAD : CON_FULL, tid);
+    u += ke;
+    __syncthreads();   // the next tile's operand staging reuses the epilogue's LDS
   }
 }
 
@@ -2152,12 +2296,32 @@ hipError_t launch_knot_reduce(const double* knot_slab, int64_t ntiles, int64_t m
 
 // dynamic LDS of the gradient-contraction launches: SGP_CON_SHMEM (sgp_probe.h) is 0 in the
 // product; tools/micro/con_trace.hip builds with a pad that leaves one workgroup per CU
+// The balanced launch when the tile grid's last residency round would be mostly empty: more
+// than 2 % of the rounds' capacity idle, and a workgroup's range at least one tile's k-steps
+static bool con_use_sk(const ConArgs& ca, int64_t nwg, int64_t mp) {
+  if (ca.sk_ws == nullptr || ca.sk_slots < 1 || nwg < ca.sk_slots) return false;
+  const int64_t G = ca.sk_slots, S = mp / BK;
+  const int64_t rounds = (nwg + G - 1) / G;
+  const double idle = 1.0 - (double)nwg / (double)(rounds * G);
+  return idle > 0.02 && nwg * S / G >= S;
+}
+
 template <int DT, bool KNOT = false>
 static void launch_con_grad(bool v2, const KernParams& kp, const double* K, const double* M,
                             const double* X, int64_t ldx, int64_t n, int64_t n_pad,
                             const double* U, int64_t ldu, int64_t m, int64_t mp,
                             const ConArgs& ca, double* slab, int nrec, int64_t nwg,
                             hipStream_t s) {
+  if (!v2 && con_use_sk(ca, nwg, mp)) {
+    ConSK sk;
+    sk.ws = ca.sk_ws;
+    sk.flags = ca.sk_flags;
+    sk.epoch = ca.sk_epoch;
+    sk.status = ca.sk_status;
+    hipLaunchKernelGGL((k_contract_sk<DT, KNOT>), dim3((unsigned)ca.sk_slots), dim3(256), 0, s,
+                       kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, sk);
+    return;
+  }
   if (v2)
     hipLaunchKernelGGL((k_contract<DT, EPI_GRAD, true, KNOT>), dim3((unsigned)nwg), dim3(256), SGP_CON_SHMEM,
                        s, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec,
@@ -2206,6 +2370,8 @@ static void launch_con_from_t(bool v2, bool kn, const KernParams& kp, const doub
     launch_con_from_t2<DT, false>(v2, kn, kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab,
                                   nrec, nwg, s);
 }
+
+int64_t sgp_con_sk_doubles(int slots) { return (int64_t)(slots + 1) * CON_SK_SLOT; }
 
 hipError_t launch_contract_args(const KernParams& kp, const double* K, const double* M,
                                 const double* X, int64_t ldx, int64_t n, int64_t n_pad,

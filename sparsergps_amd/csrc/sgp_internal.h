@@ -213,7 +213,18 @@ struct ConArgs {
   const double* M2 = nullptr;
   const double* rs_vec2 = nullptr;
   double rs2 = 0.0;
+  // the balanced (Stream-K) launch of VI's gradient contraction (k_contract_sk): hand-over
+  // slots (sgp_con_sk_doubles), per-slot flags (sk_slots words, zero at allocation), this
+  // launch's epoch (> 0, new per launch), the resident-workgroup count and a status word (-1:
+  // a hand-over wait expired).  sk_ws == nullptr: always the one-tile-per-workgroup grid
+  double* sk_ws = nullptr;
+  unsigned* sk_flags = nullptr;
+  unsigned sk_epoch = 0;
+  int sk_slots = 0;
+  int* sk_status = nullptr;
 };
+// hand-over workspace (doubles) of a balanced contraction over `slots` workgroups
+int64_t sgp_con_sk_doubles(int slots);
 hipError_t launch_contract_args(const KernParams& kp, const double* K, const double* M,
                                 const double* X, int64_t ldx, int64_t n, int64_t n_pad,
                                 const double* U, int64_t ldu, int64_t m, int64_t mp,
