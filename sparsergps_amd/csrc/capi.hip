@@ -789,6 +789,15 @@ int sgp_dsig_dtheta(int device, int kernel, const double* x, int64_t n, int64_t 
                      ldo);
 }
 
+// The balanced (Stream-K) contraction launch, k_contract_sk: opt-in with SGP_CON_SK=1.  It is
+// equivalent to the tile grid (tests/test_gpu_contract_sk.py) but measured no faster at C2 and
+// slower on the n = 125 000 shard, so the product launches the grid by default and
+// does not allocate the hand-over workspace.
+static bool con_sk_enabled() {
+  static const bool on = getenv("SGP_CON_SK") && atoi(getenv("SGP_CON_SK")) == 1;
+  return on;
+}
+
 // ------------------------------------------------------------------------- context
 int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_t ldx, int d,
                    const double* y, const double* mu, int64_t m_max) {
@@ -878,7 +887,7 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->red2f, sgp_fitc_red2_count(SGP_KERNEL_ARD, SGP_MAXD, m_max) + mp * d);
   st = st ? st : dalloc(&c->slab_syrk, c->slab_syrk_cap);
   st = st ? st : dalloc(&c->slab_con, c->slab_con_cap);
-  {   // resident workgroups of the contraction: two per CU
+  if (con_sk_enabled()) {   // resident workgroups of the balanced contraction: two per CU
     int cus = 0;
     if (!st && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) ==
                    hipSuccess && cus > 0)
@@ -1153,10 +1162,9 @@ static int contract_pass(sgp_ctx* c, const double* M, ConArgs ca, double* rec_ou
   if (c->knot_on) ca.knot_slab = c->knot_slab;
   const bool fused = ca.uvec != nullptr && ca.alpha_in == nullptr;
   if (fused) ca.alpha_out = c->alpha;   // k_coinc needs the fused alpha_i
-  // the balanced launch where the tile grid leaves a mostly idle last round (SGP_CON_SK=0 in the
-  // environment: always the one-tile grid, for A/B runs and the equivalence test)
-  static const bool sk_off = getenv("SGP_CON_SK") && atoi(getenv("SGP_CON_SK")) == 0;
-  if (c->sk_ws && !sk_off) {
+  // the balanced launch where the tile grid leaves a mostly idle last round (opt-in, see
+  // con_sk_enabled)
+  if (c->sk_ws) {
     if (++c->sk_epoch == 0) ++c->sk_epoch;   // 0 is the flags' initial value
     ca.sk_ws = c->sk_ws;
     ca.sk_flags = c->sk_flags;

@@ -1493,14 +1493,17 @@ k_contract(KernParams kp, const double* __restrict__ K, const double* __restrict
       wgid, 0, (int)(mp / BK), lds, red, s_uk, ConSK{}, CON_FULL, (int)threadIdx.x);
 }
 
-// The balanced (Stream-K) form of VI's gradient contraction for grids whose last residency
-// round would be mostly empty (C2: 1564 tiles over 512 slots = 3.05 rounds run as 4; the 8-GPU
-// shard: 15.3 as 16).  The tiles' k-steps, in tile order, are split evenly over the G resident
-// workgroups: a workgroup's range starts with the tail of a tile (handed to the previous
-// workgroup, which holds that tile's head at the END of its own range, so it never waits long),
-// then whole tiles, then the head of the next tile.  Every tile gets one epilogue, run by the
-// workgroup that holds its k = 0 step.  Requires range >= k-steps per tile (a tile meets at most
-// two workgroups).
+// The balanced form of VI's gradient contraction for grids whose last residency round would
+// be mostly empty (C2: 1564 tiles over 512 slots = 3.05 rounds run as 4; the 8-GPU shard: 15.3
+// as 16).  A persistent grid of G = resident workgroups: the first R - 1 whole rounds
+// (R = tiles / G) as the one-tile grid runs them -- in round r workgroup v takes tile r G + v,
+// v the XCD-aware index, so the tiles resident on one XCD together share their K row panels and
+// P column panels in its L2 as before -- and the last round plus the remainder (G + tiles mod G
+// tiles) Stream-K style: their k-steps, in tile order, split evenly over the G workgroups
+// (each range covers at least one tile's steps, so a tile meets at most two workgroups).  A
+// range that starts inside a tile computes that tile's tail FIRST, before its whole rounds, and
+// hands it to workgroup v - 1, which holds the tile's head at the very end of its own work and
+// adds the tail before the tile's one epilogue.
 template <int DT, bool KNOT>
 __global__ void __launch_bounds__(256, 2)
 k_contract_sk(KernParams kp, const double* __restrict__ K, const double* __restrict__ M,
@@ -1513,25 +1516,40 @@ k_contract_sk(KernParams kp, const double* __restrict__ K, const double* __restr
   const int64_t ntj = mp / T128;
   const int64_t ntiles = (n_pad / T128) * ntj;
   const int S = (int)(mp / BK);
-  const int64_t Utot = ntiles * S, G = gridDim.x, w = blockIdx.x;
-  const int64_t u1 = Utot * (w + 1) / G;
-  int64_t u = Utot * w / G;
-  if (u % S != 0) {   // the range starts inside a tile: its tail, handed to workgroup w - 1
-    const int64_t tile = u / S;
+  const int64_t G = gridDim.x, v = xcd_remap(blockIdx.x, G);
+  const int64_t dp_rounds = ntiles / G - 1;   // the host launches this with ntiles >= G
+  const int64_t t0 = dp_rounds * G;           // the balanced region: tiles [t0, ntiles)
+  const int64_t Usk = (ntiles - t0) * S;
+  const int64_t u1 = Usk * (v + 1) / G;
+  int64_t u = Usk * v / G;
+  if (u % S != 0) {   // the range starts inside a tile: its tail, handed to workgroup v - 1
+    const int64_t tile = t0 + u / S;
     const int kb = (int)(u % S);
     ConSK p = sk;
-    p.slot = w;
+    p.slot = v;
     con_tile<DT, EPI_GRAD, false, KNOT, false, true, false, CON_TAIL>(
         kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, nullptr, tile / ntj,
         tile % ntj, tile, kb, S, lds, red, s_uk, p, CON_TAIL, (int)threadIdx.x);
     u += S - kb;
     __syncthreads();
   }
-  while (u < u1) {   // whole tiles, then possibly the head of the next (its tail: w + 1's start)
-    const int64_t tile = u / S;
-    const int ke = (int)((u1 - u) < (int64_t)S ? (u1 - u) : S);
+  int64_t r = 0;
+  for (;;) {   // the whole rounds, then the range's whole tiles, then maybe a head
+    int64_t tile;
+    int ke;
+    if (r < dp_rounds) {
+      tile = r * G + v;
+      ke = S;
+      ++r;
+    } else if (u < u1) {
+      tile = t0 + u / S;
+      ke = (int)((u1 - u) < (int64_t)S ? (u1 - u) : S);
+      u += ke;
+    } else {
+      break;
+    }
     ConSK p = sk;
-    p.slot = w + 1;
+    p.slot = v + 1;
     // the thread index passed through an opaque move each iteration: every per-thread offset
     // of the tile body is then recomputed inside the loop instead of hoisted out of it and
     // kept live across the k-loop
@@ -1540,7 +1558,6 @@ k_contract_sk(KernParams kp, const double* __restrict__ K, const double* __restr
     con_tile<DT, EPI_GRAD, false, KNOT, false, true, false, CON_HEAD>(
         kp, K, M, X, ldx, n, n_pad, U, ldu, m, mp, ca, slab, nrec, nullptr, tile / ntj,
         tile % ntj, tile, 0, ke, lds, red, s_uk, p, ke < S ? CON_HEAD : CON_FULL, tid);
-    u += ke;
     __syncthreads();   // the next tile's operand staging reuses the epilogue's LDS
   }
 }

@@ -10,8 +10,13 @@ D=gpurun_out/$T
 mkdir -p $D
 for rep in $(seq 1 $REPS); do
   for v in cur $VARS; do
-    if [ "$v" = cur ]; then unset SGP_AB_LIB; else export SGP_AB_LIB=tools/ab/$v/libsgp.so; fi
-    timeout -k 10 200 python3 bench.py --no-cpu-baseline "$@" > $D/${v}_$rep.json 2> $D/${v}_$rep.err || { echo "bench $v failed"; tail -20 $D/${v}_$rep.err; exit 1; }
+    # a variant is a library under tools/ab/, or env.VAR=VALUE: the product library with that
+    # runtime switches, comma-separated (e.g. env.SGP_CON_SK=0)
+    envset=""
+    if [ "$v" = cur ]; then unset SGP_AB_LIB
+    elif [ "${v#env.}" != "$v" ]; then unset SGP_AB_LIB; envset=$(echo "${v#env.}" | tr ',' ' ')
+    else export SGP_AB_LIB=tools/ab/$v/libsgp.so; fi
+    env $envset timeout -k 10 200 python3 bench.py --no-cpu-baseline "$@" > $D/${v}_$rep.json 2> $D/${v}_$rep.err || { echo "bench $v failed"; tail -20 $D/${v}_$rep.err; exit 1; }
     python3 -c "import json,sys; d=json.load(open('$D/${v}_$rep.json')); print('$v', $rep, round(d['value'],2), round(d['ms_per_step'],4), {k: v for k, v in d['phases_ms'].items() if v > 0.01})"
   done
 done
