@@ -11,6 +11,8 @@
 #     modes             the secondary lines: C2, the n = 125 000 shard, FITC, C5, knots, the
 #                       in-library 8-shard composition -> $D/run_*.json
 #     c2x4              four C2 lines in a row (the C2 measure) -> $D/c2_*.json
+#     c2trace           rocprofv3 --kernel-trace --stats of a C2 line and the timeline of its last
+#                       evaluation (tools/trace_eval.py) -> $D/c2k/, $D/c2_timeline.txt
 #     pmc               WRITE_SIZE / FETCH_SIZE passes of the bench command (one counter set
 #                       per run, kernel trace only) -> $D/pmc_*/
 #     builderpmc        counter passes over tools/builder_probe.py (K12 builder + store ceiling)
@@ -58,6 +60,10 @@ for step in "$@"; do
           > "$D/c2_$r.json" 2> "$D/run.err" || { tail -20 "$D/run.err"; exit 1; }
         last_json "$D/c2_$r.json" "c2 $r"
       done ;;
+    c2trace)
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/c2k" -o run -- \
+        python3 bench.py --no-cpu-baseline --config C2 --steps 60 --warmup 5 > "$D/c2k.json" 2> "$D/c2k.err" || { tail -20 "$D/c2k.err"; exit 1; }
+      python3 tools/trace_eval.py "$D/c2k/run_kernel_trace.csv" "k_contract<8, 0, false, false, false" > "$D/c2_timeline.txt" && tail -1 "$D/c2_timeline.txt" ;;
     pmc)
       for ctr in "FETCH_SIZE" "WRITE_SIZE"; do
         timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $ctr --output-format csv -d "$D/pmc_$ctr" -o run -- \
