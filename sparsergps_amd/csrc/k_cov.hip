@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(256) k_build_knm(KernParams kp, const double* 
 // FITC's 1.50 ms for the same K12); the sums and their reduction order are unchanged, so t is
 // bit-identical to the register form.
 template <bool WITH_T, int NC>
-__global__ void __launch_bounds__(256, NC > 4 ? (WITH_T ? 2 : 3) : 4)
+__global__ void __launch_bounds__(256, NC > 4 ? (WITH_T ? 2 : 3) : ((WITH_T && NC == 2) ? SGP_BUILD_OCC_T2 : 4))
 k_build_knm_mfma(KernParams kp, const double* __restrict__ X, int64_t ldx, int64_t n,
                  const double* __restrict__ U, int64_t ldu, int64_t m, int64_t mp,
                  double* __restrict__ K, const double* __restrict__ rvec,

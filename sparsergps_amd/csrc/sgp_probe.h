@@ -31,6 +31,7 @@
 //   SGP_VI_BUILD_NO_T   1: VI's builder without t (wrong results: builder timing only)
 //   SGP_GJ_STEPS        1: the m x m inverses as one launch per pivot step (before round 5)
 //   SGP_GJ_GMAX         workgroups of a persistent Gauss-Jordan chain (at most)
+//   SGP_BUILD_OCC_T2    workgroups per CU of the with-t K12 builder at d <= 8 (launch bound)
 //   SGP_CHAIN_US_STEP   chain_shared_rb's model of a K22 chain beside the builder: us per
 //   SGP_CHAIN_US_FIX    64-wide step, and fixed us
 // Fault injection (environment, read by probe builds only; the product ignores it):
@@ -47,11 +48,14 @@
      defined(SGP_SYRK_W3) || defined(SGP_CON_ROWQ_KU) ||                                      \
      defined(SGP_LAP_RS_CFG) || defined(SGP_GJ_MM_UNROLL) || defined(SGP_VI_BUILD_NO_T) ||        \
      defined(SGP_GJ_STEPS) || defined(SGP_GJ_GMAX) || defined(SGP_CHAIN_US_STEP) ||         \
-     defined(SGP_CHAIN_US_FIX) || defined(SGP_HOST_PROBE)) &&      \
+     defined(SGP_CHAIN_US_FIX) || defined(SGP_HOST_PROBE) || defined(SGP_BUILD_OCC_T2)) &&      \
     !defined(SGP_PROBE_BUILD)
 #error "timing probes and experiment knobs are for variant builds only (SGP_PROBE_BUILD)"
 #endif
 
+#ifndef SGP_BUILD_OCC_T2
+#define SGP_BUILD_OCC_T2 4
+#endif
 #ifndef SGP_IL_VMEM0
 #define SGP_IL_VMEM0 0
 #endif

@@ -46,12 +46,15 @@ CHILD = textwrap.dedent("""
 """)
 
 
-def _run(cfg, n, m, knots, sk_off):
+def _run(cfg, n, m, knots, sk_off, dp=None):
     env = dict(os.environ)
+    env.pop("SGP_CON_SK_DP", None)
     if sk_off:
         env.pop("SGP_CON_SK", None)
     else:
         env["SGP_CON_SK"] = "1"
+        if dp is not None:
+            env["SGP_CON_SK_DP"] = str(dp)
     r = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT, cfg=cfg, n=n, m=m,
                                                           knots=knots)],
                        env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=250)
@@ -61,19 +64,22 @@ def _run(cfg, n, m, knots, sk_off):
     return np.array(json.loads(line[7:]))
 
 
-@pytest.mark.parametrize("cfg,n,m,knots", [
-    ("C2", 100_000, 256, False),      # configs[1]: 1564 tiles, 3.05 rounds
-    ("C3", 125_000, 1024, False),     # C4's shard: 7816 tiles, 15.3 rounds
-    ("C2", 32_800, 256, False),       # 514 tiles: each range a tile and ~1 step
-    ("C2", 60_000, 256, True),        # the knot-gradient epilogue
+@pytest.mark.parametrize("cfg,n,m,knots,dp", [
+    ("C2", 100_000, 256, False, None),      # configs[1]: 1564 tiles, 3.05 rounds
+    ("C3", 125_000, 1024, False, None),     # C4's shard: 7816 tiles, 15.3 rounds
+    ("C2", 32_800, 256, False, None),       # 514 tiles: each range a tile and ~1 step
+    ("C2", 60_000, 256, True, None),        # the knot-gradient epilogue
+    ("C2", 100_000, 256, False, 0),         # every tile's k-steps balanced (SGP_CON_SK_DP=0)
+    ("C2", 60_000, 256, True, 0),
+    ("C3", 125_000, 1024, False, 0),
 ])
-def test_balanced_contraction_matches_tile_grid(cfg, n, m, knots):
+def test_balanced_contraction_matches_tile_grid(cfg, n, m, knots, dp):
     from sparsergps_amd import _lib
     _lib.require_gpu()
-    sk = _run(cfg, n, m, knots, sk_off=False)
+    sk = _run(cfg, n, m, knots, sk_off=False, dp=dp)
     grid = _run(cfg, n, m, knots, sk_off=True)
     assert np.array_equal(sk[0], sk[1]), "balanced launch not bit-identical on repeat"
     assert np.array_equal(grid[0], grid[1])
     rel = np.abs(sk[0] - grid[0]) / np.maximum(1.0, np.abs(grid[0]))
-    print(f"\n[sk] {cfg} n={n} m={m} knots={knots}: max rel diff {rel.max():.3e}")
+    print(f"\n[sk] {cfg} n={n} m={m} knots={knots} dp={dp}: max rel diff {rel.max():.3e}")
     assert rel.max() < 1e-12
