@@ -220,13 +220,6 @@ def kernel_rooflines(mode, phase_avg, n_loc, m, ceiling=None):
                                          "non-temporal 16-byte stores, the builder's shape and "
                                          "byte count, best of 5")
         out.append(row)
-    t = phase_avg.get("build_syrk", 0.0) * 1e-3
-    if t > 0:   # m_p = 256 VI: K12 evaluated inside the SYRK (MFMA bound; K12 stored as well)
-        tf = float(n_loc) * m * m / t / 1e12
-        out.append({"kernel": "build_syrk (k_build_syrk_s256)", "bound": "mfma", "achieved": tf,
-                    "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": tf / FP64_MFMA_PEAK_TFLOPS, "flops_per_launch": float(n_loc) * m * m,
-                    "k12_bytes_written": 8.0 * n_pad * m_p})
     key = {"vi": "syrk", "fitc": "syrk", "laplace": "syrk_z"}.get(mode)
     t = phase_avg.get(key, 0.0) * 1e-3
     if t > 0:

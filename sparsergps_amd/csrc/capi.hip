@@ -243,8 +243,7 @@ struct sgp_ctx {
   unsigned* sk_flags = nullptr;
   unsigned sk_epoch = 0;
   int sk_slots = 0;
-  double* tslab = nullptr;                // builder t = K^T r partials (VI), tslab_rows x mp
-  int64_t tslab_rows = 0;
+  double* tslab = nullptr;                // builder t = K^T r partials (VI), n_pad/64 x mp
   // stored products of the FITC / Laplace row-quadratic passes (n_pad x mp each, allocated on
   // first use): tq = K K22^-1, tp = K Bm^-1 (FITC) or K C (Laplace).  The gradient
   // contraction passes read them instead of recomputing the same 2 n m^2 GEMMs.
@@ -798,11 +797,6 @@ static bool con_sk_enabled() {
   static const bool on = getenv("SGP_CON_SK") && atoi(getenv("SGP_CON_SK")) == 1;
   return on;
 }
-// K12 built inside VI's SYRK at mp = 256 (k_build_syrk_s256): on unless SGP_BS256=0
-static bool bs256_enabled() {
-  static const bool on = !(getenv("SGP_BS256") && atoi(getenv("SGP_BS256")) == 0);
-  return on;
-}
 // SGP_CON_SK_DP=k: the balanced launch runs only k whole rounds as the grid (default: all but the
 // last); 0 balances every tile's k-steps over the resident workgroups
 static int con_sk_dp() {
@@ -922,10 +916,7 @@ int sgp_ctx_create(sgp_ctx** out, int device, const double* X, int64_t n, int64_
   st = st ? st : dalloc(&c->sc, SC_N);
   st = st ? st : dalloc(&c->y, np_);
   st = st ? st : dalloc(&c->mu, np_);
-  // t partial rows: one per builder workgroup row / row block (<= np_ / 64), or one per row
-  // chunk of k_build_syrk_s256 (<= 256)
-  c->tslab_rows = std::max<int64_t>(np_ / 64, 256);
-  st = st ? st : dalloc(&c->tslab, c->tslab_rows * mp);
+  st = st ? st : dalloc(&c->tslab, (np_ / 64) * mp);
   st = st ? st : dalloc(&c->khash, mp);
   st = st ? st : dalloc(&c->kidx, mp);
   st = st ? st : dalloc(&c->cflag, np_);
@@ -1334,43 +1325,29 @@ int sgp_vi_phase1(sgp_ctx* c, int kernel, const double* theta, const double* U, 
   const bool small_syrk = syrk_use_s256(mpv, false);
   c->vi_k22_ordered = !small_syrk;
   c->t_deferred = false;
-  // mp = 256: K12 evaluated inside the SYRK's k-loop (k_build_syrk_s256; the builder's ~50 us
-  // of HBM writes ride under the SYRK's MFMA time instead of preceding it)
-  const bool fused_bs = small_syrk && build_syrk_s256_ok(kp, mpv) && !SGP_VI_BUILD_NO_T &&
-                        bs256_enabled() &&   // and tslab holds the chunks' t rows
-                        build_syrk_s256_rows(c->n_pad) <= c->tslab_rows;
-  if (fused_bs) {
-    Scope t(c, "build_syrk");
-    HIPCHK(launch_build_syrk_s256(kp, c->X, c->n_pad, c->n, c->U, mpv, m, c->r, c->n_pad, c->K,
-                                  c->slab_syrk, c->slab_syrk_cap, c->tslab,
-                                  c->tslab_rows * c->mp_max, &t_rows, c->stream));
-    st = k22_sync(c);
-    if (st) return st;
-  } else {
-    {
-      // K12, and t = K^T r riding along in the memory-bound builder (keeps the SYRK's
-      // diagonal tiles as cheap as the others); the first HIP call of the evaluation, so the
-      // GPU starts on it as soon as the host gets here
-      Scope t(c, "build_knm");
-      if (SGP_VI_BUILD_NO_T)
-        HIPCHK(launch_build_knm(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, mpv, m, mpv, c->K,
-                                c->stream, false));
-      else
-        HIPCHK(launch_build_knm_t(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, mpv, m, mpv, c->K,
-                                  c->r, c->tslab, &t_rows, c->stream, false));
-    }
-    // ev_knots after the builder: aux may build K22 from here on (first needed by phase 2),
-    // and aux_lo may reduce the builder's t partials.  The SYRK goes right behind the builder
-    // (it needs only K12); red1's reset and the small t / rr reductions run on aux_lo beside
-    // it instead of between the two on the main stream, where at small n (C2) the GPU idled
-    // while the host issued them one by one
-    st = k22_sync(c);
-    if (st) return st;
-    {
-      Scope t(c, "syrk");
-      HIPCHK(launch_syrk_aug(c->K, c->n_pad, mpv, c->r, nullptr, c->slab_syrk, c->slab_syrk_cap,
-                             red1, c->stream, 1, nullptr, 0));
-    }
+  {
+    // K12, and t = K^T r riding along in the memory-bound builder (keeps the SYRK's
+    // diagonal tiles as cheap as the others); the first HIP call of the evaluation, so the
+    // GPU starts on it as soon as the host gets here
+    Scope t(c, "build_knm");
+    if (SGP_VI_BUILD_NO_T)
+      HIPCHK(launch_build_knm(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, mpv, m, mpv, c->K,
+                              c->stream, false));
+    else
+      HIPCHK(launch_build_knm_t(kp, c->X, c->n_pad, c->n, c->n_pad, c->U, mpv, m, mpv, c->K,
+                                c->r, c->tslab, &t_rows, c->stream, false));
+  }
+  // ev_knots after the builder: aux may build K22 from here on (first needed by phase 2), and
+  // aux_lo may reduce the builder's t partials.  The SYRK goes right behind the builder (it
+  // needs only K12); red1's reset and the small t / rr reductions run on aux_lo beside it
+  // instead of between the two on the main stream, where at small n (C2) the GPU idled while
+  // the host issued them one by one
+  st = k22_sync(c);
+  if (st) return st;
+  {
+    Scope t(c, "syrk");
+    HIPCHK(launch_syrk_aug(c->K, c->n_pad, mpv, c->r, nullptr, c->slab_syrk, c->slab_syrk_cap,
+                           red1, c->stream, 1, nullptr, 0));
   }
   // K22 itself only (aux); its inverse runs in phase 2 beside the Bm inverse -- nothing in
   // phase 1 needs it, and the latency-bound chain no longer gates the one-round SYRK or shares

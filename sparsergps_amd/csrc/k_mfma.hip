@@ -820,181 +820,6 @@ k_syrk_s256(const double* __restrict__ K, int64_t n_pad, const double* __restric
 #undef S256_CASE
 }
 
-// ===================================================== K12 built inside the SYRK, mp = 256
-// VI phase 1 at mp = 256 (C2) ran the HBM-bound K12 builder (~50 us) and then this SYRK (~120
-// us, MFMA-bound) one after the other.  Here the SYRK's row slabs are computed instead of
-// loaded: each step's 16 x 256 slab of K12 = sig2 exp(-sum_c (x~_ic - u~_jc)^2) (x~ = x s, u~ =
-// u s, s_c = 1 / (sqrt(2) l_c)) is evaluated by the VALU into the idle LDS buffer while the
-// matrix cores work on the current one, stored to HBM for the later passes, and folded into t
-// = K^T r.  Thread t owns knot column t: its scaled knot coordinates stay in registers, the
-// rows' scaled coordinates (with a per-row exponent offset log sig2, or -1e300 on padding rows)
-// and r are staged once per step in LDS and read as broadcasts, t's running sum is one register
-// (its order fixed: deterministic), and a wave's stores of one row are 512 contiguous bytes.
-// Both workgroups of a row chunk evaluate the whole slab (each stages its own image, as in
-// k_syrk_s256) and both store it: the two identical stores of a line meet in their XCD's L2
-// (the pair is on one XCD), so HBM sees it once and the step stays one basic block.  On the
-// last step the slab of that step is evaluated again into the idle buffer (same values, same
-// addresses; its t share is weighted 0).  Direct differences: no span limit, and K is exactly
-// what the Layer-1 filler computes up to the exp's last bits (table exp, < 2e-18 truncation).
-constexpr int BS_ROWS = 16;   // = BK: one SYRK k-step of rows
-
-template <int DT>
-struct BsRowsLds {
-  static constexpr int XS = DT + 2;   // [s x_0 .. s x_{DT-1}, row offset, r]
-  double v[2][BS_ROWS * XS];
-};
-
-// the slab for one step: rows of xs (scaled coordinates, offset, r) against this thread's knot
-template <int DT>
-__device__ __forceinline__ double bs_slab(const double* __restrict__ xs, const double (&u)[DT],
-                                          double coloff, double* __restrict__ kdst,
-                                          double* __restrict__ kg, const KernParams& kp,
-                                          const double* etab) {
-  constexpr int XS = DT + 2;
-  double tl = 0.0;
-#pragma unroll
-  for (int row = 0; row < BS_ROWS; ++row) {
-    const double* xr = xs + row * XS;
-    double acc = coloff;
-#pragma unroll
-    for (int c = 0; c < DT; ++c) {
-      const double df = xr[c] - u[c];
-      acc = fma(df, df, acc);
-    }
-    const double v = sgp_exp_tab(fmax(xr[DT] - acc, -746.0), kp, etab);
-    kdst[row * SB2] = v;
-    kg[row * 256] = v;
-    tl = fma(v, xr[DT + 1], tl);
-  }
-  return tl;
-}
-
-template <int V, int DT>
-__device__ __forceinline__ void bsyrk256_body(const KernParams& kp, const double* __restrict__ X,
-                                              int64_t ldx, int64_t n, const double* __restrict__ r,
-                                              double ssf, const double (&u)[DT],
-                                              double coloff, int64_t rbeg, int nsteps,
-                                              double (*Ks)[BK * SB2], BsRowsLds<DT>& xl,
-                                              const double* etab, double* __restrict__ K,
-                                              double* __restrict__ out, double& tacc) {
-  constexpr int R0 = V, R1 = 15 - V, N0 = R0 + 1, N1 = R1 + 1;
-  constexpr int XS = DT + 2;
-  const int tid = threadIdx.x, lane = tid & 63;
-  d4 acc0[N0], acc1[N1];
-#pragma unroll
-  for (int c = 0; c < N0; ++c) acc0[c] = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int c = 0; c < N1; ++c) acc1[c] = d4{0.0, 0.0, 0.0, 0.0};
-  // row staging: thread e < 16 XS loads value (row e / XS, field e % XS) of a step's rows
-  const int srow = tid / XS, sf = tid % XS;
-  const bool stager = tid < BS_ROWS * XS;
-  const double lsig2 = kp.lsig2;
-  auto stage_val = [&](int step) -> double {
-    const int64_t i = rbeg + (int64_t)step * BS_ROWS + srow;
-    if (!stager) return 0.0;
-    if (sf < DT) return sf < kp.d ? X[i + sf * ldx] * ssf : 0.0;   // X zero-padded to n_pad
-    if (sf == DT) return i < n ? lsig2 : -1e300;                       // padding rows -> K = 0
-    return r[i];                                                       // r zero-padded
-  };
-  double* kcol = K + rbeg * 256 + tid;   // this thread's column of the chunk's rows
-  if (nsteps > 0) {
-    if (stager) xl.v[0][tid] = stage_val(0);
-    __syncthreads();
-    tacc += bs_slab<DT>(xl.v[0], u, coloff, &Ks[0][tid], kcol, kp, etab);
-    if (stager) xl.v[1][tid] = stage_val(nsteps > 1 ? 1 : 0);
-  }
-  __syncthreads();
-  for (int step = 0; step < nsteps; ++step) {
-    const int cur = step & 1;
-    // the rows two steps ahead (the last steps restage their own: one basic block)
-    const int s2 = step + 2 < nsteps ? step + 2 : nsteps - 1;
-    const double xv = stage_val(s2);
-    const double* Kc = Ks[cur];
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int krow = kk * 4 + (lane >> 4);
-      const double* row = Kc + krow * SB2 + (lane & 15);
-      const double a0 = row[R0 * 16], a1 = row[R1 * 16];
-#pragma unroll
-      for (int c = 0; c < N1; ++c) {
-        const double b = row[c * 16];
-        if (c < N0) acc0[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b, acc0[c], 0, 0, 0);
-        acc1[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b, acc1[c], 0, 0, 0);
-      }
-    }
-    // the next step's slab into the idle buffer (on the last step: this step's again, t share 0)
-    const int s1 = step + 1 < nsteps ? step + 1 : step;
-    const double tl = bs_slab<DT>(xl.v[s1 & 1], u, coloff, &Ks[cur ^ 1][tid],
-                                  kcol + (int64_t)s1 * BS_ROWS * 256, kp, etab);
-    tacc = fma(step + 1 < nsteps ? 1.0 : 0.0, tl, tacc);
-    if (stager && step + 2 < nsteps) xl.v[step & 1][tid] = xv;   // buffer of slab `step`: read
-    __syncthreads();
-  }
-  (void)XS;
-#pragma unroll
-  for (int c = 0; c < N1; ++c)
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      if (hh == 0 && c >= N0) continue;
-      const int R = hh == 0 ? R0 : R1;
-      const d4& a = hh == 0 ? acc0[c] : acc1[c];
-      const int rp = R / 4, cp = c / 4;
-      double* blk = out + (int64_t)(rp * (rp + 1) / 2 + cp) * 4096;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        blk[((R % 4) * 16 + (lane >> 4) + 4 * q) * 64 + (c % 4) * 16 + (lane & 15)] = a[q];
-    }
-}
-
-// grid = 2 splits workgroups (as k_syrk_s256); tslab[split][256] = the chunk's t partial
-template <int DT>
-__global__ void __launch_bounds__(256, 2)
-k_build_syrk_s256(KernParams kp, const double* __restrict__ X, int64_t ldx, int64_t n,
-                  const double* __restrict__ U, int64_t ldu, int64_t m,
-                  const double* __restrict__ r, int64_t n_pad, int64_t chunk,
-                  double* __restrict__ K, double* __restrict__ slab, double* __restrict__ tslab) {
-  __shared__ __attribute__((aligned(16))) double Ks[2][BK * SB2];
-  __shared__ BsRowsLds<DT> xl;
-  __shared__ double etab[32];
-  const int tid = threadIdx.x;
-  if (tid < 32) etab[tid] = kp.et[tid];
-  const int64_t nwg = (int64_t)gridDim.x;
-  const int64_t wgid = xcd_remap(blockIdx.x, nwg);   // a chunk's two workgroups on one XCD
-  const int64_t split = wgid >> 1;
-  const int v = (int)(wgid & 1) * 4 + (tid >> 6);
-  const int64_t rbeg = split * chunk;
-  int64_t rend = rbeg + chunk;
-  if (rend > n_pad) rend = n_pad;
-  const int nsteps = rend > rbeg ? (int)((rend - rbeg) / BK) : 0;
-  // scale s_c = 1 / (sqrt(2) l_c): sqexp -1/(2 l^2) = -s^2, ARD rl_c / sqrt(2)
-  double u[DT];
-  const double s_iso = sqrt(-kp.coef);
-#pragma unroll
-  for (int c = 0; c < DT; ++c) {
-    const double sc = kp.kernel == 1 ? kp.rl[c] * 0.70710678118654752440 : s_iso;
-    u[c] = (c < kp.d && tid < m) ? U[tid + c * ldu] * sc : 0.0;
-  }
-  // the scale of this thread's staging field (a coordinate for tid % (DT + 2) < d)
-  const int sfield = tid % (DT + 2);
-  const double ssf = sfield < kp.d ? (kp.kernel == 1 ? kp.rl[sfield] * 0.70710678118654752440
-                                                     : s_iso)
-                                   : 0.0;
-  const double coloff = tid < m ? 0.0 : 1e300;   // padding knots -> K = 0
-  double tacc = 0.0;
-  double* out = slab + split * 10 * 4096;
-#define BS256_CASE(v_)                                                                         \
-  case v_:                                                                                     \
-    bsyrk256_body<v_, DT>(kp, X, ldx, n, r, ssf, u, coloff, rbeg, nsteps, Ks, xl, etab, K, out, \
-                          tacc);                                                               \
-    break;
-  switch (v) {   // wave-uniform
-    BS256_CASE(0) BS256_CASE(1) BS256_CASE(2) BS256_CASE(3)
-    BS256_CASE(4) BS256_CASE(5) BS256_CASE(6) BS256_CASE(7)
-  }
-#undef BS256_CASE
-  if ((wgid & 1) == 0) tslab[split * 256 + tid] = tacc;
-}
-
 // ============================================================================ TN GEMM
 // C = A^T B over n rows (A: n_pad x ma, B: n_pad x mb, both row-major; ma, mb multiples of
 // 128): split-K over row chunks like k_syrk_blk, one 128x128 tile per workgroup, deterministic
@@ -2227,32 +2052,6 @@ static SyrkPlan syrk_plan_s256(int64_t n_pad) {
 
 // the fragment-balanced k_syrk_s256 serves the SYRKs without t at mp = 256
 bool syrk_use_s256(int64_t mp, bool with_t) { return mp == 256 && !with_t; }
-
-// VI phase 1 at mp = 256: K12 built inside the SYRK (k_build_syrk_s256), sqexp / ARD, d <= 8
-bool build_syrk_s256_ok(const KernParams& kp, int64_t mp) {
-  return mp == 256 && kp.kernel != 2 && kp.d <= 8;
-}
-int64_t build_syrk_s256_rows(int64_t n_pad) { return syrk_plan_s256(n_pad).splits; }
-
-hipError_t launch_build_syrk_s256(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
-                                  const double* U, int64_t ldu, int64_t m, const double* r,
-                                  int64_t n_pad, double* K, double* slab, int64_t slab_cap,
-                                  double* tslab, int64_t tslab_cap, int64_t* t_rows,
-                                  hipStream_t s) {
-  if (!build_syrk_s256_ok(kp, 256) || m > 256 || m < 1) return hipErrorInvalidValue;
-  const SyrkPlan q = syrk_plan_s256(n_pad);
-  if ((int64_t)q.splits * 10 * 4096 > slab_cap || (int64_t)q.splits * 256 > tslab_cap)
-    return hipErrorInvalidValue;
-  const dim3 grid((unsigned)(q.splits * 2));
-  if (kp.d <= 4)
-    hipLaunchKernelGGL(k_build_syrk_s256<4>, grid, dim3(256), 0, s, kp, X, ldx, n, U, ldu, m, r,
-                       n_pad, q.chunk, K, slab, tslab);
-  else
-    hipLaunchKernelGGL(k_build_syrk_s256<8>, grid, dim3(256), 0, s, kp, X, ldx, n, U, ldu, m, r,
-                       n_pad, q.chunk, K, slab, tslab);
-  *t_rows = q.splits;
-  return hipGetLastError();
-}
 
 namespace {
 

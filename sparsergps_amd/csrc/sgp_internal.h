@@ -174,15 +174,6 @@ hipError_t launch_unpack_lower64(const double* packed, int64_t mp, double* S, hi
 int64_t syrk_slab_doubles(int64_t n_pad, int64_t mp);
 // true when launch_syrk_aug uses the fragment-balanced mp = 256 kernel (S only)
 bool syrk_use_s256(int64_t mp, bool with_t);
-// VI phase 1 at mp = 256: K12 (n_pad x 256, returned in K), the SYRK's slabs (reduce with
-// launch_syrk_aug part 2) and t's partial rows tslab[q][256], q < *t_rows, in one launch
-bool build_syrk_s256_ok(const KernParams& kp, int64_t mp);
-int64_t build_syrk_s256_rows(int64_t n_pad);   // *t_rows of launch_build_syrk_s256
-hipError_t launch_build_syrk_s256(const KernParams& kp, const double* X, int64_t ldx, int64_t n,
-                                  const double* U, int64_t ldu, int64_t m, const double* r,
-                                  int64_t n_pad, double* K, double* slab, int64_t slab_cap,
-                                  double* tslab, int64_t tslab_cap, int64_t* t_rows,
-                                  hipStream_t s);
 // Gradient contraction on T = K M (K: n_pad x mp, M: mp x mp):
 //   G_ij = alpha_i u_j + rs_i T_ij,  alpha_i = (r_i - K_i u) * iz_i computed in the same pass
 //   (iz_i = invz_vec ? invz_vec[i] : invz; uvec == nullptr -> alpha = u = 0;

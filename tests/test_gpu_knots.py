@@ -48,6 +48,23 @@ def test_vi_knot_gradient(sgp, cov_fun, coinc):
         assert abs(got["gradient"][k] - ref["gradient"][k]) / max(1, abs(ref["gradient"][k])) < RTOL
 
 
+@pytest.mark.parametrize("cov_fun", ["sqexp", "ard"])
+def test_vi_knot_gradient_mp256(sgp, cov_fun):
+    # 129 <= m <= 256 (m_p = 256, C2's knot count): the fragment-balanced k_syrk_s256 path
+    P = O.make_gaussian_problem("C2", n=230, m=140)
+    cp = P["cov_par"] if cov_fun == "sqexp" else _ard_par(3)
+    U = P["U"].copy()
+    U[3] = P["X"][17]
+    ref = O.delbo_dcov_par(cp, cov_fun, U, P["X"], P["y"], P["mu"], P["delta"],
+                           dcov_fun_dknot=cov_fun)
+    got = sgp.delbo_dcov_par(cp, cov_fun, True, "dsqexp_dx2" if cov_fun == "sqexp" else
+                             "dsqexp_dx2_ard", None, U, P["X"], P["y"], None, P["mu"], True,
+                             P["delta"])
+    assert _close(got["knot_gradient"], ref["knot_gradient"])
+    for k in cp:
+        assert abs(got["gradient"][k] - ref["gradient"][k]) / max(1, abs(ref["gradient"][k])) < RTOL
+
+
 def test_vi_knot_opt_subset(sgp):
     P = O.make_gaussian_problem("C2", n=80, m=6)
     ref = O.delbo_dcov_par(P["cov_par"], "sqexp", P["U"], P["X"], P["y"], P["mu"], P["delta"],
