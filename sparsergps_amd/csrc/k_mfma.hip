@@ -1151,6 +1151,7 @@ __device__ __forceinline__ void con_tile(
   }
 
   SGP_PROBE_CON_STAMP(1);
+  if constexpr (SGP_CON_EPI_PRIO > 0) __builtin_amdgcn_s_setprio(SGP_CON_EPI_PRIO);
   SGP_PROBE_CON_SKIP_EPILOGUE()   // timing probe hook (sgp_probe.h): empty in the product
   // ---------------- alpha (per row), shared by both epilogues ----------------
   double* s_alpha = lds;                    // 128
@@ -1284,6 +1285,9 @@ __device__ __forceinline__ void con_tile(
       // the stage being read); a real two-ahead prefetch (inline-asm DMA, three buffers) was no
       // faster -- the stage phase is bound by the issue slots the co-resident workgroup's k-loop
       // leaves, not by the load latency (profiles/r3/con_epi_dma_ab.txt)
+#ifdef SGP_CON_PROBE_NO_KDMA   // timing probe (wrong results): the K stages are not loaded
+#define CON_KHALF(s_)
+#else
 #define CON_KHALF(s_)                                                                    \
       _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_) {                                 \
         const int rho_ = wv * 4 + q_;                                                    \
@@ -1294,6 +1298,7 @@ __device__ __forceinline__ void con_tile(
             (__attribute__((address_space(3))) void*)(kst + ((s_) & 1) * 16 * KST + rho_ * KST), \
             16, 0, 0);                                                                   \
       }
+#endif
       // T2: the second stored product's values of a half-stage (rows 2h, 2h + 1 of fragment fm,
       // four column fragments), loaded into registers one half-stage ahead beside the K stage's
       // DMA (the same vmcnt(0) waits cover both)
@@ -1374,8 +1379,12 @@ __device__ __forceinline__ void con_tile(
           for (int r2 = 0; r2 < 2; ++r2)
 #pragma unroll
             for (int fn = 0; fn < 4; ++fn)
+#ifndef SGP_CON_PROBE_NO_EPI_MFMA
               P[fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[fm][fn][2 * h + r2], xb[r2], P[fn],
                                                            0, 0, 0);
+#else   // timing probe (wrong results): a VALU stand-in for the D products
+              P[fn][r2] = fma(acc[fm][fn][2 * h + r2], xb[r2], P[fn][r2]);
+#endif
           if (hs == 1) SGP_PROBE_CON_STAMP(3);
         }
         __syncthreads();                        // everyone is done reading the last stage
@@ -1473,6 +1482,7 @@ __device__ __forceinline__ void con_tile(
       slab[tid * nwg + wgid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
     SGP_PROBE_CON_STAMP(2);
   }
+  if constexpr (SGP_CON_EPI_PRIO > 0) __builtin_amdgcn_s_setprio(0);
 }
 
 // one 128 x 128 output tile per workgroup (grid = tiles), XCD-aware tile order

@@ -7,6 +7,8 @@
 //
 //   SGP_CON_TRACE(k)       s_memtime stamp k of a k_contract workgroup   (tools/micro/con_trace.hip)
 //   SGP_CON_NO_EPILOGUE    k_contract<.., EPI_GRAD> returns after the k-loop (timing only)
+//   SGP_CON_PROBE_NO_EPI_MFMA  the epilogue's D products on the VALU, wrong (timing only)
+//   SGP_CON_PROBE_NO_KDMA  the epilogue's K stages not loaded (timing only)
 //   SGP_GJ_TRACE(k, p)     stamp p of the GJ look-ahead workgroup at pivot k (tools/micro/gj_trace.hip)
 //
 // Experiment knobs (schedule / staging alternatives measured in A/B runs).  The product values
@@ -31,6 +33,7 @@
 //   SGP_VI_BUILD_NO_T   1: VI's builder without t (wrong results: builder timing only)
 //   SGP_GJ_STEPS        1: the m x m inverses as one launch per pivot step (before round 5)
 //   SGP_GJ_GMAX         workgroups of a persistent Gauss-Jordan chain (at most)
+//   SGP_CON_EPI_PRIO    contraction: wave priority (s_setprio) of the epilogue (0: none)
 //   SGP_BUILD_OCC_T2    workgroups per CU of the with-t K12 builder at d <= 8 (launch bound)
 //   SGP_CHAIN_US_STEP   chain_shared_rb's model of a K22 chain beside the builder: us per
 //   SGP_CHAIN_US_FIX    64-wide step, and fixed us
@@ -48,11 +51,16 @@
      defined(SGP_SYRK_W3) || defined(SGP_CON_ROWQ_KU) ||                                      \
      defined(SGP_LAP_RS_CFG) || defined(SGP_GJ_MM_UNROLL) || defined(SGP_VI_BUILD_NO_T) ||        \
      defined(SGP_GJ_STEPS) || defined(SGP_GJ_GMAX) || defined(SGP_CHAIN_US_STEP) ||         \
-     defined(SGP_CHAIN_US_FIX) || defined(SGP_HOST_PROBE) || defined(SGP_BUILD_OCC_T2)) &&      \
+     defined(SGP_CHAIN_US_FIX) || defined(SGP_HOST_PROBE) || defined(SGP_BUILD_OCC_T2) ||      \
+     defined(SGP_CON_EPI_PRIO) || defined(SGP_CON_PROBE_NO_EPI_MFMA) ||                       \
+     defined(SGP_CON_PROBE_NO_KDMA)) &&      \
     !defined(SGP_PROBE_BUILD)
 #error "timing probes and experiment knobs are for variant builds only (SGP_PROBE_BUILD)"
 #endif
 
+#ifndef SGP_CON_EPI_PRIO
+#define SGP_CON_EPI_PRIO 0
+#endif
 #ifndef SGP_BUILD_OCC_T2
 #define SGP_BUILD_OCC_T2 4
 #endif

@@ -21,6 +21,48 @@ __device__ unsigned long long* g_trace;
   } while (0)
 #include "../../sparsergps_amd/csrc/k_mfma.hip"
 
+// medians of the per-workgroup phases of the last launch (s_memtime ticks: shader clock)
+static void report(const char* tag, const unsigned long long* tr, int64_t nwg, int64_t n,
+                   int64_t m, const char* csv) {
+  std::vector<unsigned long long> ht(nwg * 8);
+  hipMemcpy(ht.data(), tr, ht.size() * 8, hipMemcpyDeviceToHost);
+  if (csv) {
+    FILE* f = fopen(csv, "w");
+    fprintf(f, "wg,t0,t1,t4,t3,t5,t6,t2,hwid,xcc\n");
+    for (int64_t w = 0; w < nwg; ++w) {
+      const unsigned long long* t = &ht[w * 8];
+      fprintf(f, "%lld,%llu,%llu,%llu,%llu,%llu,%llu,%llu,%llu,%llu\n", (long long)w, t[0], t[1],
+              t[4], t[3], t[5], t[6], t[2], t[7] & 0xffffffffull, t[7] >> 32);
+    }
+    fclose(f);
+  }
+  std::vector<double> kl, ep;
+  for (int64_t w = 0; w < nwg; ++w) {
+    const unsigned long long* t = &ht[w * 8];
+    kl.push_back((double)(t[1] - t[0]));
+    ep.push_back((double)(t[2] - t[1]));
+  }
+  std::sort(kl.begin(), kl.end());
+  std::sort(ep.begin(), ep.end());
+  // epilogue phases: 1 -> 4 setup (alpha, u / cdiag, first K stages, coordinate staging, wait),
+  // 4 -> 5 the eight K half-stages (W and its MFMA products), 5 -> 6 column sums / E /
+  // records into LDS, 6 -> 2 the record reduction and store
+  const int idx[5] = {1, 4, 5, 6, 2};
+  for (int p = 0; p < 4; ++p) {
+    std::vector<double> ph;
+    for (int64_t w = 0; w < nwg; ++w) {
+      const unsigned long long* t = &ht[w * 8];
+      ph.push_back((double)(t[idx[p + 1]] - t[idx[p]]));
+    }
+    std::sort(ph.begin(), ph.end());
+    printf("  [%s] epilogue phase t%d->t%d: median %.0f ticks\n", tag, idx[p], idx[p + 1],
+           ph[ph.size() / 2]);
+  }
+  printf("[%s] n=%lld m=%lld nwg=%lld  median k-loop %.0f ticks (%.0f per k-step), epilogue %.0f "
+         "ticks\n", tag, (long long)n, (long long)m, (long long)nwg, kl[kl.size() / 2],
+         kl[kl.size() / 2] / (double)(m / 16), ep[ep.size() / 2]);
+}
+
 int main(int argc, char** argv) {
   const int64_t n = argc > 3 ? atoll(argv[2]) : 131072, n_pad = (n + 127) / 128 * 128;
   const int64_t m = argc > 3 ? atoll(argv[3]) : 1024, mp = (m + 127) / 128 * 128;
@@ -70,6 +112,7 @@ int main(int argc, char** argv) {
     float ms; hipEventElapsedTime(&ms, e0, e1);
     printf("1 WG/CU run %d: %.3f ms  %.2f TF/s\n", it, ms, 2.0 * n * m * m / (ms * 1e-3) / 1e12);
   }
+  report("1 WG/CU", tr, nwg, n, m, nullptr);
   for (int it = 0; it < 3; ++it) {
     hipEventRecord(e0, 0);
     launch_contract_args(kp, K, M, X, n_pad, n, n_pad, Uu, mp, m, mp, ca, slab, &nrec, &nw, 0);
@@ -78,42 +121,6 @@ int main(int argc, char** argv) {
     float ms; hipEventElapsedTime(&ms, e0, e1);
     printf("run %d: %.3f ms  %.2f TF/s\n", it, ms, 2.0 * n * m * m / (ms * 1e-3) / 1e12);
   }
-  std::vector<unsigned long long> ht(nwg * 8);
-  hipMemcpy(ht.data(), tr, ht.size() * 8, hipMemcpyDeviceToHost);
-  FILE* f = fopen(argc > 1 ? argv[1] : "con_trace.csv", "w");
-  fprintf(f, "wg,t0,t1,t4,t3,t5,t6,t2,hwid,xcc\n");
-  for (int64_t w = 0; w < nwg; ++w) {
-    const unsigned long long* t = &ht[w * 8];
-    fprintf(f, "%lld,%llu,%llu,%llu,%llu,%llu,%llu,%llu,%llu,%llu\n", (long long)w, t[0], t[1], t[4],
-            t[3], t[5], t[6], t[2], t[7] & 0xffffffffull, t[7] >> 32);
-  }
-  fclose(f);
-  // per-workgroup phases (s_memtime ticks: shader clock): k-loop = t1 - t0, epilogue = t2 - t1
-  std::vector<double> kl, ep;
-  unsigned long long tmin = ~0ull, tmax = 0;
-  for (int64_t w = 0; w < nwg; ++w) {
-    const unsigned long long* t = &ht[w * 8];
-    kl.push_back((double)(t[1] - t[0]));
-    ep.push_back((double)(t[2] - t[1]));
-    tmin = std::min(tmin, t[0]);
-    tmax = std::max(tmax, t[2]);
-  }
-  std::sort(kl.begin(), kl.end());
-  std::sort(ep.begin(), ep.end());
-  // epilogue phases: 1 -> 4 setup (alpha, u / cdiag, first K stages, coordinate staging, wait),
-  // 4 -> 5 the eight K half-stages (W and its MFMA products), 5 -> 6 column sums / E /
-  // records into LDS, 6 -> 2 the record reduction and store
-  const int idx[5] = {1, 4, 5, 6, 2};
-  for (int p = 0; p < 4; ++p) {
-    std::vector<double> ph;
-    for (int64_t w = 0; w < nwg; ++w) {
-      const unsigned long long* t = &ht[w * 8];
-      ph.push_back((double)(t[idx[p + 1]] - t[idx[p]]));
-    }
-    std::sort(ph.begin(), ph.end());
-    printf("  epilogue phase t%d->t%d: median %.0f ticks\n", idx[p], idx[p + 1], ph[ph.size() / 2]);
-  }
-  printf("n=%lld m=%lld nwg=%lld  median k-loop %.0f ticks, epilogue %.0f ticks, span %llu ticks\n",
-         (long long)n, (long long)m, (long long)nwg, kl[kl.size() / 2], ep[ep.size() / 2], tmax - tmin);
+  report("2 WG/CU", tr, nwg, n, m, argc > 1 ? argv[1] : "con_trace.csv");
   return 0;
 }
