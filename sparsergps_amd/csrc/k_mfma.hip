@@ -1174,10 +1174,13 @@ __device__ __forceinline__ void con_tile(
     const double iz = ca.invz_vec ? ca.invz_vec[i] : ca.invz;
     const double al = ca.alpha_in ? ca.alpha_in[i]
                                   : (with_u ? (r[i] - ku) * iz : 0.0);   // padded rows -> 0
-    s_alpha[arow] = al;
-    s_rs[arow] = ca.rs_vec ? ca.rs * ca.rs_vec[i] : ca.rs;
-    if constexpr (T2) s_rs2[arow] = ca.rs_vec2 ? ca.rs2 * ca.rs_vec2[i] : ca.rs2;
-    s_beta[arow] = with_v ? ca.beta_in[i] : 0.0;
+    // rows past n: every row factor 0, so G = 0 there and the epilogue needs no validity mask
+    // (K12 is exactly 0 in the padded columns j >= m, and T = K M is finite: W = G o K = 0)
+    const bool iv = i < n;
+    s_alpha[arow] = iv ? al : 0.0;
+    s_rs[arow] = iv ? (ca.rs_vec ? ca.rs * ca.rs_vec[i] : ca.rs) : 0.0;
+    if constexpr (T2) s_rs2[arow] = iv ? (ca.rs_vec2 ? ca.rs2 * ca.rs_vec2[i] : ca.rs2) : 0.0;
+    s_beta[arow] = (with_v && iv) ? ca.beta_in[i] : 0.0;
     if (tj == 0) {
       if (ca.count_a2 && i < n) a2 = al * al;
       if (ca.alpha_out) ca.alpha_out[i] = al;
@@ -1323,13 +1326,11 @@ __device__ __forceinline__ void con_tile(
 
       d4 P[4];
       double Cc[4], ucol[4], vcol[4];
-      bool cval[4];
 #pragma unroll
       for (int fn = 0; fn < 4; ++fn) {
         const int col = wc * 64 + fn * 16 + (lane & 15);
         P[fn] = d4{0.0, 0.0, 0.0, 0.0};
         Cc[fn] = 0.0;
-        cval[fn] = (j0 + col) < m;
         ucol[fn] = s_u[col];
         vcol[fn] = with_v ? s_v[col] : 0.0;
       }
@@ -1365,12 +1366,19 @@ __device__ __forceinline__ void con_tile(
             for (int r2 = 0; r2 < 2; ++r2) {
               const int q = 2 * h + r2;
               const int row = wr * 64 + fm * 16 + (lane >> 4) + 4 * q;
-              const bool valid = cval[fn] && ((i0 + row) < n);
               double G = s_rs[row] * acc[fm][fn][q];
               if constexpr (T2) G = fma(s_rs2[row], t2c[r2][fn], G);
               if constexpr (V2) G = fma(s_beta[row], vcol[fn], G);
               G = fma(s_alpha[row], ucol[fn], G);
-              const double w = valid ? G * kv[r2] : 0.0;
+              // no validity mask: padded rows have G = 0 and padded columns K = 0.  (The former
+              // `valid ? G * kv : 0` became a branch per element around its LDS reads -- an
+              // exposed LDS round trip and an exec-mask block each -- and every VALU cycle here
+              // is taken from the co-resident workgroup's MFMA stream)
+              double w = G * kv[r2];
+              // the passes over stored products (FROM_T: FITC's / Laplace's one-pass gradient)
+              // keep the select (measured 5 % slower without it) and so does Laplace with knot
+              // gradients (without it its 256 VGPRs spill)
+              if constexpr ((V2 && KNOT) || FROM_T) w = (j0 + col < m && i0 + row < n) ? w : 0.0;
               Cc[fn] += w;
               acc[fm][fn][q] = w;
             }
