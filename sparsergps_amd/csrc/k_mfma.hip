@@ -1265,6 +1265,11 @@ __device__ __forceinline__ void con_tile(
       // rides on the pass that forms W; each further chunk restages [x~ | x~^2] and u~ and adds
       // one 16-column MFMA product over the W kept in the accumulators.
       constexpr int KST = 136;                  // stage row stride (doubles)
+      // this lane's source in the first stage row of its wave (row (wv >> 1) 64 + 4 (wv & 1)
+      // + q of a stage; stage s adds 16 (s >> 1) + 8 (s & 1) rows): every stage address is this
+      // pointer plus a wave-uniform row offset times mp -- one 64-bit add per DMA instead of a
+      // 64-bit multiply-add chain (the co-resident k-loop pays for every VALU cycle here)
+      const double* const kq0 = K + (i0 + (wv >> 1) * 64 + 4 * (wv & 1)) * mp + j0 + 2 * lane;
       double* kst = s_us + ((T128 * sus + 1) & ~1);   // 2 x 16 x KST, 16-byte aligned
       // chunk ch of the coordinates: s_xs = [x~ | x~^2] (128 x 16), s_us = u~ (128 x sus)
 #define CON_XSTAGE(ch_)                                                                  \
@@ -1294,10 +1299,9 @@ __device__ __forceinline__ void con_tile(
 #define CON_KHALF(s_)                                                                    \
       _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_) {                                 \
         const int rho_ = wv * 4 + q_;                                                    \
-        const int64_t row_ = i0 + (rho_ >> 3) * 64 + ((s_) >> 1) * 16 + ((s_) & 1) * 8 + \
-                             (rho_ & 7);                                                 \
         __builtin_amdgcn_global_load_lds(                                                \
-            (const __attribute__((address_space(1))) void*)(K + row_ * mp + j0 + 2 * lane), \
+            (const __attribute__((address_space(1))) void*)(                             \
+                kq0 + (int64_t)(((s_) >> 1) * 16 + ((s_) & 1) * 8 + q_) * mp),          \
             (__attribute__((address_space(3))) void*)(kst + ((s_) & 1) * 16 * KST + rho_ * KST), \
             16, 0, 0);                                                                   \
       }
