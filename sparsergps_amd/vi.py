@@ -147,21 +147,34 @@ class SparseGPContext:
     _EVAL_PROTO = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int64,
                               C.c_int64, C.c_double, C.c_uint, C.c_void_p, C.c_void_p)
 
+    def _fast_buf(self, key, shape, order="C"):
+        # a host buffer kept for the context's lifetime with its address: `arr.ctypes.data` costs
+        # ~1.5 us per array and call, and the one-call evaluation passes three of them
+        bufs = self.__dict__.setdefault("_fast_bufs", {})
+        b = bufs.get(key)
+        if b is None or b[0].shape != shape:
+            arr = np.zeros(shape, dtype=np.float64, order=order)
+            b = bufs[key] = (arr, arr.ctypes.data)
+        return b
+
     def _eval_fast(self, name, theta, cov_fun, xu, delta, r_det, obj_only):
         fns = self.__dict__.setdefault("_fast_fns", {})
         fn = fns.get(name)
         if fn is None:
             fn = fns[name] = self._EVAL_PROTO(C.cast(getattr(self._lib, name), C.c_void_p).value)
-        theta = np.ascontiguousarray(theta, dtype=np.float64)
-        if theta.ndim != 1:
-            theta = theta.reshape(-1)
-        U, m = self._knots(xu)
-        out = np.zeros(theta.size + 1, dtype=np.float64)   # [objective, gradient]
-        a = out.ctypes.data
-        st = fn(self.handle.value, _lib.KERNELS[cov_fun], theta.ctypes.data, U.ctypes.data, m, m,
-                float(delta), self._flags(r_det, obj_only), a, None if obj_only else a + 8)
+        theta = np.asarray(theta, dtype=np.float64).reshape(-1)
+        th, th_p = self._fast_buf("theta", theta.shape)
+        th[...] = theta
+        xu = np.asarray(xu, dtype=np.float64)
+        m = xu.size // self.d
+        U, U_p = self._fast_buf("U", (m, self.d), "F")
+        U[...] = xu.reshape(m, self.d)   # (copied every call: the caller may move its knots)
+        self._last_m = m
+        out, a = self._fast_buf("out", (theta.size + 1,))   # [objective, gradient]
+        st = fn(self.handle.value, _lib.KERNELS[cov_fun], th_p, U_p, m, m, float(delta),
+                self._flags(r_det, obj_only), a, None if obj_only else a + 8)
         _lib.check(st)
-        return float(out[0]), (None if obj_only else out[1:])
+        return float(out[0]), (None if obj_only else out[1:].copy())
 
     def eval_vi(self, theta, cov_fun, xu, delta=1e-6, r_det=False, obj_only=False):
         """ELBO and d ELBO / d log(theta) with theta in [sigma, l.., tau] layout
